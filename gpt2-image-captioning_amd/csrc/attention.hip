@@ -1,0 +1,323 @@
+// Multi-head softmax attention for the short sequences of the captioning path
+// (GPT-2 S=65 causal+padding, CLIP S=50, mapper S=25 with head_dim 96).
+//
+// One workgroup per (batch, head): Q, K, V (and dO in backward) are staged once
+// from HBM into LDS as fp32 (rows padded to hd+1 floats so column walks are
+// bank-conflict free), the S x S score block lives in LDS, softmax row
+// reductions use wave shuffles, and P.V / dS.K / dS^T.Q / P^T.dO are LDS dot
+// products. At these sizes the attention core is ~1 % of the step FLOPs
+// (0.156 of 11.2 GF/sample); the kernel is bound by its
+// QKV/out HBM traffic, so it is written for coalesced loads, not for MFMA.
+#include "common.h"
+
+#include <math.h>
+
+namespace icap {
+
+struct AttnGeom {
+  int S, H, hd, D;
+  int64_t rsb, rss;  // row strides (in rows) for batch and sequence
+};
+
+__device__ __forceinline__ int64_t tok_row(const AttnGeom& g, int b, int s) { return (int64_t)b * g.rsb + (int64_t)s * g.rss; }
+
+template <typename T>
+__device__ __forceinline__ void stage_head(const T* src, int64_t ld, int col0, const AttnGeom& g, int b,
+                                           float* dst, int dld, float mul) {
+  const int nv = g.hd >> 2;  // float4 groups per row (hd % 4 == 0)
+  for (int idx = threadIdx.x; idx < g.S * nv; idx += blockDim.x) {
+    const int s = idx / nv, c = idx - s * nv;
+    float v[4];
+    io<T>::ld4(src + tok_row(g, b, s) * ld + col0 + 4 * c, v);
+    float* d = dst + s * dld + 4 * c;
+    d[0] = v[0] * mul; d[1] = v[1] * mul; d[2] = v[2] * mul; d[3] = v[3] * mul;
+  }
+}
+
+__device__ __forceinline__ bool allowed(int causal, const int32_t* key_mask, int b, int S, int i, int j) {
+  if (causal && j > i) return false;
+  if (key_mask && key_mask[(int64_t)b * S + j] == 0) return false;
+  return true;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeom g, uint32_t thr, float inv_keep) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int bh = blockIdx.x;
+  const int b = bh / g.H, h = bh - b * g.H;
+  const int S = g.S, hd = g.hd, ldp = hd + 1;
+  float* Qs = sm;
+  float* Ks = Qs + S * ldp;
+  float* Vs = Ks + S * ldp;
+  float* P = Vs + S * ldp;
+  const T* qkv = reinterpret_cast<const T*>(p.qkv);
+  stage_head<T>(qkv, p.ld_qkv, h * hd, g, b, Qs, ldp, p.scale);
+  stage_head<T>(qkv, p.ld_qkv, g.D + h * hd, g, b, Ks, ldp, 1.f);
+  stage_head<T>(qkv, p.ld_qkv, 2 * g.D + h * hd, g, b, Vs, ldp, 1.f);
+  __syncthreads();
+
+  for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
+    const int i = idx / S, j = idx - i * S;
+    float s = -INFINITY;
+    if (allowed(p.causal, p.key_mask, b, S, i, j)) {
+      const float* q = Qs + i * ldp;
+      const float* k = Ks + j * ldp;
+      float a0 = 0.f, a1 = 0.f;
+      for (int d = 0; d < hd; d += 2) {
+        a0 = fmaf(q[d], k[d], a0);
+        a1 = fmaf(q[d + 1], k[d + 1], a1);
+      }
+      s = a0 + a1;
+    }
+    P[idx] = s;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  const uint64_t drop_base = p.offset + (uint64_t)bh * S * S;
+  const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
+  for (int i = wv; i < S; i += nwv) {
+    float* row = P + i * S;
+    float m = -INFINITY;
+    for (int j = lane; j < S; j += 64) m = fmaxf(m, row[j]);
+    m = wave_max(m);
+    float l = 0.f;
+    for (int j = lane; j < S; j += 64) l += (m == -INFINITY) ? 0.f : __expf(row[j] - m);
+    l = wave_sum(l);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    for (int j = lane; j < S; j += 64) {
+      float pv = (m == -INFINITY) ? 0.f : __expf(row[j] - m) * inv;
+      if (thr) pv *= drop_scale(seed, drop_base + (uint64_t)i * S + j, thr, inv_keep);
+      row[j] = pv;
+    }
+    if (lane == 0 && p.lse) p.lse[(int64_t)bh * S + i] = (l > 0.f) ? m + logf(l) : -INFINITY;
+  }
+  __syncthreads();
+
+  T* out = reinterpret_cast<T*>(p.out);
+  for (int idx = threadIdx.x; idx < S * hd; idx += blockDim.x) {
+    const int i = idx / hd, d = idx - i * hd;
+    const float* row = P + i * S;
+    float a0 = 0.f, a1 = 0.f;
+    int j = 0;
+    for (; j + 1 < S; j += 2) {
+      a0 = fmaf(row[j], Vs[j * ldp + d], a0);
+      a1 = fmaf(row[j + 1], Vs[(j + 1) * ldp + d], a1);
+    }
+    if (j < S) a0 = fmaf(row[j], Vs[j * ldp + d], a0);
+    io<T>::st(out + tok_row(g, b, i) * p.ld_out + h * hd + d, a0 + a1);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(icap_attn_args p, AttnGeom g, uint32_t thr, float inv_keep) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int bh = blockIdx.x;
+  const int b = bh / g.H, h = bh - b * g.H;
+  const int S = g.S, hd = g.hd, ldp = hd + 1;
+  float* Qs = sm;
+  float* Ks = Qs + S * ldp;
+  float* Vs = Ks + S * ldp;
+  float* dOs = Vs + S * ldp;
+  float* P = dOs + S * ldp;   // P, then dropped P
+  float* dS = P + S * S;      // dPd, then dS
+  const T* qkv = reinterpret_cast<const T*>(p.qkv);
+  stage_head<T>(qkv, p.ld_qkv, h * hd, g, b, Qs, ldp, p.scale);
+  stage_head<T>(qkv, p.ld_qkv, g.D + h * hd, g, b, Ks, ldp, 1.f);
+  stage_head<T>(qkv, p.ld_qkv, 2 * g.D + h * hd, g, b, Vs, ldp, 1.f);
+  stage_head<T>(reinterpret_cast<const T*>(p.dout), p.ld_dout, h * hd, g, b, dOs, ldp, 1.f);
+  __syncthreads();
+
+  for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
+    const int i = idx / S, j = idx - i * S;
+    float pv = 0.f, dp = 0.f;
+    const float lse = p.lse[(int64_t)bh * S + i];
+    if (allowed(p.causal, p.key_mask, b, S, i, j) && lse != -INFINITY) {
+      const float* q = Qs + i * ldp;
+      const float* k = Ks + j * ldp;
+      const float* o = dOs + i * ldp;
+      const float* v = Vs + j * ldp;
+      float a0 = 0.f, a1 = 0.f, c0 = 0.f, c1 = 0.f;
+      for (int d = 0; d < hd; d += 2) {
+        a0 = fmaf(q[d], k[d], a0);
+        a1 = fmaf(q[d + 1], k[d + 1], a1);
+        c0 = fmaf(o[d], v[d], c0);
+        c1 = fmaf(o[d + 1], v[d + 1], c1);
+      }
+      pv = __expf(a0 + a1 - lse);
+      dp = c0 + c1;
+    }
+    P[idx] = pv;
+    dS[idx] = dp;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  const uint64_t drop_base = p.offset + (uint64_t)bh * S * S;
+  const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
+  for (int i = wv; i < S; i += nwv) {
+    float* prow = P + i * S;
+    float* drow = dS + i * S;
+    float delta = 0.f;
+    for (int j = lane; j < S; j += 64) {
+      float dp = drow[j];
+      if (thr) dp *= drop_scale(seed, drop_base + (uint64_t)i * S + j, thr, inv_keep);
+      drow[j] = dp;
+      delta += prow[j] * dp;
+    }
+    delta = wave_sum(delta);
+    for (int j = lane; j < S; j += 64) {
+      const float pv = prow[j];
+      drow[j] = pv * (drow[j] - delta);
+      if (thr) prow[j] = pv * drop_scale(seed, drop_base + (uint64_t)i * S + j, thr, inv_keep);
+    }
+  }
+  __syncthreads();
+
+  T* dqkv = reinterpret_cast<T*>(p.dqkv);
+  for (int idx = threadIdx.x; idx < S * hd; idx += blockDim.x) {
+    const int i = idx / hd, d = idx - i * hd;  // i: query row for dQ, key row for dK/dV
+    float aq = 0.f, ak = 0.f, av = 0.f;
+    for (int j = 0; j < S; ++j) {
+      aq = fmaf(dS[i * S + j], Ks[j * ldp + d], aq);   // dQ_i = sum_j dS_ij K_j
+      ak = fmaf(dS[j * S + i], Qs[j * ldp + d], ak);   // dK_i = sum_j dS_ji Qs_j
+      av = fmaf(P[j * S + i], dOs[j * ldp + d], av);   // dV_i = sum_j Pd_ji dO_j
+    }
+    T* rowp = dqkv + tok_row(g, b, i) * p.ld_dqkv;
+    io<T>::st(rowp + h * hd + d, aq * p.scale);
+    io<T>::st(rowp + g.D + h * hd + d, ak);
+    io<T>::st(rowp + 2 * g.D + h * hd + d, av);
+  }
+}
+
+// one wave per (b, h); keys 0..pos from the position-major cache
+template <typename T>
+__global__ __launch_bounds__(64) void attn_decode_kernel(int B, int H, int hd, int pos, const T* __restrict__ cache,
+                                                        int64_t ld, T* __restrict__ out, int64_t ld_out,
+                                                        float scale) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* q = sm;            // hd
+  float* sc = sm + 128;     // pos+1 scores
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - b * H;
+  const int D = H * hd;
+  const int lane = threadIdx.x;
+  const int n = pos + 1;
+  const T* qrow = cache + ((int64_t)pos * B + b) * ld + h * hd;
+  for (int d = lane; d < hd; d += 64) q[d] = io<T>::ld(qrow + d) * scale;
+  __syncthreads();
+  float m = -INFINITY;
+  for (int j = lane; j < n; j += 64) {
+    const T* krow = cache + ((int64_t)j * B + b) * ld + D + h * hd;
+    float a = 0.f;
+    for (int d = 0; d < hd; d += 4) {
+      float kv[4];
+      io<T>::ld4(krow + d, kv);
+      a = fmaf(q[d], kv[0], a);
+      a = fmaf(q[d + 1], kv[1], a);
+      a = fmaf(q[d + 2], kv[2], a);
+      a = fmaf(q[d + 3], kv[3], a);
+    }
+    sc[j] = a;
+    m = fmaxf(m, a);
+  }
+  m = wave_max(m);
+  float l = 0.f;
+  for (int j = lane; j < n; j += 64) {
+    const float e = __expf(sc[j] - m);
+    sc[j] = e;
+    l += e;
+  }
+  l = wave_sum(l);
+  __syncthreads();
+  const float inv = 1.f / l;
+  for (int d = lane; d < hd; d += 64) {
+    float a = 0.f;
+    for (int j = 0; j < n; ++j) a = fmaf(sc[j], io<T>::ld(cache + ((int64_t)j * B + b) * ld + 2 * D + h * hd + d), a);
+    io<T>::st(out + (int64_t)b * ld_out + h * hd + d, a * inv);
+  }
+}
+
+static size_t fwd_lds(int S, int hd) { return sizeof(float) * ((size_t)3 * S * (hd + 1) + (size_t)S * S); }
+static size_t bwd_lds(int S, int hd) { return sizeof(float) * ((size_t)4 * S * (hd + 1) + (size_t)2 * S * S); }
+constexpr size_t LDS_CAP = 160 * 1024;
+
+template <typename K>
+static void raise_lds_limit(K kernel) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+}
+
+static int check_attn(const icap_attn_args* a, bool bwd) {
+  ICAP_REQUIRE(a != nullptr, "icap_attention: null args");
+  ICAP_REQUIRE(a->dtype == ICAP_F32 || a->dtype == ICAP_BF16, "icap_attention: bad dtype");
+  ICAP_REQUIRE(a->B >= 0 && a->S > 0 && a->H > 0 && a->hd > 0 && a->hd % 4 == 0, "icap_attention: bad geometry (hd % 4 == 0)");
+  ICAP_REQUIRE(a->qkv && (bwd ? (a->dout && a->dqkv && a->lse) : (a->out != nullptr)), "icap_attention: null pointer");
+  ICAP_REQUIRE(a->ld_qkv % 4 == 0, "icap_attention: ld_qkv must be a multiple of 4");
+  ICAP_REQUIRE(a->drop_p >= 0.f && a->drop_p < 1.f, "icap_attention: drop_p out of range");
+  const size_t need = bwd ? bwd_lds(a->S, a->hd) : fwd_lds(a->S, a->hd);
+  ICAP_REQUIRE(need <= LDS_CAP, "icap_attention: sequence/head too large for the LDS-resident kernel");
+  return ICAP_OK;
+}
+
+}  // namespace icap
+
+using namespace icap;
+
+extern "C" int icap_attention_fwd(const icap_attn_args* a, void* stream) {
+  int rc = check_attn(a, false);
+  if (rc) return rc;
+  if (a->B == 0) return ICAP_OK;
+  AttnGeom g{a->S, a->H, a->hd, a->H * a->hd, a->row_stride_b, a->row_stride_s};
+  const uint32_t thr = a->drop_p > 0.f ? drop_threshold(a->drop_p) : 0u;
+  const float inv_keep = a->drop_p > 0.f ? 1.f / (1.f - a->drop_p) : 1.f;
+  const size_t lds = fwd_lds(a->S, a->hd);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((unsigned)(a->B * a->H)), block(256);
+  if (a->dtype == ICAP_BF16) {
+    static bool once = (raise_lds_limit(attn_fwd_kernel<bf16_t>), true); (void)once;
+    hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, grid, block, lds, s, *a, g, thr, inv_keep);
+  } else {
+    static bool once = (raise_lds_limit(attn_fwd_kernel<float>), true); (void)once;
+    hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, block, lds, s, *a, g, thr, inv_keep);
+  }
+  return check_launch("icap_attention_fwd");
+}
+
+extern "C" int icap_attention_bwd(const icap_attn_args* a, void* stream) {
+  int rc = check_attn(a, true);
+  if (rc) return rc;
+  if (a->B == 0) return ICAP_OK;
+  AttnGeom g{a->S, a->H, a->hd, a->H * a->hd, a->row_stride_b, a->row_stride_s};
+  const uint32_t thr = a->drop_p > 0.f ? drop_threshold(a->drop_p) : 0u;
+  const float inv_keep = a->drop_p > 0.f ? 1.f / (1.f - a->drop_p) : 1.f;
+  const size_t lds = bwd_lds(a->S, a->hd);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((unsigned)(a->B * a->H)), block(256);
+  if (a->dtype == ICAP_BF16) {
+    static bool once = (raise_lds_limit(attn_bwd_kernel<bf16_t>), true); (void)once;
+    hipLaunchKernelGGL(attn_bwd_kernel<bf16_t>, grid, block, lds, s, *a, g, thr, inv_keep);
+  } else {
+    static bool once = (raise_lds_limit(attn_bwd_kernel<float>), true); (void)once;
+    hipLaunchKernelGGL(attn_bwd_kernel<float>, grid, block, lds, s, *a, g, thr, inv_keep);
+  }
+  return check_launch("icap_attention_bwd");
+}
+
+extern "C" int icap_attention_decode(int32_t dtype, int32_t B, int32_t H, int32_t hd, int32_t pos,
+                                     const void* cache, int64_t ld_cache, void* out, int64_t ld_out,
+                                     float scale, void* stream) {
+  ICAP_REQUIRE(hd > 0 && hd <= 128 && hd % 4 == 0, "icap_attention_decode: hd must be <= 128, multiple of 4");
+  ICAP_REQUIRE(pos >= 0 && pos < 4096, "icap_attention_decode: pos out of range");
+  ICAP_REQUIRE(cache && out, "icap_attention_decode: null pointer");
+  if (B == 0) return ICAP_OK;
+  const size_t lds = sizeof(float) * (128 + (size_t)pos + 1);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((unsigned)(B * H)), block(64);
+  if (dtype == ICAP_BF16)
+    hipLaunchKernelGGL(attn_decode_kernel<bf16_t>, grid, block, lds, s, B, H, hd, pos, (const bf16_t*)cache, ld_cache,
+                       (bf16_t*)out, ld_out, scale);
+  else
+    hipLaunchKernelGGL(attn_decode_kernel<float>, grid, block, lds, s, B, H, hd, pos, (const float*)cache, ld_cache,
+                       (float*)out, ld_out, scale);
+  return check_launch("icap_attention_decode");
+}

@@ -1,0 +1,145 @@
+// Shared device helpers for the icap HIP library (gfx950 / CDNA4 only).
+//
+// Storage types: activations/weights are either fp32 or bf16 (raw 16-bit words);
+// every kernel computes in fp32. Wave size is 64 (hard-coded, see
+// /opt/skills/guides/cdna_hip_programming.md §1).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "icap.h"
+
+namespace icap {
+
+typedef uint16_t bf16_t;
+
+// ---- error reporting (thread-local, C-ABI icap_last_error) -------------------
+void set_error(const std::string& msg);
+int check_launch(const char* what);
+
+#define ICAP_REQUIRE(cond, msg)                 \
+  do {                                          \
+    if (!(cond)) {                              \
+      ::icap::set_error(std::string(msg));      \
+      return ICAP_ERR_ARG;                      \
+    }                                           \
+  } while (0)
+
+// ---- bf16 <-> f32 ------------------------------------------------------------
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+// round-to-nearest-even; NaN stays NaN (quiet bit forced)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+template <typename T> struct io;
+template <> struct io<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+  // 4 consecutive elements
+  static __device__ __forceinline__ void ld4(const float* p, float v[4]) {
+    float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  static __device__ __forceinline__ void st4(float* p, const float v[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct io<bf16_t> {
+  static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void st(bf16_t* p, float v) { *p = f2bf(v); }
+  static __device__ __forceinline__ void ld4(const bf16_t* p, float v[4]) {
+    uint2 t = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+    v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+  }
+  static __device__ __forceinline__ void st4(bf16_t* p, const float v[4]) {
+    uint2 t;
+    t.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    t.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = t;
+  }
+};
+
+// ---- wave reductions (64 lanes) ---------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- counter-based dropout RNG (splitmix64 finaliser) ------------------------
+// keep(idx) is a pure function of (seed, idx): forward and backward regenerate
+// the same mask without storing it.
+__device__ __forceinline__ uint32_t hash32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+__device__ __forceinline__ uint64_t eff_seed(uint64_t seed, const uint64_t* ptr) {
+  return ptr ? seed + (*ptr) * 0x9E3779B97F4A7C15ull : seed;
+}
+// returns 0 or 1/(1-p)
+__device__ __forceinline__ float drop_scale(uint64_t seed, uint64_t idx, uint32_t thresh, float inv_keep) {
+  return hash32(seed, idx) >= thresh ? inv_keep : 0.f;
+}
+inline uint32_t drop_threshold(float p) {
+  double t = (double)p * 4294967296.0;
+  if (t >= 4294967295.0) t = 4294967295.0;
+  if (t < 0) t = 0;
+  return (uint32_t)t;
+}
+
+// ---- activations -------------------------------------------------------------
+__device__ __forceinline__ float act_fwd(int act, float x) {
+  switch (act) {
+    case ICAP_ACT_GELU_NEW: {
+      // HF activations.py NewGELUActivation: 0.5x(1+tanh(sqrt(2/pi)(x+0.044715x^3)))
+      const float c = 0.7978845608028654f;
+      return 0.5f * x * (1.f + tanhf(c * (x + 0.044715f * x * x * x)));
+    }
+    case ICAP_ACT_RELU: return x > 0.f ? x : 0.f;
+    case ICAP_ACT_QUICK_GELU: return x / (1.f + __expf(-1.702f * x));
+    case ICAP_ACT_TANH: return tanhf(x);
+    default: return x;
+  }
+}
+// derivative; `a` is the value stored by the forward as aux:
+//   gelu_new / quick_gelu: pre-activation z;  relu: z or relu(z);  tanh: tanh(z)
+__device__ __forceinline__ float act_bwd(int act, float a) {
+  switch (act) {
+    case ICAP_ACT_GELU_NEW: {
+      const float c = 0.7978845608028654f;
+      float x2 = a * a;
+      float u = c * (a + 0.044715f * x2 * a);
+      float t = tanhf(u);
+      float du = c * (1.f + 3.f * 0.044715f * x2);
+      return 0.5f * (1.f + t) + 0.5f * a * (1.f - t * t) * du;
+    }
+    case ICAP_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case ICAP_ACT_QUICK_GELU: {
+      float s = 1.f / (1.f + __expf(-1.702f * a));
+      return s + a * 1.702f * s * (1.f - s);
+    }
+    case ICAP_ACT_TANH: return 1.f - a * a;
+    default: return 1.f;
+  }
+}
+
+inline int dsize(int dtype) { return dtype == ICAP_BF16 ? 2 : 4; }
+
+}  // namespace icap

@@ -1,0 +1,720 @@
+// HBM-bound kernels of the captioning path: input assembly, cross entropy,
+// clip + AdamW, layout/reduction helpers, CLIP tower glue, greedy-decode glue.
+#include "common.h"
+
+#include <math.h>
+
+namespace icap {
+
+static inline hipStream_t S_(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline unsigned nblk(int64_t n, int per, int cap = 65535) {
+  int64_t b = (n + per - 1) / per;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (unsigned)b;
+}
+
+// block-wide sum (256 threads)
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = red[0] + red[1] + red[2] + red[3];
+  return r;
+}
+
+// ---------------------------------------------------------------- GPT-2 input
+template <typename T>
+__global__ void gpt2_embed_kernel(int B, int P, int L, int D, const T* __restrict__ prefix, int64_t pbs,
+                                  const T* __restrict__ wte, const T* __restrict__ wpe,
+                                  const int64_t* __restrict__ ids, T* __restrict__ x, uint32_t thr,
+                                  float inv_keep, uint64_t seed0, const uint64_t* seed_ptr, uint64_t offset) {
+  const int S = P + L, D4 = D >> 2;
+  const uint64_t seed = thr ? eff_seed(seed0, seed_ptr) : 0ull;
+  const int64_t total = (int64_t)B * S * D4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / D4;
+    const int c = (int)(i - row * D4) * 4;
+    const int b = (int)(row / S), t = (int)(row - (int64_t)b * S);
+    float v[4], w[4];
+    if (t < P) io<T>::ld4(prefix + (int64_t)b * pbs + (int64_t)t * D + c, v);
+    else io<T>::ld4(wte + ids[(int64_t)b * L + (t - P)] * D + c, v);
+    io<T>::ld4(wpe + (int64_t)t * D + c, w);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] += w[e];
+      if (thr) v[e] *= drop_scale(seed, offset + (uint64_t)(row * D + c + e), thr, inv_keep);
+    }
+    io<T>::st4(x + row * D + c, v);
+  }
+}
+
+__global__ void caption_prep_kernel(int B, int P, int L, const int64_t* __restrict__ mask,
+                                    const int64_t* __restrict__ labels, int32_t* key_mask, int32_t* lab_shift,
+                                    int32_t* n_valid) {
+  __shared__ float red[4];
+  const int S = P + L;
+  float cnt = 0.f;
+  for (int i = threadIdx.x; i < B * S; i += blockDim.x) {
+    const int b = i / S, t = i - b * S;
+    if (key_mask) key_mask[i] = (t < P || mask == nullptr) ? 1 : (mask[(int64_t)b * L + t - P] != 0 ? 1 : 0);
+    if (lab_shift) {
+      int lab = -100;
+      const int tn = t + 1;
+      if (tn < S && tn >= P && labels) lab = (int)labels[(int64_t)b * L + tn - P];
+      lab_shift[i] = lab;
+      cnt += (lab != -100) ? 1.f : 0.f;
+    }
+  }
+  const float tot = block_sum256(cnt, red);
+  if (threadIdx.x == 0 && n_valid) *n_valid = (int32_t)(tot + 0.5f);
+}
+
+// ---------------------------------------------------------------- cross entropy
+template <typename T>
+__global__ __launch_bounds__(256) void ce_kernel(int64_t V, const T* __restrict__ logits, int64_t ld,
+                                                const int32_t* __restrict__ labels,
+                                                const int32_t* __restrict__ n_valid, float* __restrict__ loss_rows,
+                                                T* dlogits, float grad_scale) {
+  __shared__ float redm[4], reds[4];
+  const int64_t r = blockIdx.x;
+  const int y = labels[r];
+  const T* x = logits + r * ld;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (y < 0) {
+    if (tid == 0) loss_rows[r] = 0.f;
+    if (dlogits) {
+      T* dx = dlogits + r * ld;
+      for (int64_t j = tid; j < ld; j += 256) io<T>::st(dx + j, 0.f);
+    }
+    return;
+  }
+  // pass 1: online max / sum-exp per thread over float4 groups
+  float m = -INFINITY, s = 0.f;
+  const int64_t V4 = V >> 2;
+  for (int64_t g = tid; g < V4; g += 256) {
+    float v[4];
+    io<T>::ld4(x + 4 * g, v);
+    const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+    if (mx > m) { s *= __expf(m - mx); m = mx; }
+    s += __expf(v[0] - m) + __expf(v[1] - m) + __expf(v[2] - m) + __expf(v[3] - m);
+  }
+  for (int64_t j = 4 * V4 + tid; j < V; j += 256) {
+    const float v = io<T>::ld(x + j);
+    if (v > m) { s *= __expf(m - v); m = v; }
+    s += __expf(v - m);
+  }
+  // combine (m, s) across the block
+  float bm = wave_max(m);
+  s = (m == -INFINITY) ? 0.f : s * __expf(m - bm);
+  s = wave_sum(s);
+  if (lane == 0) { redm[w] = bm; reds[w] = s; }
+  __syncthreads();
+  float M = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+  float Ssum = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) Ssum += reds[k] * __expf(redm[k] - M);
+  const float lse = M + logf(Ssum);
+  if (tid == 0) loss_rows[r] = lse - io<T>::ld(x + y);
+  if (dlogits) {
+    const float nv = (float)(*n_valid);
+    const float sc = grad_scale / nv;
+    T* dx = dlogits + r * ld;
+    for (int64_t g = tid; g < V4; g += 256) {
+      float v[4];
+      io<T>::ld4(x + 4 * g, v);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t j = 4 * g + e;
+        v[e] = (__expf(v[e] - lse) - (j == y ? 1.f : 0.f)) * sc;
+      }
+      io<T>::st4(dx + 4 * g, v);
+    }
+    for (int64_t j = 4 * V4 + tid; j < ld; j += 256) {
+      float v = 0.f;
+      if (j < V) v = (__expf(io<T>::ld(x + j) - lse) - (j == y ? 1.f : 0.f)) * sc;
+      io<T>::st(dx + j, v);
+    }
+  }
+}
+
+__global__ void ce_reduce_kernel(int64_t rows, const float* __restrict__ loss_rows, const int32_t* n_valid,
+                                 float* loss) {
+  __shared__ double red[256];
+  double a = 0.0;
+  for (int64_t i = threadIdx.x; i < rows; i += 256) a += (double)loss_rows[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss = (float)(red[0] / (double)(*n_valid));
+}
+
+// ---------------------------------------------------------------- norm / AdamW
+constexpr int SQ_BLOCKS = 1024;
+
+__global__ __launch_bounds__(256) void sqnorm_partial_kernel(int64_t n, const float* __restrict__ x, float* partial) {
+  __shared__ float red[4];
+  float a = 0.f;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    a += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += 256) a += x[i] * x[i];
+  a = block_sum256(a, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = a;
+}
+
+struct AdamState {  // 64-byte device state, see icap.h
+  int64_t step;
+  float norm, clip, lr, step_size, bc2_sqrt, decay;
+  float pad[8];
+};
+
+__global__ void adam_finalize_kernel(int nparts, const float* __restrict__ partial, AdamState* st, float* sq_out,
+                                     float lr0, float beta1, float beta2, float wd, float max_norm,
+                                     int64_t warmup, int64_t total) {
+  __shared__ double red[256];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) a += (double)partial[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  if (sq_out) { *sq_out = (float)red[0]; return; }
+  const float norm = (float)sqrt(red[0]);
+  // TORCH/nn/utils/clip_grad.py:165-169: coef = max_norm / (norm + 1e-6), clamped to 1
+  float clip = 1.f;
+  if (max_norm > 0.f) {
+    clip = max_norm / (norm + 1e-6f);
+    if (clip > 1.f) clip = 1.f;
+  }
+  const int64_t k = st->step;
+  // HF/optimization.py:101-107 linear schedule with warmup
+  double lam;
+  if (k < warmup) lam = (double)k / (double)(warmup > 1 ? warmup : 1);
+  else {
+    const double den = (double)((total - warmup) > 1 ? (total - warmup) : 1);
+    lam = (double)(total - k) / den;
+    if (lam < 0.0) lam = 0.0;
+  }
+  const double lr = (double)lr0 * lam;
+  const double t = (double)(k + 1);
+  const double bc1 = 1.0 - pow((double)beta1, t);
+  const double bc2 = 1.0 - pow((double)beta2, t);
+  st->norm = norm;
+  st->clip = clip;
+  st->lr = (float)lr;
+  st->step_size = (float)(lr / bc1);
+  st->bc2_sqrt = (float)sqrt(bc2);
+  st->decay = (float)(1.0 - lr * (double)wd);
+  st->step = k + 1;
+}
+
+__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, float clip, float decay, float w1,
+                                         float b2, float w2, float step_size, float bc2s, float eps) {
+  g *= clip;
+  p *= decay;
+  m = m + w1 * (g - m);        // exp_avg.lerp_(grad, 1-beta1)
+  v = v * b2 + w2 * (g * g);   // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1-beta2)
+  const float denom = sqrtf(v) / bc2s + eps;
+  p = p + (-step_size) * (m / denom);
+}
+
+__global__ __launch_bounds__(256) void adam_update_kernel(int64_t n, float* __restrict__ P, const float* __restrict__ G,
+                                                         float* __restrict__ M1, float* __restrict__ M2,
+                                                         bf16_t* __restrict__ out16, const AdamState* __restrict__ st,
+                                                         float beta1, float beta2, float eps) {
+  const float clip = st->clip, decay = st->decay, step_size = st->step_size, bc2s = st->bc2_sqrt;
+  const float w1 = 1.f - beta1, w2 = 1.f - beta2;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 p = reinterpret_cast<float4*>(P)[i];
+    const float4 g = reinterpret_cast<const float4*>(G)[i];
+    float4 m = reinterpret_cast<float4*>(M1)[i];
+    float4 v = reinterpret_cast<float4*>(M2)[i];
+    adam_one(p.x, g.x, m.x, v.x, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
+    adam_one(p.y, g.y, m.y, v.y, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
+    adam_one(p.z, g.z, m.z, v.z, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
+    adam_one(p.w, g.w, m.w, v.w, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
+    reinterpret_cast<float4*>(P)[i] = p;
+    reinterpret_cast<float4*>(M1)[i] = m;
+    reinterpret_cast<float4*>(M2)[i] = v;
+    if (out16) {
+      const float o[4] = {p.x, p.y, p.z, p.w};
+      io<bf16_t>::st4(out16 + 4 * i, o);
+    }
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += 256) {
+      float p = P[i], m = M1[i], v = M2[i];
+      adam_one(p, G[i], m, v, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
+      P[i] = p; M1[i] = m; M2[i] = v;
+      if (out16) out16[i] = f2bf(p);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- layout helpers
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(int64_t rows, int64_t cols, const T* __restrict__ src,
+                                                       int64_t lds, T* __restrict__ dst, int64_t ldd,
+                                                       int64_t rows_pad) {
+  __shared__ T tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    T v = (T)0;
+    if (r < rows && c < cols) v = src[r * lds + c];
+    tile[i][tx] = v;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < cols && r < rows_pad) dst[c * ldd + r] = tile[tx][i];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int64_t N, const T* __restrict__ src, int64_t ld,
+                                                    int64_t rows_per_chunk, float* __restrict__ partial) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + tx;
+  const int64_t m0 = (int64_t)blockIdx.y * rows_per_chunk;
+  int64_t m1 = m0 + rows_per_chunk;
+  if (m1 > M) m1 = M;
+  float a = 0.f;
+  if (c < N)
+    for (int64_t m = m0 + ty; m < m1; m += 4) a += io<T>::ld(src + m * ld + c);
+  red[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && c < N) partial[(int64_t)blockIdx.y * N + c] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+}
+
+__global__ void colsum_reduce_kernel(int64_t N, int nchunks, const float* __restrict__ partial, float* out, int acc) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float a = 0.f;
+  for (int i = 0; i < nchunks; ++i) a += partial[(int64_t)i * N + c];
+  out[c] = acc ? out[c] + a : a;
+}
+
+template <typename TS, typename TD>
+__global__ void map2d_kernel(int64_t M, int64_t N, const TS* __restrict__ src, int64_t lds, TD* __restrict__ dst,
+                             int64_t ldd, uint32_t thr, float inv_keep, uint64_t seed0, const uint64_t* seed_ptr,
+                             uint64_t offset) {
+  const int64_t total = M * N;
+  const uint64_t seed = thr ? eff_seed(seed0, seed_ptr) : 0ull;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / N, n = i - m * N;
+    float v = io<TS>::ld(src + m * lds + n);
+    if (thr) v *= drop_scale(seed, offset + (uint64_t)i, thr, inv_keep);
+    io<TD>::st(dst + m * ldd + n, v);
+  }
+}
+
+__global__ void counter_inc_kernel(uint64_t* c) {
+  if (threadIdx.x == 0) *c += 1;
+}
+
+template <typename T>
+__global__ void broadcast_rows_kernel(int B, int64_t R, int64_t D, const float* __restrict__ src, T* __restrict__ dst,
+                                      int64_t bs) {
+  const int64_t per = R * D, total = (int64_t)B * per;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = i / per, k = i - b * per;
+    io<T>::st(dst + b * bs + k, src[k]);
+  }
+}
+
+// ---------------------------------------------------------------- CLIP glue
+template <typename T>
+__global__ void im2col_kernel(int B, int C, int HW, int p, const float* __restrict__ px, T* __restrict__ out) {
+  const int G = HW / p;
+  const int K = C * p * p;
+  const int p4 = p >> 2;
+  const int64_t total = (int64_t)B * G * G * C * p * p4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = i;
+    const int kx4 = (int)(t % p4); t /= p4;
+    const int ky = (int)(t % p); t /= p;
+    const int c = (int)(t % C); t /= C;
+    const int gx = (int)(t % G); t /= G;
+    const int gy = (int)(t % G); t /= G;
+    const int b = (int)t;
+    const float4 v = *reinterpret_cast<const float4*>(px + (((int64_t)b * C + c) * HW + gy * p + ky) * HW + gx * p + 4 * kx4);
+    const float o[4] = {v.x, v.y, v.z, v.w};
+    const int64_t row = ((int64_t)b * G + gy) * G + gx;
+    io<T>::st4(out + row * K + c * p * p + ky * p + 4 * kx4, o);
+  }
+}
+
+template <typename T>
+__global__ void vit_embed_kernel(int B, int G2, int D, const T* __restrict__ pe, const float* __restrict__ cls,
+                                 const float* __restrict__ pos, T* __restrict__ x) {
+  const int S = G2 + 1;
+  const int64_t total = (int64_t)B * S * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / D;
+    const int d = (int)(i - row * D);
+    const int b = (int)(row / S), t = (int)(row - (int64_t)b * S);
+    const float v = (t == 0) ? cls[d] : io<T>::ld(pe + ((int64_t)b * G2 + t - 1) * D + d);
+    io<T>::st(x + i, v + pos[(int64_t)t * D + d]);
+  }
+}
+
+template <typename T>
+__global__ void l2norm_kernel(int64_t rows, int64_t D, const T* __restrict__ x, int64_t ldx, float* __restrict__ out,
+                              int64_t ldo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  float s = 0.f;
+  for (int64_t d = lane; d < D; d += 64) {
+    const float v = io<T>::ld(x + r * ldx + d);
+    s += v * v;
+  }
+  s = wave_sum(s);
+  const float inv = 1.f / sqrtf(s);
+  for (int64_t d = lane; d < D; d += 64) out[r * ldo + d] = io<T>::ld(x + r * ldx + d) * inv;
+}
+
+// ---------------------------------------------------------------- greedy decode glue
+template <typename T>
+__global__ __launch_bounds__(256) void greedy_next_kernel(int64_t V, const T* __restrict__ logits, int64_t ld,
+                                                         int64_t eos, int32_t* finished, int64_t* tokens,
+                                                         int64_t ld_tokens, int step, const T* __restrict__ wte,
+                                                         const T* __restrict__ wpe, int pos, int D, T* __restrict__ x) {
+  __shared__ float rv[4];
+  __shared__ int64_t ri[4];
+  __shared__ int64_t nxt;
+  const int b = blockIdx.x;
+  const T* row = logits + (int64_t)b * ld;
+  float best = -INFINITY;
+  int64_t bi = V;  // sentinel
+  for (int64_t j = threadIdx.x; j < V; j += 256) {
+    const float v = io<T>::ld(row + j);
+    if (v > best || (v == best && j < bi) || (v != v && best == best)) { best = v; bi = j; }
+  }
+  // wave argmax (ties -> smallest index)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int64_t oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { rv[w] = best; ri[w] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float bv = rv[0];
+    int64_t bj = ri[0];
+    for (int k = 1; k < 4; ++k)
+      if (rv[k] > bv || (rv[k] == bv && ri[k] < bj)) { bv = rv[k]; bj = ri[k]; }
+    if (bj >= V) bj = 0;
+    int fin = finished[b];
+    if (fin) bj = eos;
+    if (bj == eos) fin = 1;
+    finished[b] = fin;
+    tokens[(int64_t)b * ld_tokens + step] = bj;
+    nxt = bj;
+  }
+  __syncthreads();
+  if (x) {
+    const int64_t id = nxt;
+    for (int d = threadIdx.x; d < D; d += 256)
+      io<T>::st(x + (int64_t)b * D + d, io<T>::ld(wte + id * D + d) + io<T>::ld(wpe + (int64_t)pos * D + d));
+  }
+}
+
+template <typename T>
+__global__ void add_position_kernel(int B, int npos, int D, const T* __restrict__ src, int64_t sbs, int64_t sts,
+                                    const T* __restrict__ wpe, int pos0, T* __restrict__ x) {
+  const int64_t total = (int64_t)npos * B * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / D;
+    const int d = (int)(i - row * D);
+    const int t = (int)(row / B), b = (int)(row - (int64_t)t * B);
+    const float v = io<T>::ld(src + (int64_t)b * sbs + (int64_t)t * sts + d) + io<T>::ld(wpe + (int64_t)(pos0 + t) * D + d);
+    io<T>::st(x + i, v);
+  }
+}
+
+}  // namespace icap
+
+using namespace icap;
+
+// launch KERNEL<T> with every typed pointer argument cast to T* via the TP()/CTP() helpers
+#define DISPATCH_T(dtype, BODY)                       \
+  do {                                                \
+    if ((dtype) == ICAP_BF16) {                       \
+      typedef bf16_t T;                               \
+      BODY;                                           \
+    } else if ((dtype) == ICAP_F32) {                 \
+      typedef float T;                                \
+      BODY;                                           \
+    } else {                                          \
+      set_error("bad dtype");                         \
+      return ICAP_ERR_ARG;                            \
+    }                                                 \
+  } while (0)
+#define TP(x) reinterpret_cast<T*>(x)
+#define CTP(x) reinterpret_cast<const T*>(x)
+
+extern "C" int icap_gpt2_embed(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D, const void* prefix,
+                               int64_t prefix_bstride, const void* wte, const void* wpe, const int64_t* ids, void* x,
+                               float drop_p, uint64_t seed, uint64_t offset, const uint64_t* seed_ptr,
+                               void* stream) {
+  ICAP_REQUIRE(D % 4 == 0 && B >= 0 && P >= 0 && L >= 0, "icap_gpt2_embed: bad geometry");
+  ICAP_REQUIRE(x && wpe && (P == 0 || prefix) && (L == 0 || (wte && ids)), "icap_gpt2_embed: null pointer");
+  ICAP_REQUIRE(prefix_bstride % 4 == 0, "icap_gpt2_embed: prefix_bstride must be a multiple of 4");
+  const int64_t n = (int64_t)B * (P + L) * (D / 4);
+  if (n == 0) return ICAP_OK;
+  const uint32_t thr = drop_p > 0.f ? drop_threshold(drop_p) : 0u;
+  const float ik = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  if (dtype == ICAP_BF16)
+    hipLaunchKernelGGL(gpt2_embed_kernel<bf16_t>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B, P, L, D,
+                       (const bf16_t*)prefix, prefix_bstride, (const bf16_t*)wte, (const bf16_t*)wpe, ids, (bf16_t*)x,
+                       thr, ik, seed, seed_ptr, offset);
+  else
+    hipLaunchKernelGGL(gpt2_embed_kernel<float>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B, P, L, D,
+                       (const float*)prefix, prefix_bstride, (const float*)wte, (const float*)wpe, ids, (float*)x,
+                       thr, ik, seed, seed_ptr, offset);
+  return check_launch("icap_gpt2_embed");
+}
+
+extern "C" int icap_caption_prep(int32_t B, int32_t P, int32_t L, const int64_t* mask, const int64_t* labels,
+                                 int32_t* key_mask, int32_t* labels_shift, int32_t* n_valid, void* stream) {
+  ICAP_REQUIRE(B >= 0 && P >= 0 && L >= 0, "icap_caption_prep: bad geometry");
+  hipLaunchKernelGGL(caption_prep_kernel, dim3(1), dim3(256), 0, S_(stream), B, P, L, mask, labels, key_mask,
+                     labels_shift, n_valid);
+  return check_launch("icap_caption_prep");
+}
+
+extern "C" size_t icap_cross_entropy_workspace_bytes(int64_t rows) {
+  return (size_t)(rows > 0 ? rows : 1) * sizeof(float);
+}
+
+extern "C" int icap_cross_entropy(int32_t dtype, int64_t rows, int64_t V, const void* logits, int64_t ld,
+                                  const int32_t* labels, const int32_t* n_valid, float* loss, void* dlogits,
+                                  float grad_scale, void* workspace, void* stream) {
+  ICAP_REQUIRE(logits && labels && n_valid && loss && workspace, "icap_cross_entropy: null pointer");
+  ICAP_REQUIRE(V > 0 && ld >= V && ld % 4 == 0, "icap_cross_entropy: ld must be >= V and a multiple of 4");
+  if (rows <= 0) return ICAP_OK;
+  ICAP_REQUIRE(rows < (1ll << 31), "icap_cross_entropy: too many rows");
+  float* lrows = reinterpret_cast<float*>(workspace);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(ce_kernel<T>, dim3((unsigned)rows), dim3(256), 0, S_(stream), V, CTP(logits),
+                                       ld, labels, n_valid, lrows, TP(dlogits), grad_scale));
+  int rc = check_launch("icap_cross_entropy");
+  if (rc) return rc;
+  hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(256), 0, S_(stream), rows, lrows, n_valid, loss);
+  return check_launch("icap_cross_entropy(reduce)");
+}
+
+extern "C" size_t icap_adamw_workspace_bytes(int64_t n) {
+  (void)n;
+  return SQ_BLOCKS * sizeof(float);
+}
+
+static int sq_partials(int64_t n, const float* x, float* partial, hipStream_t s, int* nparts) {
+  const int nb = (int)nblk(n / 4 + 1, 256, SQ_BLOCKS);
+  hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, s, n, x, partial);
+  *nparts = nb;
+  return check_launch("sqnorm");
+}
+
+extern "C" int icap_sqnorm(int64_t n, const float* x, float* out, void* workspace, void* stream) {
+  ICAP_REQUIRE(x && out && workspace, "icap_sqnorm: null pointer");
+  ICAP_REQUIRE((reinterpret_cast<uintptr_t>(x) & 15) == 0, "icap_sqnorm: x must be 16-byte aligned");
+  int np = 0;
+  float* partial = reinterpret_cast<float*>(workspace);
+  int rc = sq_partials(n, x, partial, S_(stream), &np);
+  if (rc) return rc;
+  hipLaunchKernelGGL(adam_finalize_kernel, dim3(1), dim3(256), 0, S_(stream), np, partial, (AdamState*)nullptr, out,
+                     0.f, 0.f, 0.f, 0.f, 0.f, (int64_t)0, (int64_t)0);
+  return check_launch("icap_sqnorm");
+}
+
+extern "C" int icap_adamw_step(const icap_adamw_args* a, void* workspace, void* stream) {
+  ICAP_REQUIRE(a && workspace, "icap_adamw_step: null args/workspace");
+  ICAP_REQUIRE(a->params && a->grads && a->exp_avg && a->exp_avg_sq && a->state, "icap_adamw_step: null pointer");
+  ICAP_REQUIRE(((reinterpret_cast<uintptr_t>(a->params) | reinterpret_cast<uintptr_t>(a->grads) |
+                 reinterpret_cast<uintptr_t>(a->exp_avg) | reinterpret_cast<uintptr_t>(a->exp_avg_sq)) & 15) == 0,
+               "icap_adamw_step: buffers must be 16-byte aligned");
+  ICAP_REQUIRE(a->bf16_out == nullptr || (reinterpret_cast<uintptr_t>(a->bf16_out) & 7) == 0,
+               "icap_adamw_step: bf16_out must be 8-byte aligned");
+  if (a->n <= 0) return ICAP_OK;
+  hipStream_t s = S_(stream);
+  float* partial = reinterpret_cast<float*>(workspace);
+  int np = 0;
+  int rc = sq_partials(a->n, a->grads, partial, s, &np);
+  if (rc) return rc;
+  hipLaunchKernelGGL(adam_finalize_kernel, dim3(1), dim3(256), 0, s, np, partial, (AdamState*)a->state,
+                     (float*)nullptr, a->lr, a->beta1, a->beta2, a->weight_decay, a->max_norm, a->num_warmup_steps,
+                     a->num_training_steps);
+  rc = check_launch("icap_adamw_step(finalize)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(adam_update_kernel, dim3(nblk(a->n / 4 + 1, 256, 4096)), dim3(256), 0, s, a->n, a->params,
+                     a->grads, a->exp_avg, a->exp_avg_sq, (bf16_t*)a->bf16_out, (const AdamState*)a->state, a->beta1,
+                     a->beta2, a->eps);
+  return check_launch("icap_adamw_step(update)");
+}
+
+extern "C" int icap_transpose(int32_t dtype, int64_t rows, int64_t cols, const void* src, int64_t lds, void* dst,
+                              int64_t ldd, int64_t rows_pad, void* stream) {
+  ICAP_REQUIRE(src && dst && rows_pad >= rows, "icap_transpose: bad args");
+  if (rows_pad == 0 || cols == 0) return ICAP_OK;
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows_pad + 63) / 64));
+  ICAP_REQUIRE(grid.y < 65536, "icap_transpose: too many rows");
+  if (dtype == ICAP_BF16)
+    hipLaunchKernelGGL(transpose_kernel<uint16_t>, grid, dim3(256), 0, S_(stream), rows, cols, (const uint16_t*)src,
+                       lds, (uint16_t*)dst, ldd, rows_pad);
+  else
+    hipLaunchKernelGGL(transpose_kernel<uint32_t>, grid, dim3(256), 0, S_(stream), rows, cols, (const uint32_t*)src,
+                       lds, (uint32_t*)dst, ldd, rows_pad);
+  return check_launch("icap_transpose");
+}
+
+static int64_t colsum_chunks(int64_t M) {
+  int64_t c = (M + 255) / 256;
+  if (c > 64) c = 64;
+  if (c < 1) c = 1;
+  return c;
+}
+
+extern "C" size_t icap_colsum_workspace_bytes(int64_t M, int64_t N) {
+  return (size_t)colsum_chunks(M) * (size_t)(N > 0 ? N : 1) * sizeof(float);
+}
+
+extern "C" int icap_colsum(int32_t dtype, int64_t M, int64_t N, const void* src, int64_t ld, float* out,
+                           int32_t accumulate, void* workspace, void* stream) {
+  ICAP_REQUIRE(src && out && workspace, "icap_colsum: null pointer");
+  if (N == 0) return ICAP_OK;
+  const int64_t ch = colsum_chunks(M);
+  const int64_t rpc = (M + ch - 1) / ch;
+  float* partial = reinterpret_cast<float*>(workspace);
+  dim3 grid((unsigned)((N + 63) / 64), (unsigned)ch);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_kernel<T>, grid, dim3(256), 0, S_(stream), M, N, CTP(src), ld,
+                                       rpc > 0 ? rpc : 1, partial));
+  int rc = check_launch("icap_colsum");
+  if (rc) return rc;
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, S_(stream), N, (int)ch,
+                     partial, out, accumulate);
+  return check_launch("icap_colsum(reduce)");
+}
+
+extern "C" int icap_dropout_apply(int32_t dtype, int64_t M, int64_t N, const void* src, int64_t lds, void* dst,
+                                  int64_t ldd, float drop_p, uint64_t seed, uint64_t offset,
+                                  const uint64_t* seed_ptr, void* stream) {
+  ICAP_REQUIRE(src && dst && drop_p >= 0.f && drop_p < 1.f, "icap_dropout_apply: bad args");
+  if (M * N == 0) return ICAP_OK;
+  const uint32_t thr = drop_p > 0.f ? drop_threshold(drop_p) : 0u;
+  const float ik = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  DISPATCH_T(dtype, hipLaunchKernelGGL((map2d_kernel<T, T>), dim3(nblk(M * N, 256, 8192)), dim3(256), 0, S_(stream),
+                                       M, N, CTP(src), lds, TP(dst), ldd, thr, ik, seed, seed_ptr, offset));
+  return check_launch("icap_dropout_apply");
+}
+
+extern "C" int icap_convert(int32_t src_dtype, int32_t dst_dtype, int64_t M, int64_t N, const void* src, int64_t lds,
+                            void* dst, int64_t ldd, void* stream) {
+  ICAP_REQUIRE(src && dst, "icap_convert: null pointer");
+  if (M * N == 0) return ICAP_OK;
+  const dim3 g(nblk(M * N, 256, 8192)), b(256);
+  if (src_dtype == ICAP_F32 && dst_dtype == ICAP_BF16)
+    hipLaunchKernelGGL((map2d_kernel<float, bf16_t>), g, b, 0, S_(stream), M, N, (const float*)src, lds, (bf16_t*)dst,
+                       ldd, 0u, 1.f, (uint64_t)0, (const uint64_t*)nullptr, (uint64_t)0);
+  else if (src_dtype == ICAP_BF16 && dst_dtype == ICAP_F32)
+    hipLaunchKernelGGL((map2d_kernel<bf16_t, float>), g, b, 0, S_(stream), M, N, (const bf16_t*)src, lds, (float*)dst,
+                       ldd, 0u, 1.f, (uint64_t)0, (const uint64_t*)nullptr, (uint64_t)0);
+  else if (src_dtype == ICAP_F32 && dst_dtype == ICAP_F32)
+    hipLaunchKernelGGL((map2d_kernel<float, float>), g, b, 0, S_(stream), M, N, (const float*)src, lds, (float*)dst,
+                       ldd, 0u, 1.f, (uint64_t)0, (const uint64_t*)nullptr, (uint64_t)0);
+  else if (src_dtype == ICAP_BF16 && dst_dtype == ICAP_BF16)
+    hipLaunchKernelGGL((map2d_kernel<bf16_t, bf16_t>), g, b, 0, S_(stream), M, N, (const bf16_t*)src, lds,
+                       (bf16_t*)dst, ldd, 0u, 1.f, (uint64_t)0, (const uint64_t*)nullptr, (uint64_t)0);
+  else {
+    set_error("icap_convert: bad dtype");
+    return ICAP_ERR_ARG;
+  }
+  return check_launch("icap_convert");
+}
+
+extern "C" int icap_broadcast_rows(int32_t dtype, int32_t B, int64_t R, int64_t D, const float* src, void* dst,
+                                   int64_t dst_bstride, void* stream) {
+  ICAP_REQUIRE(src && dst, "icap_broadcast_rows: null pointer");
+  if ((int64_t)B * R * D == 0) return ICAP_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(broadcast_rows_kernel<T>, dim3(nblk((int64_t)B * R * D, 256, 8192)), dim3(256),
+                                       0, S_(stream), B, R, D, src, TP(dst), dst_bstride));
+  return check_launch("icap_broadcast_rows");
+}
+
+extern "C" int icap_im2col_patches(int32_t dtype, int32_t B, int32_t C, int32_t HW, int32_t patch, const float* pixels,
+                                   void* patches, void* stream) {
+  ICAP_REQUIRE(pixels && patches, "icap_im2col_patches: null pointer");
+  ICAP_REQUIRE(patch > 0 && patch % 4 == 0 && HW % patch == 0, "icap_im2col_patches: patch must divide HW and be a multiple of 4");
+  const int G = HW / patch;
+  const int64_t n = (int64_t)B * G * G * C * patch * (patch / 4);
+  if (n == 0) return ICAP_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(im2col_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B, C, HW,
+                                       patch, pixels, TP(patches)));
+  return check_launch("icap_im2col_patches");
+}
+
+extern "C" int icap_vit_embed(int32_t dtype, int32_t B, int32_t G2, int32_t D, const void* patch_emb, const float* cls,
+                              const float* pos, void* x, void* stream) {
+  ICAP_REQUIRE(patch_emb && cls && pos && x, "icap_vit_embed: null pointer");
+  const int64_t n = (int64_t)B * (G2 + 1) * D;
+  if (n == 0) return ICAP_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(vit_embed_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B, G2,
+                                       D, CTP(patch_emb), cls, pos, TP(x)));
+  return check_launch("icap_vit_embed");
+}
+
+extern "C" int icap_l2norm_rows(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx, float* out,
+                                int64_t ldo, void* stream) {
+  ICAP_REQUIRE(x && out, "icap_l2norm_rows: null pointer");
+  if (rows == 0) return ICAP_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(l2norm_kernel<T>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, S_(stream),
+                                       rows, D, CTP(x), ldx, out, ldo));
+  return check_launch("icap_l2norm_rows");
+}
+
+extern "C" int icap_greedy_next(int32_t dtype, int32_t B, int64_t V, const void* logits, int64_t ld, int64_t eos,
+                                int32_t* finished, int64_t* tokens, int64_t ld_tokens, int32_t step, const void* wte,
+                                const void* wpe, int32_t pos, int32_t D, void* x, void* stream) {
+  ICAP_REQUIRE(logits && finished && tokens, "icap_greedy_next: null pointer");
+  ICAP_REQUIRE(x == nullptr || (wte && wpe), "icap_greedy_next: x requires wte/wpe");
+  if (B == 0) return ICAP_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(greedy_next_kernel<T>, dim3((unsigned)B), dim3(256), 0, S_(stream), V,
+                                       CTP(logits), ld, eos, finished, tokens, ld_tokens, step, CTP(wte), CTP(wpe),
+                                       pos, D, TP(x)));
+  return check_launch("icap_greedy_next");
+}
+
+extern "C" int icap_add_position(int32_t dtype, int32_t B, int32_t npos, int32_t D, const void* src,
+                                 int64_t src_bstride, int64_t src_tstride, const void* wpe, int32_t pos0, void* x,
+                                 void* stream) {
+  ICAP_REQUIRE(src && wpe && x, "icap_add_position: null pointer");
+  const int64_t n = (int64_t)npos * B * D;
+  if (n == 0) return ICAP_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(add_position_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B,
+                                       npos, D, CTP(src), src_bstride, src_tstride, CTP(wpe), pos0, TP(x)));
+  return check_launch("icap_add_position");
+}
+
+extern "C" int icap_counter_increment(uint64_t* counter, void* stream) {
+  ICAP_REQUIRE(counter, "icap_counter_increment: null pointer");
+  hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(64), 0, S_(stream), counter);
+  return check_launch("icap_counter_increment");
+}

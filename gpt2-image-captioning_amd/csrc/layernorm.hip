@@ -1,0 +1,240 @@
+// LayerNorm forward/backward (HBM-bound): one wave per row, 4 waves per block,
+// grid-stride over rows; each lane owns D/256 float4 groups (D <= 1024).
+// Stats in fp32 with a two-pass variance held in registers.
+#include "common.h"
+
+namespace icap {
+
+constexpr int LN_MAXV = 4;       // float4 groups per lane -> D <= 1024
+constexpr int LN_BWD_BLOCKS = 256;
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t rows, int D, const T* __restrict__ x, int64_t ldx,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, float eps,
+                                                    T* __restrict__ y, int64_t ldy, float* mean_out,
+                                                    float* rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int D4 = D >> 2;
+  const float invD = 1.f / (float)D;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += nw) {
+    float v[LN_MAXV][4];
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) {
+      const int g = lane + 64 * t;
+      if (g < D4) {
+        io<T>::ld4(x + r * ldx + 4 * g, v[t]);
+        s += (v[t][0] + v[t][1]) + (v[t][2] + v[t][3]);
+      }
+    }
+    const float mean = wave_sum(s) * invD;
+    float s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) {
+      const int g = lane + 64 * t;
+      if (g < D4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[t][e] - mean;
+          s2 += d * d;
+        }
+      }
+    }
+    const float var = wave_sum(s2) * invD;
+    const float rs = 1.f / sqrtf(var + eps);
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) {
+      const int g = lane + 64 * t;
+      if (g < D4) {
+        const float4 gm = *reinterpret_cast<const float4*>(gamma + 4 * g);
+        const float4 bt = *reinterpret_cast<const float4*>(beta + 4 * g);
+        float o[4];
+        o[0] = (v[t][0] - mean) * rs * gm.x + bt.x;
+        o[1] = (v[t][1] - mean) * rs * gm.y + bt.y;
+        o[2] = (v[t][2] - mean) * rs * gm.z + bt.z;
+        o[3] = (v[t][3] - mean) * rs * gm.w + bt.w;
+        io<T>::st4(y + r * ldy + 4 * g, o);
+      }
+    }
+    if (lane == 0) {
+      if (mean_out) mean_out[r] = mean;
+      if (rstd_out) rstd_out[r] = rs;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t rows, int D, const T* __restrict__ x, int64_t ldx,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ mean_in,
+                                                    const float* __restrict__ rstd_in,
+                                                    const T* __restrict__ dy, int64_t lddy,
+                                                    const T* __restrict__ dres, int64_t lddres,
+                                                    T* __restrict__ dx, int64_t lddx, T* __restrict__ dx_drop,
+                                                    uint32_t thr, float inv_keep, uint64_t seed0,
+                                                    const uint64_t* seed_ptr, uint64_t offset,
+                                                    float* __restrict__ partial) {
+  __shared__ float red[4][2][LN_MAXV * 256];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int D4 = D >> 2;
+  const float invD = 1.f / (float)D;
+  const uint64_t seed = thr ? eff_seed(seed0, seed_ptr) : 0ull;
+  float dg[LN_MAXV][4], db[LN_MAXV][4];
+#pragma unroll
+  for (int t = 0; t < LN_MAXV; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dg[t][e] = db[t][e] = 0.f;
+
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wv; r < rows; r += nw) {
+    const float mean = mean_in[r], rs = rstd_in[r];
+    float xh[LN_MAXV][4], gy[LN_MAXV][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) {
+      const int g = lane + 64 * t;
+      if (g < D4) {
+        float xv[4], dv[4];
+        io<T>::ld4(x + r * ldx + 4 * g, xv);
+        io<T>::ld4(dy + r * lddy + 4 * g, dv);
+        const float4 gm = *reinterpret_cast<const float4*>(gamma + 4 * g);
+        const float gmv[4] = {gm.x, gm.y, gm.z, gm.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[t][e] = (xv[e] - mean) * rs;
+          gy[t][e] = dv[e] * gmv[e];
+          s1 += gy[t][e];
+          s2 += gy[t][e] * xh[t][e];
+          dg[t][e] += dv[e] * xh[t][e];
+          db[t][e] += dv[e];
+        }
+      }
+    }
+    const float m1 = wave_sum(s1) * invD;
+    const float m2 = wave_sum(s2) * invD;
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) {
+      const int g = lane + 64 * t;
+      if (g < D4) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rs * (gy[t][e] - m1 - xh[t][e] * m2);
+        if (dres) {
+          float rv[4];
+          io<T>::ld4(dres + r * lddres + 4 * g, rv);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += rv[e];
+        }
+        io<T>::st4(dx + r * lddx + 4 * g, o);
+        if (dx_drop) {
+          const uint64_t base = offset + (uint64_t)(r * D + 4 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] *= drop_scale(seed, base + e, thr, inv_keep);
+          io<T>::st4(dx_drop + r * lddx + 4 * g, o);
+        }
+      }
+    }
+  }
+  if (partial) {
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) {
+      const int g = lane + 64 * t;
+      if (g < D4) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          red[wv][0][4 * g + e] = dg[t][e];
+          red[wv][1][4 * g + e] = db[t][e];
+        }
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256) {
+      float a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+      float b = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+      partial[(int64_t)blockIdx.x * 2 * D + c] = a;
+      partial[(int64_t)blockIdx.x * 2 * D + D + c] = b;
+    }
+  }
+}
+
+__global__ void ln_param_reduce(int nblk, int D, const float* __restrict__ partial, float* dgamma,
+                                float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float a = 0.f, b = 0.f;
+  for (int i = 0; i < nblk; ++i) {
+    a += partial[(int64_t)i * 2 * D + c];
+    b += partial[(int64_t)i * 2 * D + D + c];
+  }
+  if (dgamma) dgamma[c] += a;
+  if (dbeta) dbeta[c] += b;
+}
+
+}  // namespace icap
+
+using namespace icap;
+
+static int ln_blocks(int64_t rows, int cap) {
+  int64_t b = (rows + 3) / 4;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+extern "C" int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
+                                  const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
+                                  float* mean, float* rstd, void* stream) {
+  ICAP_REQUIRE(D > 0 && D % 4 == 0 && D <= 4 * 64 * LN_MAXV, "icap_layernorm_fwd: D must be a multiple of 4, <= 1024");
+  ICAP_REQUIRE(x && y && gamma && beta, "icap_layernorm_fwd: null pointer");
+  ICAP_REQUIRE(ldx % 4 == 0 && ldy % 4 == 0, "icap_layernorm_fwd: strides must be multiples of 4");
+  if (rows == 0) return ICAP_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nb = ln_blocks(rows, 4096);
+  if (dtype == ICAP_BF16)
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, rows, (int)D,
+                       (const bf16_t*)x, ldx, gamma, beta, eps, (bf16_t*)y, ldy, mean, rstd);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const float*)x,
+                       ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
+  return check_launch("icap_layernorm_fwd");
+}
+
+extern "C" size_t icap_layernorm_bwd_workspace_bytes(int64_t rows, int64_t D) {
+  return (size_t)ln_blocks(rows, LN_BWD_BLOCKS) * 2 * (size_t)D * sizeof(float);
+}
+
+extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
+                                  const float* gamma, const float* mean, const float* rstd,
+                                  const void* dy, int64_t lddy, const void* dres, int64_t lddres,
+                                  void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
+                                  uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
+                                  void* workspace, void* stream) {
+  ICAP_REQUIRE(D > 0 && D % 4 == 0 && D <= 4 * 64 * LN_MAXV, "icap_layernorm_bwd: D must be a multiple of 4, <= 1024");
+  ICAP_REQUIRE(x && gamma && mean && rstd && dy && dx, "icap_layernorm_bwd: null pointer");
+  ICAP_REQUIRE((dgamma == nullptr && dbeta == nullptr) || workspace != nullptr,
+               "icap_layernorm_bwd: dgamma/dbeta need a workspace");
+  ICAP_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "icap_layernorm_bwd: drop_p out of range");
+  if (rows == 0) return ICAP_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const bool want_params = dgamma || dbeta;
+  const int nb = ln_blocks(rows, want_params ? LN_BWD_BLOCKS : 4096);
+  const uint32_t thr = drop_p > 0.f ? drop_threshold(drop_p) : 0u;
+  const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  float* partial = want_params ? reinterpret_cast<float*>(workspace) : nullptr;
+  if (dtype == ICAP_BF16)
+    hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const bf16_t*)x, ldx,
+                       gamma, mean, rstd, (const bf16_t*)dy, lddy, (const bf16_t*)dres, lddres, (bf16_t*)dx,
+                       lddx, (bf16_t*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const float*)x, ldx,
+                       gamma, mean, rstd, (const float*)dy, lddy, (const float*)dres, lddres, (float*)dx,
+                       lddx, (float*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial);
+  int rc = check_launch("icap_layernorm_bwd");
+  if (rc != ICAP_OK || !want_params) return rc;
+  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, nb, (int)D, partial,
+                     dgamma, dbeta);
+  return check_launch("icap_layernorm_bwd(reduce)");
+}

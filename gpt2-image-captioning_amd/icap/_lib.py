@@ -1,0 +1,161 @@
+"""ctypes binding of libicap_hip.so (C-ABI declared in include/icap.h).
+
+The library is the product path: there is no CPU or PyTorch fallback. If the
+shared object is missing, or its gfx950 code object cannot be loaded on the
+current device, every op raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must be imported first: the .so binds to torch's HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libicap_hip.so")
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_GELU_NEW, ACT_RELU, ACT_QUICK_GELU, ACT_TANH = 0, 1, 2, 3, 4
+
+vp = C.c_void_p
+i32, i64, u64, f32, sz = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_size_t
+pi32 = C.POINTER(C.c_int32)
+pi64 = C.POINTER(C.c_int64)
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [
+        ("M", i64), ("N", i64), ("K", i64),
+        ("in_dtype", i32), ("c_dtype", i32),
+        ("A", vp), ("lda", i64),
+        ("B", vp), ("ldb", i64),
+        ("C", vp), ("ldc", i64),
+        ("alpha", f32), ("beta", f32),
+        ("bias", vp),
+        ("act", i32),
+        ("aux", vp), ("ldaux", i64),
+        ("dact", i32),
+        ("dact_src", vp), ("ld_dact", i64),
+        ("resid", vp), ("ldr", i64),
+        ("drop_p", f32), ("seed", u64), ("offset", u64),
+        ("seed_ptr", vp),
+    ]
+
+
+class AttnArgs(C.Structure):
+    _fields_ = [
+        ("dtype", i32),
+        ("B", i32), ("S", i32), ("H", i32), ("hd", i32),
+        ("row_stride_b", i64), ("row_stride_s", i64),
+        ("qkv", vp), ("ld_qkv", i64),
+        ("out", vp), ("ld_out", i64),
+        ("lse", vp),
+        ("key_mask", vp),
+        ("causal", i32),
+        ("scale", f32),
+        ("drop_p", f32), ("seed", u64), ("offset", u64),
+        ("seed_ptr", vp),
+        ("dout", vp), ("ld_dout", i64),
+        ("dqkv", vp), ("ld_dqkv", i64),
+    ]
+
+
+class AdamWArgs(C.Structure):
+    _fields_ = [
+        ("n", i64),
+        ("params", vp), ("grads", vp), ("exp_avg", vp), ("exp_avg_sq", vp),
+        ("bf16_out", vp),
+        ("state", vp),
+        ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("weight_decay", f32),
+        ("max_norm", f32),
+        ("num_warmup_steps", i64), ("num_training_steps", i64),
+    ]
+
+
+# name -> (restype, argtypes); must mirror include/icap.h exactly
+SIGNATURES = {
+    "icap_last_error": (C.c_char_p, []),
+    "icap_version": (C.c_int, []),
+    "icap_device_arch_ok": (C.c_int, []),
+    "icap_gemm": (C.c_int, [C.POINTER(GemmArgs), vp]),
+    "icap_layernorm_fwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, f32, vp, i64, vp, vp, vp]),
+    "icap_layernorm_bwd_workspace_bytes": (sz, [i64, i64]),
+    "icap_layernorm_bwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, vp,
+                                     f32, u64, u64, vp, vp, vp, vp, vp]),
+    "icap_attention_fwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
+    "icap_attention_bwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
+    "icap_attention_decode": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, i64, f32, vp]),
+    "icap_gpt2_embed": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, vp, f32, u64, u64, vp, vp]),
+    "icap_caption_prep": (C.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+    "icap_cross_entropy_workspace_bytes": (sz, [i64]),
+    "icap_cross_entropy": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, f32, vp, vp]),
+    "icap_adamw_workspace_bytes": (sz, [i64]),
+    "icap_adamw_step": (C.c_int, [C.POINTER(AdamWArgs), vp, vp]),
+    "icap_sqnorm": (C.c_int, [i64, vp, vp, vp, vp]),
+    "icap_transpose": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, i64, vp]),
+    "icap_colsum_workspace_bytes": (sz, [i64, i64]),
+    "icap_colsum": (C.c_int, [i32, i64, i64, vp, i64, vp, i32, vp, vp]),
+    "icap_dropout_apply": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, f32, u64, u64, vp, vp]),
+    "icap_counter_increment": (C.c_int, [vp, vp]),
+    "icap_convert": (C.c_int, [i32, i32, i64, i64, vp, i64, vp, i64, vp]),
+    "icap_broadcast_rows": (C.c_int, [i32, i32, i64, i64, vp, vp, i64, vp]),
+    "icap_im2col_patches": (C.c_int, [i32, i32, i32, i32, i32, vp, vp, vp]),
+    "icap_vit_embed": (C.c_int, [i32, i32, i32, i32, vp, vp, vp, vp, vp]),
+    "icap_l2norm_rows": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, vp]),
+    "icap_greedy_next": (C.c_int, [i32, i32, i64, vp, i64, i64, vp, vp, i64, i32, vp, vp, i32, i32, vp, vp]),
+    "icap_add_position": (C.c_int, [i32, i32, i32, i32, vp, i64, i64, vp, i32, vp, vp]),
+}
+
+_lib = None
+
+
+class IcapError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load (once) and bind the library; raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise IcapError(
+            f"libicap_hip.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no fallback path)"
+        )
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().icap_last_error()
+    return msg.decode() if msg else ""
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise IcapError(f"{name} failed ({rc}): {last_error()}")
+
+
+_device_checked = set()
+
+
+def require_device(dev: torch.device) -> None:
+    """Fail loudly unless `dev` is a GPU on which the gfx950 code object loads."""
+    if dev.type != "cuda":
+        raise IcapError(f"icap kernels run on the GPU only (got device {dev}); there is no CPU fallback")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx in _device_checked:
+        return
+    lib = load()
+    with torch.cuda.device(idx):
+        if not lib.icap_device_arch_ok():
+            raise IcapError(f"libicap_hip.so code object not loadable on device {idx}: {last_error()}")
+    _device_checked.add(idx)

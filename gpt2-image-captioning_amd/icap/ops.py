@@ -1,0 +1,305 @@
+"""Thin torch-tensor wrappers over the C-ABI (include/icap.h).
+
+Tensors are PyTorch-owned device memory; every wrapper passes raw pointers,
+element strides and the current HIP stream to libicap_hip.so. No wrapper does
+arithmetic itself and none falls back to PyTorch or the CPU.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from ._lib import AdamWArgs, AttnArgs, GemmArgs, call
+
+Tensor = torch.Tensor
+
+
+def dtype_code(t: torch.dtype) -> int:
+    if t == torch.float32:
+        return L.F32
+    if t == torch.bfloat16:
+        return L.BF16
+    raise L.IcapError(f"unsupported storage dtype {t} (float32 or bfloat16)")
+
+
+def _p(t: Optional[Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _ld(t: Tensor) -> int:
+    if t.dim() == 1:
+        return t.shape[0]
+    if t.stride(-1) != 1:
+        raise L.IcapError("operand must have unit stride in its last dimension")
+    return t.stride(-2)
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _rows(t: Tensor) -> int:
+    return t.shape[0] if t.dim() >= 1 else 1
+
+
+class Dropout:
+    """Dropout descriptor: (p, seed, offset, device seed counter)."""
+
+    __slots__ = ("p", "seed", "offset", "counter")
+
+    def __init__(self, p: float = 0.0, seed: int = 0, offset: int = 0, counter: Optional[Tensor] = None):
+        self.p, self.seed, self.offset, self.counter = float(p), int(seed) & (2**64 - 1), int(offset), counter
+
+    def at(self, offset: int) -> "Dropout":
+        return Dropout(self.p, self.seed, offset, self.counter)
+
+    @property
+    def ptr(self):
+        return None if self.counter is None else self.counter.data_ptr()
+
+
+NO_DROP = Dropout()
+
+
+def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, act: int = L.ACT_NONE,
+         aux: Optional[Tensor] = None, dact: int = L.ACT_NONE, dact_src: Optional[Tensor] = None,
+         resid: Optional[Tensor] = None, alpha: float = 1.0, beta: float = 0.0, drop: Dropout = NO_DROP,
+         M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None) -> Tensor:
+    """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h."""
+    M = A.shape[0] if M is None else M
+    K = A.shape[1] if K is None else K
+    N = B.shape[0] if N is None else N
+    a = GemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.in_dtype = dtype_code(A.dtype)
+    a.c_dtype = dtype_code(out.dtype)
+    if B.dtype != A.dtype:
+        raise L.IcapError("gemm: A and B must share a dtype")
+    a.A, a.lda = A.data_ptr(), _ld(A)
+    a.B, a.ldb = B.data_ptr(), _ld(B)
+    a.C, a.ldc = out.data_ptr(), _ld(out)
+    a.alpha, a.beta = alpha, beta
+    a.bias = _p(bias)
+    a.act = act
+    if aux is not None:
+        a.aux, a.ldaux = aux.data_ptr(), _ld(aux)
+    a.dact = dact
+    if dact_src is not None:
+        a.dact_src, a.ld_dact = dact_src.data_ptr(), _ld(dact_src)
+    if resid is not None:
+        a.resid, a.ldr = resid.data_ptr(), _ld(resid)
+    a.drop_p, a.seed, a.offset, a.seed_ptr = drop.p, drop.seed, drop.offset, drop.ptr
+    call("icap_gemm", C.byref(a), _stream())
+    return out
+
+
+def layernorm_fwd(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, y: Tensor, mean: Optional[Tensor],
+                  rstd: Optional[Tensor], rows: Optional[int] = None) -> Tensor:
+    rows = _rows(x) if rows is None else rows
+    D = gamma.shape[0]
+    call("icap_layernorm_fwd", dtype_code(x.dtype), rows, D, x.data_ptr(), _ld(x), gamma.data_ptr(),
+         beta.data_ptr(), eps, y.data_ptr(), _ld(y), _p(mean), _p(rstd), _stream())
+    return y
+
+
+def layernorm_bwd_workspace(rows: int, D: int) -> int:
+    return int(L.load().icap_layernorm_bwd_workspace_bytes(rows, D))
+
+
+def layernorm_bwd(x: Tensor, gamma: Tensor, mean: Tensor, rstd: Tensor, dy: Tensor, dx: Tensor, *,
+                  dres: Optional[Tensor] = None, dx_drop: Optional[Tensor] = None, drop: Dropout = NO_DROP,
+                  dgamma: Optional[Tensor] = None, dbeta: Optional[Tensor] = None,
+                  workspace: Optional[Tensor] = None, rows: Optional[int] = None) -> Tensor:
+    rows = _rows(x) if rows is None else rows
+    D = gamma.shape[0]
+    call("icap_layernorm_bwd", dtype_code(x.dtype), rows, D, x.data_ptr(), _ld(x), gamma.data_ptr(),
+         mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), _ld(dy), _p(dres), _ld(dres) if dres is not None else 0,
+         dx.data_ptr(), _ld(dx), _p(dx_drop), drop.p, drop.seed, drop.offset, drop.ptr, _p(dgamma), _p(dbeta),
+         _p(workspace), _stream())
+    return dx
+
+
+def _attn_args(qkv: Tensor, B: int, S: int, H: int, hd: int, rsb: int, rss: int, scale: float, causal: bool,
+               key_mask: Optional[Tensor], lse: Optional[Tensor], drop: Dropout) -> AttnArgs:
+    a = AttnArgs()
+    a.dtype = dtype_code(qkv.dtype)
+    a.B, a.S, a.H, a.hd = B, S, H, hd
+    a.row_stride_b, a.row_stride_s = rsb, rss
+    a.qkv, a.ld_qkv = qkv.data_ptr(), _ld(qkv)
+    a.lse = _p(lse)
+    a.key_mask = _p(key_mask)
+    a.causal = 1 if causal else 0
+    a.scale = scale
+    a.drop_p, a.seed, a.offset, a.seed_ptr = drop.p, drop.seed, drop.offset, drop.ptr
+    return a
+
+
+def attention_fwd(qkv: Tensor, out: Tensor, *, B: int, S: int, H: int, hd: int, scale: float,
+                  causal: bool = False, key_mask: Optional[Tensor] = None, lse: Optional[Tensor] = None,
+                  drop: Dropout = NO_DROP, rsb: Optional[int] = None, rss: int = 1) -> Tensor:
+    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop)
+    a.out, a.ld_out = out.data_ptr(), _ld(out)
+    call("icap_attention_fwd", C.byref(a), _stream())
+    return out
+
+
+def attention_bwd(qkv: Tensor, dout: Tensor, lse: Tensor, dqkv: Tensor, *, B: int, S: int, H: int, hd: int,
+                  scale: float, causal: bool = False, key_mask: Optional[Tensor] = None, drop: Dropout = NO_DROP,
+                  rsb: Optional[int] = None, rss: int = 1) -> Tensor:
+    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop)
+    a.dout, a.ld_dout = dout.data_ptr(), _ld(dout)
+    a.dqkv, a.ld_dqkv = dqkv.data_ptr(), _ld(dqkv)
+    call("icap_attention_bwd", C.byref(a), _stream())
+    return dqkv
+
+
+def attention_decode(cache: Tensor, out: Tensor, *, B: int, H: int, hd: int, pos: int, scale: float) -> Tensor:
+    call("icap_attention_decode", dtype_code(cache.dtype), B, H, hd, pos, cache.data_ptr(), _ld(cache),
+         out.data_ptr(), _ld(out), scale, _stream())
+    return out
+
+
+def gpt2_embed(prefix: Optional[Tensor], prefix_bstride: int, wte: Tensor, wpe: Tensor, ids: Optional[Tensor],
+               x: Tensor, *, B: int, P: int, L_: int, D: int, drop: Dropout = NO_DROP) -> Tensor:
+    call("icap_gpt2_embed", dtype_code(x.dtype), B, P, L_, D, _p(prefix), prefix_bstride, wte.data_ptr(),
+         wpe.data_ptr(), _p(ids), x.data_ptr(), drop.p, drop.seed, drop.offset, drop.ptr, _stream())
+    return x
+
+
+def caption_prep(B: int, P: int, L_: int, mask: Optional[Tensor], labels: Optional[Tensor],
+                 key_mask: Optional[Tensor], labels_shift: Optional[Tensor], n_valid: Optional[Tensor]) -> None:
+    for t in (mask, labels):
+        if t is not None and t.dtype != torch.int64:
+            raise L.IcapError("caption_prep: mask/labels must be int64")
+    call("icap_caption_prep", B, P, L_, _p(mask), _p(labels), _p(key_mask), _p(labels_shift), _p(n_valid),
+         _stream())
+
+
+def cross_entropy_workspace(rows: int) -> int:
+    return int(L.load().icap_cross_entropy_workspace_bytes(rows))
+
+
+def cross_entropy(logits: Tensor, V: int, labels: Tensor, n_valid: Tensor, loss: Tensor,
+                  dlogits: Optional[Tensor], workspace: Tensor, grad_scale: float = 1.0,
+                  rows: Optional[int] = None) -> Tensor:
+    rows = logits.shape[0] if rows is None else rows
+    call("icap_cross_entropy", dtype_code(logits.dtype), rows, V, logits.data_ptr(), _ld(logits),
+         labels.data_ptr(), n_valid.data_ptr(), loss.data_ptr(), _p(dlogits), grad_scale, workspace.data_ptr(),
+         _stream())
+    return loss
+
+
+def adamw_workspace(n: int) -> int:
+    return int(L.load().icap_adamw_workspace_bytes(n))
+
+
+def adamw_step(params: Tensor, grads: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor, state: Tensor,
+               workspace: Tensor, *, lr: float, betas=(0.9, 0.999), eps: float = 1e-8,
+               weight_decay: float = 0.01, max_norm: float = 1.0, num_warmup_steps: int = 0,
+               num_training_steps: int = 1, bf16_out: Optional[Tensor] = None) -> None:
+    a = AdamWArgs()
+    a.n = params.numel()
+    a.params, a.grads, a.exp_avg, a.exp_avg_sq = (params.data_ptr(), grads.data_ptr(), exp_avg.data_ptr(),
+                                                  exp_avg_sq.data_ptr())
+    a.bf16_out = _p(bf16_out)
+    a.state = state.data_ptr()
+    a.lr, a.beta1, a.beta2, a.eps, a.weight_decay = lr, betas[0], betas[1], eps, weight_decay
+    a.max_norm = max_norm
+    a.num_warmup_steps, a.num_training_steps = num_warmup_steps, num_training_steps
+    call("icap_adamw_step", C.byref(a), workspace.data_ptr(), _stream())
+
+
+def sqnorm(x: Tensor, out: Tensor, workspace: Tensor) -> Tensor:
+    call("icap_sqnorm", x.numel(), x.data_ptr(), out.data_ptr(), workspace.data_ptr(), _stream())
+    return out
+
+
+def transpose(src: Tensor, dst: Tensor, rows_pad: Optional[int] = None, rows: Optional[int] = None,
+              cols: Optional[int] = None) -> Tensor:
+    rows = src.shape[0] if rows is None else rows
+    cols = src.shape[1] if cols is None else cols
+    call("icap_transpose", dtype_code(src.dtype), rows, cols, src.data_ptr(), _ld(src), dst.data_ptr(), _ld(dst),
+         rows if rows_pad is None else rows_pad, _stream())
+    return dst
+
+
+def colsum_workspace(M: int, N: int) -> int:
+    return int(L.load().icap_colsum_workspace_bytes(M, N))
+
+
+def colsum(src: Tensor, out: Tensor, workspace: Tensor, accumulate: bool = True, M: Optional[int] = None,
+           N: Optional[int] = None) -> Tensor:
+    M = src.shape[0] if M is None else M
+    N = src.shape[1] if N is None else N
+    call("icap_colsum", dtype_code(src.dtype), M, N, src.data_ptr(), _ld(src), out.data_ptr(),
+         1 if accumulate else 0, workspace.data_ptr(), _stream())
+    return out
+
+
+def dropout_apply(src: Tensor, dst: Tensor, drop: Dropout, M: Optional[int] = None,
+                  N: Optional[int] = None) -> Tensor:
+    M = src.shape[0] if M is None else M
+    N = src.shape[1] if N is None else N
+    call("icap_dropout_apply", dtype_code(src.dtype), M, N, src.data_ptr(), _ld(src), dst.data_ptr(), _ld(dst),
+         drop.p, drop.seed, drop.offset, drop.ptr, _stream())
+    return dst
+
+
+def counter_increment(counter: Tensor) -> None:
+    call("icap_counter_increment", counter.data_ptr(), _stream())
+
+
+def convert(src: Tensor, dst: Tensor) -> Tensor:
+    """dst = src cast to dst.dtype (2-D, strided rows)."""
+    s2 = src if src.dim() == 2 else src.reshape(-1, src.shape[-1])
+    d2 = dst if dst.dim() == 2 else dst.reshape(-1, dst.shape[-1])
+    call("icap_convert", dtype_code(src.dtype), dtype_code(dst.dtype), s2.shape[0], s2.shape[1], s2.data_ptr(),
+         _ld(s2), d2.data_ptr(), _ld(d2), _stream())
+    return dst
+
+
+def broadcast_rows(src: Tensor, dst: Tensor, B: int, dst_bstride: int) -> Tensor:
+    R, D = src.shape
+    call("icap_broadcast_rows", dtype_code(dst.dtype), B, R, D, src.data_ptr(), dst.data_ptr(), dst_bstride,
+         _stream())
+    return dst
+
+
+def im2col_patches(pixels: Tensor, patches: Tensor, patch: int) -> Tensor:
+    B, Cc, H, W = pixels.shape
+    if H != W or pixels.dtype != torch.float32 or not pixels.is_contiguous():
+        raise L.IcapError("im2col_patches: pixels must be contiguous fp32 [B,C,H,H]")
+    call("icap_im2col_patches", dtype_code(patches.dtype), B, Cc, H, patch, pixels.data_ptr(), patches.data_ptr(),
+         _stream())
+    return patches
+
+
+def vit_embed(patch_emb: Tensor, cls: Tensor, pos: Tensor, x: Tensor, B: int, G2: int, D: int) -> Tensor:
+    call("icap_vit_embed", dtype_code(x.dtype), B, G2, D, patch_emb.data_ptr(), cls.data_ptr(), pos.data_ptr(),
+         x.data_ptr(), _stream())
+    return x
+
+
+def l2norm_rows(x: Tensor, out: Tensor, rows: Optional[int] = None) -> Tensor:
+    rows = x.shape[0] if rows is None else rows
+    call("icap_l2norm_rows", dtype_code(x.dtype), rows, x.shape[-1], x.data_ptr(), _ld(x), out.data_ptr(),
+         _ld(out), _stream())
+    return out
+
+
+def greedy_next(logits: Tensor, V: int, eos: int, finished: Tensor, tokens: Tensor, step: int,
+                wte: Optional[Tensor], wpe: Optional[Tensor], pos: int, D: int, x: Optional[Tensor]) -> None:
+    B = finished.shape[0]
+    call("icap_greedy_next", dtype_code(logits.dtype), B, V, logits.data_ptr(), _ld(logits), eos,
+         finished.data_ptr(), tokens.data_ptr(), _ld(tokens), step, _p(wte), _p(wpe), pos, D, _p(x), _stream())
+
+
+def add_position(src: Tensor, src_bstride: int, src_tstride: int, wpe: Tensor, x: Tensor, *, B: int, npos: int,
+                 D: int, pos0: int) -> Tensor:
+    call("icap_add_position", dtype_code(x.dtype), B, npos, D, src.data_ptr(), src_bstride, src_tstride,
+         wpe.data_ptr(), pos0, x.data_ptr(), _stream())
+    return x

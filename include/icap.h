@@ -1,0 +1,260 @@
+/*
+ * icap.h — C-ABI of libicap_hip.so, the MI355X-native (gfx950) hot path of the
+ * prefix image-captioning trainer (reference: thenoobychocobo/gpt2-image-captioning).
+ *
+ * The reference has no FFI of its own: its seam is the Python module surface of
+ * src/models.py / src/train.py, and all of its device arithmetic happens inside
+ * HF transformers + ATen. Each entry point below replaces one piece of that
+ * arithmetic; the reference call site it stands in for is cited per function
+ * (paths relative to the reference root; HF/ = transformers/, TORCH/ = torch/).
+ *
+ * Conventions
+ *  - Plain device pointers + int64 sizes/strides, no torch types. Strides are in
+ *    ELEMENTS. Storage dtype is ICAP_F32 (parity mode) or ICAP_BF16 (perf mode);
+ *    every kernel computes in fp32. Biases, LayerNorm affine params, optimizer
+ *    state and loss outputs are always fp32.
+ *  - `stream` is a hipStream_t passed as void*. Every call is asynchronous and
+ *    stream-ordered; no call allocates, frees or synchronises, so a sequence of
+ *    calls can be captured into a hipGraph. Caller-owned workspaces are sized by
+ *    the *_workspace_bytes queries.
+ *  - Return 0 on success, nonzero ICAP_ERR_* on failure; icap_last_error()
+ *    returns a thread-local message for the last failure on the calling thread.
+ *  - Dropout: keep(i) = hash(seed', offset + i) >= p*2^32, scale 1/(1-p); the
+ *    index i is the row-major element index of the tensor the mask applies to,
+ *    so forward and backward regenerate identical masks. p == 0 disables it.
+ *    seed' = seed + (seed_ptr ? *seed_ptr * 0x9E3779B97F4A7C15 : 0): a device
+ *    counter (icap_counter_increment) lets a captured graph draw fresh masks
+ *    on every replay.
+ */
+#ifndef ICAP_H
+#define ICAP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ICAP_F32 = 0, ICAP_BF16 = 1 };
+enum {
+  ICAP_ACT_NONE = 0,
+  ICAP_ACT_GELU_NEW = 1,   /* HF/activations.py:59-66 (GPT-2 gelu_new)        */
+  ICAP_ACT_RELU = 2,       /* TORCH/nn/modules/transformer.py (mapper FFN)     */
+  ICAP_ACT_QUICK_GELU = 3, /* HF/activations.py:117-123 (CLIP)                 */
+  ICAP_ACT_TANH = 4        /* src/models.py:29 (MLPMappingNetwork activation)  */
+};
+enum { ICAP_OK = 0, ICAP_ERR_ARG = 1, ICAP_ERR_LAUNCH = 2 };
+
+const char* icap_last_error(void);
+int icap_version(void);
+/* number of device kernels compiled into the library (>0 when the gfx950 code object loaded) */
+int icap_device_arch_ok(void);
+
+/* ------------------------------------------------------------------------- */
+/* GEMM: C[M,N] = epi(alpha * A[M,K] . B[N,K]^T)                              */
+/* Replaces every dense contraction of the path: GPT-2 Conv1D c_attn/c_proj/  */
+/* c_fc/mlp.c_proj (HF/models/gpt2/modeling_gpt2.py:185,223,238-241;          */
+/* HF/pytorch_utils.py:117-121), the tied LM head (modeling_gpt2.py:698),     */
+/* the mapper Linear + encoder projections (src/models.py:119,129-139,154),   */
+/* MLPMappingNetwork (src/models.py:52-56), CLIP patch-embed/q,k,v/out/fc1/fc2/*/
+/* visual_projection (HF/models/clip/modeling_clip.py:148-154,280-350,751),   */
+/* and every backward dX / dW product of train.py:145.                         */
+/* Both operands are K-contiguous (row-major A, row-major B = "weight [out,in]").*/
+/* Epilogue order (forward): v = alpha*acc + bias[n];                          */
+/*   if aux: aux[m,n] = (act==TANH ? act(v) : v);  v = act(v);                 */
+/*   v *= dropmask(m*N+n);  if resid: v += resid[m,n];  C = beta*C + v.        */
+/* Backward epilogue (dact != NONE): v = alpha*acc * dropmask * act'(dact_src).*/
+/* Constraints: K % 8 == 0 (bf16) / K % 4 == 0 (f32); lda,ldb multiples of 8/4;*/
+/* beta != 0 only with f32 C.                                                  */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  int64_t M, N, K;
+  int32_t in_dtype;   /* dtype of A and B */
+  int32_t c_dtype;    /* dtype of C, aux, resid, dact_src */
+  const void* A; int64_t lda;
+  const void* B; int64_t ldb;
+  void* C; int64_t ldc;
+  float alpha, beta;
+  const float* bias;  /* [N] or NULL */
+  int32_t act;        /* ICAP_ACT_* forward activation */
+  void* aux; int64_t ldaux;             /* store of pre-activation (or tanh output) or NULL */
+  int32_t dact;                          /* backward: multiply by act'(dact_src) */
+  const void* dact_src; int64_t ld_dact;
+  const void* resid; int64_t ldr;        /* residual added last, or NULL */
+  float drop_p; uint64_t seed; uint64_t offset;
+  const uint64_t* seed_ptr;               /* optional device seed counter */
+} icap_gemm_args;
+int icap_gemm(const icap_gemm_args* a, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* LayerNorm over the last dim D (eps given; GPT-2 ln_1/ln_2/ln_f             */
+/* modeling_gpt2.py:252-254,497,620; mapper norm1/norm2 TORCH transformer.py  */
+/* :946-950; CLIP pre/post/layer_norm1/2 modeling_clip.py:641-651,365-384).   */
+/* y = (x-mean)*rstd*gamma + beta; mean/rstd (fp32 [rows]) saved for backward. */
+/* D % 4 == 0, D <= 1024.                                                      */
+/* ------------------------------------------------------------------------- */
+int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
+                       const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
+                       float* mean, float* rstd, void* stream);
+/* dx = LN'(x)^T dy [+ dres];  optional dx_drop = dx * dropmask(p,seed,offset)  */
+/* (the residual-dropout backward of the producing layer, fused);             */
+/* optional dgamma/dbeta (+= into fp32 [D]) via a caller workspace of          */
+/* icap_layernorm_bwd_workspace_bytes(rows, D) bytes.                           */
+size_t icap_layernorm_bwd_workspace_bytes(int64_t rows, int64_t D);
+int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
+                       const float* gamma, const float* mean, const float* rstd,
+                       const void* dy, int64_t lddy, const void* dres, int64_t lddres,
+                       void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
+                       uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
+                       void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Multi-head softmax attention over a fused QKV activation.                  */
+/* GPT-2: causal + key padding (HF/integrations/sdpa_attention.py:79-166,     */
+/* HF/masking_utils.py:76-80,168-180), attn dropout modeling_gpt2.py:87;      */
+/* mapper MHA (TORCH/nn/modules/activation.py, bidirectional, hd 96);         */
+/* CLIP (modeling_clip.py:280-335, bidirectional).                            */
+/* Row of token (b,s) = b*row_stride_b + s*row_stride_s in qkv/out/dqkv/dout. */
+/* q at column h*hd, k at D+h*hd, v at 2D+h*hd (D = H*hd).                     */
+/* allowed(q,k) = (!causal || k<=q) && (!key_mask || key_mask[b*S+k]).         */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t dtype;
+  int32_t B, S, H, hd;
+  int64_t row_stride_b, row_stride_s;
+  const void* qkv; int64_t ld_qkv;
+  void* out; int64_t ld_out;
+  float* lse;               /* [B*H*S] fp32 log-sum-exp of scaled scores, or NULL */
+  const int32_t* key_mask;  /* [B*S] or NULL */
+  int32_t causal;
+  float scale;
+  float drop_p; uint64_t seed; uint64_t offset; /* dropout on P, index (b*H+h)*S*S + q*S + k */
+  const uint64_t* seed_ptr;
+  /* backward only */
+  const void* dout; int64_t ld_dout;
+  void* dqkv; int64_t ld_dqkv;
+} icap_attn_args;
+int icap_attention_fwd(const icap_attn_args* a, void* stream);
+int icap_attention_bwd(const icap_attn_args* a, void* stream);
+
+/* Decode-step attention (KV-cached greedy decode; replaces the full          */
+/* recompute of src/models.py:395 with an exactly-equivalent causal step).    */
+/* cache rows are position-major: row of (b, t) = t*B + b, ld = 3*D (fused qkv).*/
+/* The new token is at position `pos`; attends to keys 0..pos.                 */
+int icap_attention_decode(int32_t dtype, int32_t B, int32_t H, int32_t hd, int32_t pos,
+                          const void* cache, int64_t ld_cache, void* out, int64_t ld_out,
+                          float scale, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Caption/prefix assembly for the GPT-2 input (src/models.py:261,283-317,    */
+/* modeling_gpt2.py:571-577,604):                                               */
+/*   x[b,t] = (t<P ? prefix[b*prefix_bstride + t*D] : wte[ids[b,t-P]]) + wpe[t]*/
+/*   then embd dropout.  key_mask[b,t] = t<P ? 1 : mask[b,t-P] (1 if mask NULL)*/
+/*   labels_shift[b*S+t] = t+1<S ? (t+1<P ? -100 : labels[b,t+1-P]) : -100    */
+/*   (HF/loss/loss_utils.py:49-71 shift).  S = P + L. ids/mask/labels int64.   */
+/* ------------------------------------------------------------------------- */
+int icap_gpt2_embed(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D,
+                    const void* prefix, int64_t prefix_bstride, const void* wte,
+                    const void* wpe, const int64_t* ids, void* x, float drop_p,
+                    uint64_t seed, uint64_t offset, const uint64_t* seed_ptr, void* stream);
+int icap_caption_prep(int32_t B, int32_t P, int32_t L, const int64_t* mask,
+                      const int64_t* labels, int32_t* key_mask, int32_t* labels_shift,
+                      int32_t* n_valid, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Causal-LM cross entropy fused with its backward (HF/loss/loss_utils.py     */
+/* :32-46,49-71): per row r with label y != -100 over V classes:               */
+/*   loss_r = lse(x_r) - x_r[y];  loss = sum(loss_r)/n_valid                   */
+/*   dlogits_r = grad_scale*(softmax(x_r) - onehot(y))/n_valid (0 for ignored  */
+/*   rows and for padding columns V..ld). dlogits may alias logits. n_valid is */
+/*   read from device memory (written by icap_caption_prep).                   */
+/* ------------------------------------------------------------------------- */
+size_t icap_cross_entropy_workspace_bytes(int64_t rows);
+int icap_cross_entropy(int32_t dtype, int64_t rows, int64_t V, const void* logits, int64_t ld,
+                       const int32_t* labels, const int32_t* n_valid, float* loss,
+                       void* dlogits, float grad_scale, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Global grad-norm clip + AdamW + linear LR schedule over ONE flat fp32       */
+/* parameter buffer (src/train.py:94-103,150-159; TORCH/nn/utils/clip_grad.py */
+/* :121-186; TORCH/optim/adam.py:419,457,476,499,545-547;                       */
+/* HF/optimization.py:101-107). Step counter and lr live in device memory     */
+/* (`state`, 64 bytes, zero-initialised by the caller) so the call is graph-   */
+/* capturable. bf16_out (optional) receives the updated params in bf16.        */
+/* state layout (float/int64 view): [0]=int64 step (completed steps),         */
+/* [2]=f32 last grad norm, [3]=f32 clip coef, [4]=f32 lr used, [5]=f32 step   */
+/* size lr/bc1, [6]=f32 sqrt(bc2), [7]=f32 decay factor 1-lr*wd.              */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  int64_t n;
+  float* params; float* grads; float* exp_avg; float* exp_avg_sq;
+  void* bf16_out;           /* or NULL */
+  void* state;              /* 64-byte device state */
+  float lr, beta1, beta2, eps, weight_decay;
+  float max_norm;           /* <= 0 disables clipping */
+  int64_t num_warmup_steps, num_training_steps;
+} icap_adamw_args;
+size_t icap_adamw_workspace_bytes(int64_t n);
+int icap_adamw_step(const icap_adamw_args* a, void* workspace, void* stream);
+/* sum of squares of a flat fp32 buffer -> out[0] (deterministic) */
+int icap_sqnorm(int64_t n, const float* x, float* out, void* workspace, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Layout / reduction helpers used by the backward pass.                      */
+/* ------------------------------------------------------------------------- */
+/* dst[c*ldd + r] = src[r*lds + c] for r<rows, c<cols; zero for rows<=r<rows_pad */
+int icap_transpose(int32_t dtype, int64_t rows, int64_t cols, const void* src, int64_t lds,
+                   void* dst, int64_t ldd, int64_t rows_pad, void* stream);
+/* out[n] (+)= sum_m src[m*ld + n]  (bias grads, prefix_const grad); fp32 out */
+size_t icap_colsum_workspace_bytes(int64_t M, int64_t N);
+int icap_colsum(int32_t dtype, int64_t M, int64_t N, const void* src, int64_t ld, float* out,
+                int32_t accumulate, void* workspace, void* stream);
+/* dst[m, n] = src[m, n] * dropmask(p, seed, offset + m*N + n) (or plain copy) */
+int icap_dropout_apply(int32_t dtype, int64_t M, int64_t N, const void* src, int64_t lds,
+                       void* dst, int64_t ldd, float drop_p, uint64_t seed, uint64_t offset,
+                       const uint64_t* seed_ptr, void* stream);
+/* *counter += 1 (device-side dropout seed counter, graph-capturable) */
+int icap_counter_increment(uint64_t* counter, void* stream);
+/* dtype conversion copy, strided rows: dst = (dst_dtype) src */
+int icap_convert(int32_t src_dtype, int32_t dst_dtype, int64_t M, int64_t N, const void* src,
+                 int64_t lds, void* dst, int64_t ldd, void* stream);
+/* dst[b, r, :] = src[r, :] for b < B (broadcast fp32 rows into a strided dtype tensor):  */
+/* mapper prefix_const expand (src/models.py:163-168).                                    */
+int icap_broadcast_rows(int32_t dtype, int32_t B, int64_t R, int64_t D, const float* src,
+                        void* dst, int64_t dst_bstride, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* CLIP ViT image tower helpers (HF/models/clip/modeling_clip.py:148-219,     */
+/* 650-651,751; src/embeddings/clip.py:132-137).                              */
+/* ------------------------------------------------------------------------- */
+/* patches[(b*G*G + gy*G + gx), c*p*p + ky*p + kx] = pixels[b, c, gy*p+ky, gx*p+kx] (fp32 in) */
+int icap_im2col_patches(int32_t dtype, int32_t B, int32_t C, int32_t HW, int32_t patch,
+                        const float* pixels, void* patches, void* stream);
+/* x[b, 0] = cls + pos[0];  x[b, 1+i] = patch_emb[b*G2 + i] + pos[1+i] */
+int icap_vit_embed(int32_t dtype, int32_t B, int32_t G2, int32_t D, const void* patch_emb,
+                   const float* cls, const float* pos, void* x, void* stream);
+/* out[b] = x[b] / ||x[b]||_2 (fp32 out) */
+int icap_l2norm_rows(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
+                     float* out, int64_t ldo, void* stream);
+
+/* ------------------------------------------------------------------------- */
+/* Greedy-decode step helpers (src/models.py:389-469).                        */
+/* ------------------------------------------------------------------------- */
+/* next[b] = finished[b] ? eos : argmax_v(logits[b, :V]) (first max on ties);  */
+/* finished[b] |= next[b]==eos; tokens[b*ld_tokens + step] = next[b];          */
+/* x[b] = wte[next[b]] + wpe[pos] (the next step's input embedding).           */
+int icap_greedy_next(int32_t dtype, int32_t B, int64_t V, const void* logits, int64_t ld,
+                     int64_t eos, int32_t* finished, int64_t* tokens, int64_t ld_tokens,
+                     int32_t step, const void* wte, const void* wpe, int32_t pos, int32_t D,
+                     void* x, void* stream);
+/* x[(t*B + b)*D + d] = src[b*src_bstride + t*src_tstride + d] + wpe[(pos0+t)*D + d], t < npos */
+/* (prefix rows into the position-major decode input, modeling_gpt2.py:571-577).            */
+int icap_add_position(int32_t dtype, int32_t B, int32_t npos, int32_t D, const void* src,
+                      int64_t src_bstride, int64_t src_tstride, const void* wpe, int32_t pos0,
+                      void* x, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ICAP_H */

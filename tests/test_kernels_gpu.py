@@ -1,0 +1,270 @@
+"""Kernel-level numerics of libicap_hip.so vs plain PyTorch fp64 references of the same op.
+
+Each reference here is the textbook definition of the op the reference model reaches
+through HF transformers / torch (cited per test); tolerances are written per test.
+"""
+
+import math
+
+import pytest
+import torch
+
+from icap import _lib as L
+from icap import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(shape, dev, dtype=torch.float32, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(device=dev, dtype=dtype)
+
+
+def rel_err(a, b):
+    a = a.double()
+    b = b.double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (130, 200, 72), (520, 2304, 768), (7, 50304, 768), (333, 96, 3072)])
+def test_gemm_plain(dev, dtype, M, N, K):
+    A = rnd((M, K), dev, dtype, seed=1)
+    B = rnd((N, K), dev, dtype, seed=2)
+    C = torch.empty((M, N), device=dev, dtype=torch.float32)
+    ops.gemm(A, B, C)
+    ref = A.double() @ B.double().t()
+    # fp32 inputs: exact-fp32 MFMA chain; bf16 inputs: exact products, fp32 accumulation
+    tol = 2e-6 if dtype == torch.float32 else 1e-5
+    err = ((C.double() - ref).abs() / (A.double().abs() @ B.double().abs().t())).max().item()
+    assert err < tol, err
+
+
+def test_gemm_strided_and_beta(dev):
+    A_full = rnd((64, 200), dev, seed=3)
+    B_full = rnd((96, 300), dev, seed=4)
+    A = A_full[:, 8:8 + 128]
+    B = B_full[:, 0:128]
+    C0 = rnd((64, 96), dev, seed=5)
+    C = C0.clone()
+    ops.gemm(A, B, C, alpha=0.5, beta=1.0)
+    ref = C0.double() + 0.5 * (A.double() @ B.double().t())
+    assert rel_err(C, ref) < 1e-5
+
+
+@pytest.mark.parametrize("act", [L.ACT_GELU_NEW, L.ACT_RELU, L.ACT_QUICK_GELU, L.ACT_TANH])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dev, act, dtype):
+    M, N, K = 200, 384, 256
+    A = rnd((M, K), dev, dtype, 0.1, seed=6)
+    B = rnd((N, K), dev, dtype, 0.1, seed=7)
+    bias = rnd((N,), dev, scale=0.5, seed=8)
+    resid = rnd((M, N), dev, dtype, seed=9)
+    C = torch.empty((M, N), device=dev, dtype=dtype)
+    aux = torch.empty((M, N), device=dev, dtype=dtype)
+    ops.gemm(A, B, C, bias=bias, act=act, aux=aux, resid=resid)
+    z = A.double() @ B.double().t() + bias.double()
+    if act == L.ACT_GELU_NEW:  # HF/activations.py:59-66
+        y = 0.5 * z * (1 + torch.tanh(math.sqrt(2 / math.pi) * (z + 0.044715 * z ** 3)))
+        dy = None
+    elif act == L.ACT_RELU:
+        y = torch.relu(z)
+    elif act == L.ACT_QUICK_GELU:  # HF/activations.py:117-123
+        y = z * torch.sigmoid(1.702 * z)
+    else:
+        y = torch.tanh(z)
+    ref = y + resid.double()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(C, ref) < tol
+    aux_ref = y if act == L.ACT_TANH else z
+    assert rel_err(aux, aux_ref) < tol
+    # backward epilogue: dZ = (G @ W) * act'(aux)
+    G = rnd((M, 64), dev, dtype, seed=10)
+    W = rnd((N, 64), dev, dtype, seed=11)
+    dZ = torch.empty((M, N), device=dev, dtype=dtype)
+    ops.gemm(G, W, dZ, dact=act, dact_src=aux)
+    zz = aux.double()
+    if act == L.ACT_GELU_NEW:
+        zr = zz.clone().requires_grad_(True)
+        yy = 0.5 * zr * (1 + torch.tanh(math.sqrt(2 / math.pi) * (zr + 0.044715 * zr ** 3)))
+        d = torch.autograd.grad(yy.sum(), zr)[0]
+    elif act == L.ACT_RELU:
+        d = (zz > 0).double()
+    elif act == L.ACT_QUICK_GELU:
+        zr = zz.clone().requires_grad_(True)
+        d = torch.autograd.grad((zr * torch.sigmoid(1.702 * zr)).sum(), zr)[0]
+    else:
+        d = 1 - zz * zz
+    ref = (G.double() @ W.double().t()) * d
+    assert rel_err(dZ, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+def test_gemm_dropout_statistics(dev):
+    M, N, K = 512, 512, 64
+    A = torch.ones((M, K), device=dev)
+    B = torch.full((N, K), 1.0 / K, device=dev)
+    C = torch.empty((M, N), device=dev)
+    ops.gemm(A, B, C, drop=ops.Dropout(0.1, seed=1234))
+    kept = (C != 0).double().mean().item()
+    assert abs(kept - 0.9) < 0.005
+    assert torch.allclose(C[C != 0], torch.full_like(C[C != 0], 1 / 0.9), rtol=1e-6)
+    C2 = torch.empty_like(C)
+    ops.gemm(A, B, C2, drop=ops.Dropout(0.1, seed=1234))
+    assert torch.equal(C, C2)  # deterministic mask
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm(dev, dtype):
+    rows, D = 333, 768
+    x = rnd((rows, D), dev, dtype, 2.0, seed=12) + 0.5
+    g = rnd((D,), dev, seed=13) * 0.2 + 1
+    b = rnd((D,), dev, seed=14) * 0.1
+    y = torch.empty_like(x)
+    mean = torch.empty(rows, device=dev)
+    rstd = torch.empty(rows, device=dev)
+    ops.layernorm_fwd(x, g, b, 1e-5, y, mean, rstd)
+    xr = x.double().requires_grad_(True)
+    gr = g.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), gr, br, 1e-5)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(y, yr) < tol
+    dy = rnd((rows, D), dev, dtype, seed=15)
+    dres = rnd((rows, D), dev, dtype, seed=16)
+    dx = torch.empty_like(x)
+    dg = torch.zeros(D, device=dev)
+    db = torch.zeros(D, device=dev)
+    ws = torch.empty(ops.layernorm_bwd_workspace(rows, D), dtype=torch.uint8, device=dev)
+    ops.layernorm_bwd(x, g, mean, rstd, dy, dx, dres=dres, dgamma=dg, dbeta=db, workspace=ws)
+    gx, gg, gb = torch.autograd.grad(yr, (xr, gr, br), dy.double())
+    assert rel_err(dx, gx + dres.double()) < (1e-5 if dtype == torch.float32 else 2e-2)
+    assert rel_err(dg, gg) < (1e-5 if dtype == torch.float32 else 1e-2)
+    assert rel_err(db, gb) < 1e-5
+
+
+def ref_attention(q, k, v, scale, causal, key_mask):
+    # q,k,v: [B,H,S,hd] float64; mask rule HF/masking_utils.py:76-80 (causal) & padding
+    s = (q @ k.transpose(-1, -2)) * scale
+    S = q.shape[-2]
+    allowed = torch.ones((S, S), dtype=torch.bool, device=q.device)
+    if causal:
+        allowed = torch.tril(allowed)
+    allowed = allowed[None, None]
+    if key_mask is not None:
+        allowed = allowed & key_mask.bool()[:, None, None, :]
+    s = s.masked_fill(~allowed, float("-inf"))
+    p = torch.softmax(s, -1)
+    return p @ v
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,S,H,hd,causal,masked", [(3, 65, 12, 64, True, True), (2, 25, 8, 96, False, False),
+                                                    (2, 50, 12, 64, False, False)])
+def test_attention(dev, dtype, B, S, H, hd, causal, masked):
+    D = H * hd
+    qkv = rnd((B * S, 3 * D), dev, dtype, seed=20)
+    key_mask = None
+    if masked:
+        km = torch.ones((B, S), dtype=torch.int32)
+        km[0, 30:] = 0
+        km[1, 40:] = 0
+        key_mask = km.to(dev)
+    out = torch.empty((B * S, D), device=dev, dtype=dtype)
+    lse = torch.empty(B * H * S, device=dev)
+    scale = 1.0 / math.sqrt(hd)
+    ops.attention_fwd(qkv, out, B=B, S=S, H=H, hd=hd, scale=scale, causal=causal, key_mask=key_mask, lse=lse)
+    x = qkv.double().view(B, S, 3, H, hd).permute(2, 0, 3, 1, 4).requires_grad_(True)
+    o = ref_attention(x[0], x[1], x[2], scale, causal, key_mask)
+    o2 = o.permute(0, 2, 1, 3).reshape(B * S, D)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(out, o2) < tol
+    dout = rnd((B * S, D), dev, dtype, seed=21)
+    dqkv = torch.empty_like(qkv)
+    ops.attention_bwd(qkv, dout, lse, dqkv, B=B, S=S, H=H, hd=hd, scale=scale, causal=causal, key_mask=key_mask)
+    (gx,) = torch.autograd.grad(o2, x, dout.double())
+    g = gx.permute(1, 3, 0, 2, 4).reshape(B * S, 3 * D)
+    assert rel_err(dqkv, g) < (1e-5 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_attention_decode_matches_full(dev, dtype):
+    B, H, hd, T = 4, 12, 64, 20
+    D = H * hd
+    qkv = rnd((T * B, 3 * D), dev, dtype, seed=22)  # position-major rows t*B+b
+    out = torch.empty((B, D), device=dev, dtype=dtype)
+    pos = T - 1
+    ops.attention_decode(qkv, out, B=B, H=H, hd=hd, pos=pos, scale=0.125)
+    x = qkv.double().view(T, B, 3, H, hd).permute(2, 1, 3, 0, 4)  # [3,B,H,T,hd]
+    o = ref_attention(x[0], x[1], x[2], 0.125, True, None)[:, :, pos]  # [B,H,hd]
+    assert rel_err(out, o.reshape(B, D)) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cross_entropy(dev, dtype):
+    rows, V, ld = 130, 50257, 50304
+    logits = torch.zeros((rows, ld), device=dev, dtype=dtype)
+    logits[:, :V] = rnd((rows, V), dev, dtype, 3.0, seed=30)
+    g = torch.Generator().manual_seed(31)
+    labels = torch.randint(0, V, (rows,), generator=g, dtype=torch.int32)
+    labels[::3] = -100
+    labels = labels.to(dev)
+    nvalid = (labels != -100).sum().to(torch.int32).reshape(1)
+    loss = torch.empty(1, device=dev)
+    dl = torch.empty_like(logits)
+    ws = torch.empty(ops.cross_entropy_workspace(rows), dtype=torch.uint8, device=dev)
+    ops.cross_entropy(logits, V, labels, nvalid, loss, dl, ws)
+    x = logits[:, :V].double().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(x, labels.long(), ignore_index=-100)  # HF/loss/loss_utils.py:32-46
+    (gx,) = torch.autograd.grad(ref, x)
+    assert abs(loss.item() - ref.item()) < 1e-5 * max(1, abs(ref.item()))
+    assert rel_err(dl[:, :V], gx) < (1e-4 if dtype == torch.float32 else 1e-2)
+    assert torch.all(dl[:, V:] == 0)
+
+
+def test_adamw_matches_torch(dev):
+    n = 100003
+    p0 = rnd((n,), dev, seed=40)
+    steps = 4
+    grads = [rnd((n,), dev, scale=0.01 * (k + 1), seed=41 + k) for k in range(steps)]
+    # reference: clip_grad_norm_ + AdamW + linear schedule (src/train.py:94-103,150-156)
+    pr = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.AdamW([pr], lr=1e-3, weight_decay=0.01)
+    total = 10
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda s: max(0.0, (total - s) / total))
+    P = p0.clone()
+    M1 = torch.zeros_like(P)
+    M2 = torch.zeros_like(P)
+    st = torch.zeros(16, dtype=torch.float32, device=dev)
+    ws = torch.empty(ops.adamw_workspace(n), dtype=torch.uint8, device=dev)
+    out16 = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    for k in range(steps):
+        pr.grad = grads[k].clone()
+        torch.nn.utils.clip_grad_norm_([pr], max_norm=1.0)
+        opt.step()
+        sched.step()
+        ops.adamw_step(P, grads[k].clone(), M1, M2, st, ws, lr=1e-3, weight_decay=0.01, max_norm=1.0,
+                       num_training_steps=total, bf16_out=out16)
+    assert rel_err(P, pr.detach()) < 1e-6
+    assert torch.equal(out16, P.to(torch.bfloat16))
+    assert st[:2].view(torch.int64).item() == steps
+
+
+def test_transpose_colsum_dropout(dev):
+    x = rnd((77, 130), dev, seed=50)
+    t = torch.full((130, 96), 7.0, device=dev)
+    ops.transpose(x, t, rows_pad=96)
+    assert torch.equal(t[:, :77], x.t())
+    assert torch.all(t[:, 77:] == 0)
+    cs = torch.ones(130, device=dev)
+    ws = torch.empty(ops.colsum_workspace(77, 130), dtype=torch.uint8, device=dev)
+    ops.colsum(x, cs, ws, accumulate=True)
+    assert rel_err(cs, 1 + x.double().sum(0)) < 1e-6
+    y = torch.empty_like(x)
+    ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+    ops.dropout_apply(x, y, ops.Dropout(0.5, 99, 0, ctr))
+    y2 = torch.empty_like(x)
+    ops.counter_increment(ctr)
+    ops.dropout_apply(x, y2, ops.Dropout(0.5, 99, 0, ctr))
+    assert not torch.equal(y, y2)
+    m = y != 0
+    assert torch.allclose(y[m], 2 * x[m])
