@@ -1,0 +1,472 @@
+"""ORACLE — test infrastructure only; never imported by the product path.
+
+CPU restatement (PyTorch CPU tensors, no transformers, no HIP) of the reference's
+hot-path arithmetic, used by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the CHECKER. The product (gpt2-image-captioning_amd/icap)
+must never import this module.
+
+Each function cites the reference file:line it restates. Paths are relative to
+the reference root (thenoobychocobo/gpt2-image-captioning @ 2025-12-12); HF/ is
+transformers (pinned 4.57.3 by the reference, uv.lock:3069-3070; 5.15.0 installed
+here, GPT-2 math unchanged), TORCH/ is torch.
+
+Parity pinning: the reference has no tests or golden vectors, so
+this restatement is pinned against golden vectors produced by importing the
+reference itself in the build container (tools/make_goldens.py ->
+tests/golden/*.npz; tests/test_oracle.py checks them).
+
+Weights: the pretrained checkpoints are unavailable offline, so all weights come
+from the closed-form deterministic generator below (splitmix64 over
+(seed, tensor name, element index)); tools/make_goldens.py loads the same
+tensors into the reference modules.
+"""
+
+from __future__ import annotations
+
+import math
+import zlib
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+Tensor = torch.Tensor
+
+# --------------------------------------------------------------------------- configs
+
+
+@dataclass
+class GPT2Cfg:  # HF/models/gpt2/configuration_gpt2.py:84-103 defaults = GPT-2 small
+    n_layer: int = 12
+    n_embd: int = 768
+    n_head: int = 12
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    eps: float = 1e-5
+    eos: int = 50256
+
+
+@dataclass
+class MapperCfg:  # src/models.py:96-139, config.yml:14-19
+    embed_dim: int = 512
+    gpt_dim: int = 768
+    prefix_length: int = 15
+    hidden_length: int = 10
+    num_layers: int = 8
+    nhead: int = 8  # models.py:131
+    eps: float = 1e-5
+
+
+@dataclass
+class MLPMapperCfg:  # src/models.py:23-56
+    prefix_length: int = 15
+    embed_dim: int = 512
+    gpt_dim: int = 768
+
+
+@dataclass
+class ClipCfg:  # HF/models/clip/configuration_clip.py:99-105 (ViT-B/32 vision tower)
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    patch: int = 32
+    image: int = 224
+    inter: int = 3072
+    proj: int = 512
+    eps: float = 1e-5
+    channels: int = 3
+
+
+# --------------------------------------------------------------------------- weights
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix_uniform(seed: int, tag: int, n: int) -> np.ndarray:
+    """n uniforms in [-1, 1) from splitmix64(seed, tag, index) (float64)."""
+    with np.errstate(over="ignore"):
+        base = np.uint64((seed * 0x9E3779B97F4A7C15 + tag * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF)
+        z = base + (np.arange(n, dtype=np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z >> np.uint64(11)).astype(np.float64) * (2.0 / 9007199254740992.0) - 1.0
+
+
+def gen_tensor(seed: int, name: str, shape, std: float, mean: float = 0.0) -> Tensor:
+    """Deterministic fp32 tensor: mean + std * sqrt(3) * U[-1,1)."""
+    n = int(np.prod(shape)) if len(shape) else 1
+    tag = zlib.crc32(name.encode())
+    u = _splitmix_uniform(seed, tag, n)
+    return torch.from_numpy((mean + std * math.sqrt(3.0) * u).astype(np.float32).reshape(shape))
+
+
+def gpt2_state_dict(cfg: GPT2Cfg, seed: int = 0) -> Dict[str, Tensor]:
+    """HF GPT2LMHeadModel parameter names/shapes (Conv1D weights are [in, out])."""
+    d, L = cfg.n_embd, cfg.n_layer
+    sd = {
+        "transformer.wte.weight": gen_tensor(seed, "wte", (cfg.vocab_size, d), 0.02),
+        "transformer.wpe.weight": gen_tensor(seed, "wpe", (cfg.n_positions, d), 0.01),
+        "transformer.ln_f.weight": gen_tensor(seed, "ln_f.w", (d,), 0.05, 1.0),
+        "transformer.ln_f.bias": gen_tensor(seed, "ln_f.b", (d,), 0.02),
+    }
+    proj_std = 0.02 / math.sqrt(2 * L)
+    for i in range(L):
+        p = f"transformer.h.{i}."
+        sd[p + "ln_1.weight"] = gen_tensor(seed, p + "ln_1.w", (d,), 0.05, 1.0)
+        sd[p + "ln_1.bias"] = gen_tensor(seed, p + "ln_1.b", (d,), 0.02)
+        sd[p + "attn.c_attn.weight"] = gen_tensor(seed, p + "c_attn.w", (d, 3 * d), 0.02)
+        sd[p + "attn.c_attn.bias"] = gen_tensor(seed, p + "c_attn.b", (3 * d,), 0.02)
+        sd[p + "attn.c_proj.weight"] = gen_tensor(seed, p + "attn.c_proj.w", (d, d), proj_std)
+        sd[p + "attn.c_proj.bias"] = gen_tensor(seed, p + "attn.c_proj.b", (d,), 0.02)
+        sd[p + "ln_2.weight"] = gen_tensor(seed, p + "ln_2.w", (d,), 0.05, 1.0)
+        sd[p + "ln_2.bias"] = gen_tensor(seed, p + "ln_2.b", (d,), 0.02)
+        sd[p + "mlp.c_fc.weight"] = gen_tensor(seed, p + "c_fc.w", (d, 4 * d), 0.02)
+        sd[p + "mlp.c_fc.bias"] = gen_tensor(seed, p + "c_fc.b", (4 * d,), 0.02)
+        sd[p + "mlp.c_proj.weight"] = gen_tensor(seed, p + "mlp.c_proj.w", (4 * d, d), proj_std)
+        sd[p + "mlp.c_proj.bias"] = gen_tensor(seed, p + "mlp.c_proj.b", (d,), 0.02)
+    return sd
+
+
+def mapper_state_dict(cfg: MapperCfg, seed: int = 0) -> Dict[str, Tensor]:
+    """TransformerMappingNetwork names (src/models.py:119-139; nn.TransformerEncoderLayer)."""
+    d, ff = cfg.gpt_dim, 4 * cfg.gpt_dim
+    sd = {
+        "linear.weight": gen_tensor(seed, "m.linear.w", (cfg.hidden_length * d, cfg.embed_dim), 1 / math.sqrt(3 * cfg.embed_dim)),
+        "linear.bias": gen_tensor(seed, "m.linear.b", (cfg.hidden_length * d,), 1 / math.sqrt(3 * cfg.embed_dim)),
+        "prefix_const": gen_tensor(seed, "m.prefix_const", (cfg.prefix_length, d), 1.0),
+    }
+    for i in range(cfg.num_layers):
+        p = f"transformer.layers.{i}."
+        sd[p + "self_attn.in_proj_weight"] = gen_tensor(seed, p + "in_w", (3 * d, d), math.sqrt(2.0 / (4 * d)))
+        sd[p + "self_attn.in_proj_bias"] = gen_tensor(seed, p + "in_b", (3 * d,), 0.02)
+        sd[p + "self_attn.out_proj.weight"] = gen_tensor(seed, p + "out_w", (d, d), 1 / math.sqrt(3 * d))
+        sd[p + "self_attn.out_proj.bias"] = gen_tensor(seed, p + "out_b", (d,), 0.02)
+        sd[p + "linear1.weight"] = gen_tensor(seed, p + "l1_w", (ff, d), 1 / math.sqrt(3 * d))
+        sd[p + "linear1.bias"] = gen_tensor(seed, p + "l1_b", (ff,), 1 / math.sqrt(3 * d))
+        sd[p + "linear2.weight"] = gen_tensor(seed, p + "l2_w", (d, ff), 1 / math.sqrt(3 * ff))
+        sd[p + "linear2.bias"] = gen_tensor(seed, p + "l2_b", (d,), 1 / math.sqrt(3 * ff))
+        sd[p + "norm1.weight"] = gen_tensor(seed, p + "n1_w", (d,), 0.05, 1.0)
+        sd[p + "norm1.bias"] = gen_tensor(seed, p + "n1_b", (d,), 0.02)
+        sd[p + "norm2.weight"] = gen_tensor(seed, p + "n2_w", (d,), 0.05, 1.0)
+        sd[p + "norm2.bias"] = gen_tensor(seed, p + "n2_b", (d,), 0.02)
+    return sd
+
+
+def mlp_mapper_state_dict(cfg: MLPMapperCfg, seed: int = 0) -> Dict[str, Tensor]:
+    """MLPMappingNetwork names (src/models.py:52-56: model.0 / model.2 Linear)."""
+    out = cfg.prefix_length * cfg.gpt_dim
+    hid = out // 2
+    return {
+        "model.0.weight": gen_tensor(seed, "mlp.0.w", (hid, cfg.embed_dim), 1 / math.sqrt(3 * cfg.embed_dim)),
+        "model.0.bias": gen_tensor(seed, "mlp.0.b", (hid,), 1 / math.sqrt(3 * cfg.embed_dim)),
+        "model.2.weight": gen_tensor(seed, "mlp.2.w", (out, hid), 1 / math.sqrt(3 * hid)),
+        "model.2.bias": gen_tensor(seed, "mlp.2.b", (out,), 1 / math.sqrt(3 * hid)),
+    }
+
+
+def clip_vision_state_dict(cfg: ClipCfg, seed: int = 0) -> Dict[str, Tensor]:
+    """HF CLIPModel vision-tower + visual_projection names (modeling_clip.py:138-219,594-657,751)."""
+    d, g = cfg.hidden, cfg.image // cfg.patch
+    v = "vision_model."
+    sd = {
+        v + "embeddings.class_embedding": gen_tensor(seed, "c.cls", (d,), 0.5),
+        v + "embeddings.patch_embedding.weight": gen_tensor(seed, "c.patch", (d, cfg.channels, cfg.patch, cfg.patch), 0.02),
+        v + "embeddings.position_embedding.weight": gen_tensor(seed, "c.pos", (g * g + 1, d), 0.02),
+        v + "pre_layrnorm.weight": gen_tensor(seed, "c.pre.w", (d,), 0.05, 1.0),
+        v + "pre_layrnorm.bias": gen_tensor(seed, "c.pre.b", (d,), 0.02),
+        v + "post_layernorm.weight": gen_tensor(seed, "c.post.w", (d,), 0.05, 1.0),
+        v + "post_layernorm.bias": gen_tensor(seed, "c.post.b", (d,), 0.02),
+        "visual_projection.weight": gen_tensor(seed, "c.proj", (cfg.proj, d), 0.02),
+    }
+    for i in range(cfg.layers):
+        p = v + f"encoder.layers.{i}."
+        for nm in ("q_proj", "k_proj", "v_proj", "out_proj"):
+            sd[p + f"self_attn.{nm}.weight"] = gen_tensor(seed, p + nm + ".w", (d, d), 0.02)
+            sd[p + f"self_attn.{nm}.bias"] = gen_tensor(seed, p + nm + ".b", (d,), 0.02)
+        sd[p + "layer_norm1.weight"] = gen_tensor(seed, p + "ln1.w", (d,), 0.05, 1.0)
+        sd[p + "layer_norm1.bias"] = gen_tensor(seed, p + "ln1.b", (d,), 0.02)
+        sd[p + "layer_norm2.weight"] = gen_tensor(seed, p + "ln2.w", (d,), 0.05, 1.0)
+        sd[p + "layer_norm2.bias"] = gen_tensor(seed, p + "ln2.b", (d,), 0.02)
+        sd[p + "mlp.fc1.weight"] = gen_tensor(seed, p + "fc1.w", (cfg.inter, d), 0.02)
+        sd[p + "mlp.fc1.bias"] = gen_tensor(seed, p + "fc1.b", (cfg.inter,), 0.02)
+        sd[p + "mlp.fc2.weight"] = gen_tensor(seed, p + "fc2.w", (d, cfg.inter), 0.02)
+        sd[p + "mlp.fc2.bias"] = gen_tensor(seed, p + "fc2.b", (d,), 0.02)
+    return sd
+
+
+# --------------------------------------------------------------------------- synthetic inputs
+
+
+def synthetic_batch(B: int, L: int = 50, real: int = 13, vocab: int = 50257, eos: int = 50256,
+                    embed_dim: int = 512, seed: int = 1):
+    """COCO-shaped batch: `real` random tokens + EOS (mask 1), then pad=EOS (mask 0, label -100);
+    dataset.py:181-206 semantics. Embeddings: L2-normalised gaussians (clip.py:135-137)."""
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, vocab - 1, (B, L), generator=g, dtype=torch.int64)
+    mask = torch.zeros((B, L), dtype=torch.int64)
+    n = min(real, L - 1)
+    ids[:, n] = eos
+    ids[:, n + 1:] = eos
+    mask[:, : n + 1] = 1
+    labels = ids.clone()
+    labels[mask == 0] = -100
+    emb = torch.randn((B, embed_dim), generator=g)
+    emb = emb / emb.norm(dim=-1, keepdim=True)
+    return ids, mask, labels, emb
+
+
+# --------------------------------------------------------------------------- GPT-2
+
+
+def gelu_new(x: Tensor) -> Tensor:  # HF/activations.py:59-66
+    return 0.5 * x * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (x + 0.044715 * torch.pow(x, 3.0))))
+
+
+def _drop(x: Tensor, p: float, train: bool) -> Tensor:
+    return F.dropout(x, p, True) if (train and p > 0) else x
+
+
+def gpt2_forward(sd: Dict[str, Tensor], cfg: GPT2Cfg, inputs_embeds: Tensor, attention_mask: Optional[Tensor] = None,
+                 labels: Optional[Tensor] = None, train: bool = False, p_drop: float = 0.0):
+    """GPT2LMHeadModel.forward(inputs_embeds=, attention_mask=, labels=) — HF/models/gpt2/modeling_gpt2.py:514-725.
+
+    Returns (loss or None, logits [B,S,V])."""
+    B, S, d = inputs_embeds.shape
+    H = cfg.n_head
+    hd = d // H
+    pos = torch.arange(S)
+    h = inputs_embeds + sd["transformer.wpe.weight"][pos]  # :571-577
+    h = _drop(h, p_drop, train)  # :604
+    # mask: allowed(q,k) = k<=q and attention_mask[b,k]  (HF/masking_utils.py:76-80,168-180)
+    allowed = torch.tril(torch.ones(S, S, dtype=torch.bool))[None, None]
+    if attention_mask is not None:
+        allowed = allowed & attention_mask.bool()[:, None, None, :]
+    neg = torch.finfo(h.dtype).min
+    for i in range(cfg.n_layer):  # GPT2Block.forward :262-310
+        p = f"transformer.h.{i}."
+        a = F.layer_norm(h, (d,), sd[p + "ln_1.weight"], sd[p + "ln_1.bias"], cfg.eps)
+        qkv = a @ sd[p + "attn.c_attn.weight"] + sd[p + "attn.c_attn.bias"]  # Conv1D, pytorch_utils.py:117-121
+        q, k, v = qkv.split(d, dim=2)  # :185
+        q = q.view(B, S, H, hd).transpose(1, 2)
+        k = k.view(B, S, H, hd).transpose(1, 2)
+        v = v.view(B, S, H, hd).transpose(1, 2)
+        w = (q @ k.transpose(-1, -2)) / math.sqrt(hd)
+        w = torch.where(allowed, w, torch.tensor(neg, dtype=w.dtype))
+        w = torch.softmax(w, dim=-1)
+        w = _drop(w, p_drop, train)
+        o = (w @ v).transpose(1, 2).reshape(B, S, d)
+        o = o @ sd[p + "attn.c_proj.weight"] + sd[p + "attn.c_proj.bias"]  # :223
+        h = h + _drop(o, p_drop, train)
+        a = F.layer_norm(h, (d,), sd[p + "ln_2.weight"], sd[p + "ln_2.bias"], cfg.eps)
+        f = gelu_new(a @ sd[p + "mlp.c_fc.weight"] + sd[p + "mlp.c_fc.bias"])  # GPT2MLP :238-244
+        f = f @ sd[p + "mlp.c_proj.weight"] + sd[p + "mlp.c_proj.bias"]
+        h = h + _drop(f, p_drop, train)
+    h = F.layer_norm(h, (d,), sd["transformer.ln_f.weight"], sd["transformer.ln_f.bias"], cfg.eps)  # :620
+    logits = h @ sd["transformer.wte.weight"].t()  # tied lm_head :638,:698
+    loss = None
+    if labels is not None:
+        loss = causal_lm_loss(logits, labels)
+    return loss, logits
+
+
+def causal_lm_loss(logits: Tensor, labels: Tensor) -> Tensor:
+    """HF/loss/loss_utils.py:49-71 ForCausalLMLoss + fixed_cross_entropy :32-46 (mean over labels != -100)."""
+    logits = logits.float()
+    labels = F.pad(labels, (0, 1), value=-100)
+    shift = labels[..., 1:].contiguous()
+    return F.cross_entropy(logits.view(-1, logits.shape[-1]), shift.view(-1), ignore_index=-100, reduction="mean")
+
+
+# --------------------------------------------------------------------------- mapping networks
+
+
+def mapper_forward(sd: Dict[str, Tensor], cfg: MapperCfg, emb: Tensor, train: bool = False, p_drop: float = 0.0):
+    """TransformerMappingNetwork.forward — src/models.py:141-174 (norm_first encoder layers, TORCH/nn/modules/
+    transformer.py:946-982: x += drop(MHA(LN1 x)); x += drop(W2 drop(relu(W1 LN2 x))))."""
+    B = emb.shape[0]
+    d, H = cfg.gpt_dim, cfg.nhead
+    hd = d // H
+    x = (emb @ sd["linear.weight"].t() + sd["linear.bias"]).view(B, cfg.hidden_length, d)  # :154-159
+    x = torch.cat((x, sd["prefix_const"].unsqueeze(0).expand(B, -1, -1)), dim=1)  # :163-168
+    S = x.shape[1]
+    for i in range(cfg.num_layers):
+        p = f"transformer.layers.{i}."
+        a = F.layer_norm(x, (d,), sd[p + "norm1.weight"], sd[p + "norm1.bias"], cfg.eps)
+        qkv = a @ sd[p + "self_attn.in_proj_weight"].t() + sd[p + "self_attn.in_proj_bias"]
+        q, k, v = qkv.split(d, dim=2)
+        q = q.view(B, S, H, hd).transpose(1, 2)
+        k = k.view(B, S, H, hd).transpose(1, 2)
+        v = v.view(B, S, H, hd).transpose(1, 2)
+        w = torch.softmax((q @ k.transpose(-1, -2)) / math.sqrt(hd), dim=-1)
+        w = _drop(w, p_drop, train)
+        o = (w @ v).transpose(1, 2).reshape(B, S, d)
+        o = o @ sd[p + "self_attn.out_proj.weight"].t() + sd[p + "self_attn.out_proj.bias"]
+        x = x + _drop(o, p_drop, train)
+        a = F.layer_norm(x, (d,), sd[p + "norm2.weight"], sd[p + "norm2.bias"], cfg.eps)
+        f = torch.relu(a @ sd[p + "linear1.weight"].t() + sd[p + "linear1.bias"])
+        f = _drop(f, p_drop, train) @ sd[p + "linear2.weight"].t() + sd[p + "linear2.bias"]
+        x = x + _drop(f, p_drop, train)
+    return x[:, cfg.hidden_length:, :]  # :174
+
+
+def mlp_mapper_forward(sd: Dict[str, Tensor], cfg: MLPMapperCfg, emb: Tensor) -> Tensor:
+    """MLPMappingNetwork.forward — src/models.py:58-74 (Linear, Tanh, Linear, view)."""
+    h = torch.tanh(emb @ sd["model.0.weight"].t() + sd["model.0.bias"])
+    out = h @ sd["model.2.weight"].t() + sd["model.2.bias"]
+    return out.view(emb.shape[0], cfg.prefix_length, cfg.gpt_dim)
+
+
+# --------------------------------------------------------------------------- captioner
+
+
+def caption_forward(gpt_sd, gcfg: GPT2Cfg, prefix: Tensor, ids: Tensor, mask: Optional[Tensor] = None,
+                    labels: Optional[Tensor] = None, train: bool = False, p_drop: float = 0.0):
+    """ImageCaptioningModel.forward — src/models.py:237-325 given the mapper output `prefix`."""
+    cap = gpt_sd["transformer.wte.weight"][ids]  # :261
+    P = prefix.shape[1]
+    x = torch.cat((prefix, cap), dim=1)  # :286
+    if labels is not None:  # :289-304
+        labels = torch.cat((torch.full((labels.shape[0], P), -100, dtype=torch.int64), labels), dim=1)
+    if mask is not None:  # :307-317
+        mask = torch.cat((torch.ones((mask.shape[0], P), dtype=mask.dtype), mask), dim=1)
+    return gpt2_forward(gpt_sd, gcfg, x, mask, labels, train, p_drop)
+
+
+@torch.no_grad()
+def greedy_generate(gpt_sd, gcfg: GPT2Cfg, prefix: Tensor, max_length: int = 50) -> Tensor:
+    """ImageCaptioningModel.generate with temperature=0 — src/models.py:327-477: full recompute over all tokens
+    each step (:395, no KV cache), last-position argmax (:441), EOS latch (:453-460), early exit (:390)."""
+    B = prefix.shape[0]
+    eos = gcfg.eos
+    cur = prefix
+    finished = torch.zeros(B, dtype=torch.bool)
+    out = []
+    for _ in range(max_length):
+        if bool(finished.all()):
+            break
+        _, logits = gpt2_forward(gpt_sd, gcfg, cur)
+        nxt = torch.argmax(logits[:, -1, :], dim=-1).unsqueeze(-1)
+        finished = finished | nxt.squeeze(-1).eq(eos)
+        nxt[finished] = eos
+        out.append(nxt)
+        cur = torch.cat((cur, gpt_sd["transformer.wte.weight"][nxt]), dim=1)
+    if not out:
+        return torch.empty((B, 0), dtype=torch.long)
+    return torch.cat(out, dim=1)
+
+
+# --------------------------------------------------------------------------- CLIP
+
+
+def quick_gelu(x: Tensor) -> Tensor:  # HF/activations.py:117-123
+    return x * torch.sigmoid(1.702 * x)
+
+
+def clip_image_features(sd: Dict[str, Tensor], cfg: ClipCfg, pixels: Tensor) -> Tensor:
+    """CLIPModel.get_image_features(...).pooler_output — HF/models/clip/modeling_clip.py:138-219 (embeddings),
+    :280-384 (encoder layers), :594-657 (vision transformer), :719-752 (projection)."""
+    v = "vision_model."
+    d, H = cfg.hidden, cfg.heads
+    hd = d // H
+    B = pixels.shape[0]
+    pe = F.conv2d(pixels, sd[v + "embeddings.patch_embedding.weight"], stride=cfg.patch)  # :209-210
+    pe = pe.flatten(2).transpose(1, 2)
+    cls = sd[v + "embeddings.class_embedding"].expand(B, 1, -1)
+    x = torch.cat([cls, pe], dim=1) + sd[v + "embeddings.position_embedding.weight"].unsqueeze(0)  # :212-217
+    x = F.layer_norm(x, (d,), sd[v + "pre_layrnorm.weight"], sd[v + "pre_layrnorm.bias"], cfg.eps)  # :642
+    S = x.shape[1]
+    for i in range(cfg.layers):
+        p = v + f"encoder.layers.{i}."
+        a = F.layer_norm(x, (d,), sd[p + "layer_norm1.weight"], sd[p + "layer_norm1.bias"], cfg.eps)
+        q = a @ sd[p + "self_attn.q_proj.weight"].t() + sd[p + "self_attn.q_proj.bias"]
+        k = a @ sd[p + "self_attn.k_proj.weight"].t() + sd[p + "self_attn.k_proj.bias"]
+        vv = a @ sd[p + "self_attn.v_proj.weight"].t() + sd[p + "self_attn.v_proj.bias"]
+        q = q.view(B, S, H, hd).transpose(1, 2)
+        k = k.view(B, S, H, hd).transpose(1, 2)
+        vv = vv.view(B, S, H, hd).transpose(1, 2)
+        w = torch.softmax((q @ k.transpose(-1, -2)) * (hd ** -0.5), dim=-1)
+        o = (w @ vv).transpose(1, 2).reshape(B, S, d)
+        o = o @ sd[p + "self_attn.out_proj.weight"].t() + sd[p + "self_attn.out_proj.bias"]
+        x = x + o
+        a = F.layer_norm(x, (d,), sd[p + "layer_norm2.weight"], sd[p + "layer_norm2.bias"], cfg.eps)
+        f = quick_gelu(a @ sd[p + "mlp.fc1.weight"].t() + sd[p + "mlp.fc1.bias"])
+        x = x + (f @ sd[p + "mlp.fc2.weight"].t() + sd[p + "mlp.fc2.bias"])
+    pooled = F.layer_norm(x[:, 0, :], (d,), sd[v + "post_layernorm.weight"], sd[v + "post_layernorm.bias"], cfg.eps)
+    return pooled @ sd["visual_projection.weight"].t()
+
+
+def clip_embed_normalized(sd, cfg: ClipCfg, pixels: Tensor) -> Tensor:
+    """src/embeddings/clip.py:132-137: get_image_features then L2 normalise."""
+    f = clip_image_features(sd, cfg, pixels)
+    return f / f.norm(p=2, dim=-1, keepdim=True)
+
+
+# --------------------------------------------------------------------------- optimisation
+
+
+@dataclass
+class AdamWState:
+    exp_avg: Dict[str, Tensor] = field(default_factory=dict)
+    exp_avg_sq: Dict[str, Tensor] = field(default_factory=dict)
+    step: int = 0
+
+
+def linear_schedule(step: int, warmup: int, total: int) -> float:
+    """HF/optimization.py:101-107 get_linear_schedule_with_warmup lr_lambda."""
+    if step < warmup:
+        return float(step) / float(max(1, warmup))
+    return max(0.0, float(total - step) / float(max(1, total - warmup)))
+
+
+@torch.no_grad()
+def clip_and_adamw(params: Dict[str, Tensor], grads: Dict[str, Tensor], st: AdamWState, lr0: float,
+                   warmup: int, total: int, max_norm: float = 1.0, betas=(0.9, 0.999), eps: float = 1e-8,
+                   wd: float = 0.01) -> float:
+    """clip_grad_norm_(max_norm) then AdamW.step then scheduler.step — src/train.py:150-156;
+    TORCH/nn/utils/clip_grad.py:121-186; TORCH/optim/adam.py:419,457,476,499,545-547 (single-tensor form)."""
+    norms = [torch.linalg.vector_norm(g, 2) for g in grads.values()]
+    total_norm = torch.linalg.vector_norm(torch.stack(norms), 2)
+    coef = torch.clamp(max_norm / (total_norm + 1e-6), max=1.0)
+    lr = lr0 * linear_schedule(st.step, warmup, total)
+    st.step += 1
+    b1, b2 = betas
+    bc1 = 1 - b1 ** st.step
+    bc2 = 1 - b2 ** st.step
+    for k, p in params.items():
+        g = grads[k] * coef
+        if k not in st.exp_avg:
+            st.exp_avg[k] = torch.zeros_like(p)
+            st.exp_avg_sq[k] = torch.zeros_like(p)
+        m, v = st.exp_avg[k], st.exp_avg_sq[k]
+        p.mul_(1 - lr * wd)
+        m.lerp_(g, 1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+        p.addcdiv_(m, denom, value=-(lr / bc1))
+    return float(total_norm)
+
+
+def train_steps(gpt_sd, gcfg: GPT2Cfg, map_sd, mcfg: MapperCfg, batches, lr0: float = 1e-4, total_steps: int = 10,
+                warmup: int = 0, freeze_gpt: bool = True):
+    """The inner loop of src/train.py:119-166 with grad_accum_steps=1 and dropout off: forward, backward, clip,
+    AdamW, schedule. Returns (losses, grad_norms, map_sd, gpt_sd) after len(batches) steps."""
+    map_sd = {k: v.clone().requires_grad_(True) for k, v in map_sd.items()}
+    gpt_sd = {k: v.clone().requires_grad_(not freeze_gpt) for k, v in gpt_sd.items()}
+    st = AdamWState()
+    losses, norms = [], []
+    for ids, mask, labels, emb in batches:
+        prefix = mapper_forward(map_sd, mcfg, emb)
+        loss, _ = caption_forward(gpt_sd, gcfg, prefix, ids, mask, labels)
+        trainable = dict(map_sd)
+        if not freeze_gpt:
+            trainable.update({"gpt." + k: v for k, v in gpt_sd.items()})
+        grads = torch.autograd.grad(loss, list(trainable.values()), allow_unused=True)
+        grads = {k: (g if g is not None else torch.zeros_like(trainable[k])) for k, g in zip(trainable, grads)}
+        with torch.no_grad():
+            params = {k: v.data for k, v in trainable.items()}
+            norms.append(clip_and_adamw(params, grads, st, lr0, warmup, total_steps))
+        losses.append(float(loss.detach()))
+    return losses, norms, {k: v.detach() for k, v in map_sd.items()}, {k: v.detach() for k, v in gpt_sd.items()}
