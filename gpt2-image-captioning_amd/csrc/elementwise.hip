@@ -51,6 +51,20 @@ __global__ void gpt2_embed_kernel(int B, int P, int L, int D, const T* __restric
   }
 }
 
+// d(wte)[ids[b,t-P]] += dx[b*S+t] for caption rows (fp32 atomics; unfrozen GPT-2 only)
+template <typename T>
+__global__ void embed_scatter_kernel(int B, int P, int L, int D, const T* __restrict__ dx,
+                                     const int64_t* __restrict__ ids, float* __restrict__ dwte) {
+  const int S = P + L;
+  const int64_t total = (int64_t)B * L * D;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / D;
+    const int d = (int)(i - r * D);
+    const int b = (int)(r / L), t = (int)(r - (int64_t)b * L);
+    atomicAdd(dwte + ids[(int64_t)b * L + t] * D + d, io<T>::ld(dx + ((int64_t)b * S + P + t) * D + d));
+  }
+}
+
 __global__ void caption_prep_kernel(int B, int P, int L, const int64_t* __restrict__ mask,
                                     const int64_t* __restrict__ labels, int32_t* key_mask, int32_t* lab_shift,
                                     int32_t* n_valid) {
@@ -393,7 +407,8 @@ __global__ void l2norm_kernel(int64_t rows, int64_t D, const T* __restrict__ x, 
 // ---------------------------------------------------------------- greedy decode glue
 template <typename T>
 __global__ __launch_bounds__(256) void greedy_next_kernel(int64_t V, const T* __restrict__ logits, int64_t ld,
-                                                         int64_t eos, int32_t* finished, int64_t* tokens,
+                                                         int64_t eos, const int64_t* __restrict__ forced,
+                                                         int32_t* finished, int64_t* tokens,
                                                          int64_t ld_tokens, int step, const T* __restrict__ wte,
                                                          const T* __restrict__ wpe, int pos, int D, T* __restrict__ x) {
   __shared__ float rv[4];
@@ -423,6 +438,7 @@ __global__ __launch_bounds__(256) void greedy_next_kernel(int64_t V, const T* __
     for (int k = 1; k < 4; ++k)
       if (rv[k] > bv || (rv[k] == bv && ri[k] < bj)) { bv = rv[k]; bj = ri[k]; }
     if (bj >= V) bj = 0;
+    if (forced) bj = forced[b];
     int fin = finished[b];
     if (fin) bj = eos;
     if (bj == eos) fin = 1;
@@ -691,13 +707,13 @@ extern "C" int icap_l2norm_rows(int32_t dtype, int64_t rows, int64_t D, const vo
 }
 
 extern "C" int icap_greedy_next(int32_t dtype, int32_t B, int64_t V, const void* logits, int64_t ld, int64_t eos,
-                                int32_t* finished, int64_t* tokens, int64_t ld_tokens, int32_t step, const void* wte,
+                                const int64_t* forced, int32_t* finished, int64_t* tokens, int64_t ld_tokens, int32_t step, const void* wte,
                                 const void* wpe, int32_t pos, int32_t D, void* x, void* stream) {
   ICAP_REQUIRE(logits && finished && tokens, "icap_greedy_next: null pointer");
   ICAP_REQUIRE(x == nullptr || (wte && wpe), "icap_greedy_next: x requires wte/wpe");
   if (B == 0) return ICAP_OK;
   DISPATCH_T(dtype, hipLaunchKernelGGL(greedy_next_kernel<T>, dim3((unsigned)B), dim3(256), 0, S_(stream), V,
-                                       CTP(logits), ld, eos, finished, tokens, ld_tokens, step, CTP(wte), CTP(wpe),
+                                       CTP(logits), ld, eos, forced, finished, tokens, ld_tokens, step, CTP(wte), CTP(wpe),
                                        pos, D, TP(x)));
   return check_launch("icap_greedy_next");
 }
@@ -717,4 +733,14 @@ extern "C" int icap_counter_increment(uint64_t* counter, void* stream) {
   ICAP_REQUIRE(counter, "icap_counter_increment: null pointer");
   hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(64), 0, S_(stream), counter);
   return check_launch("icap_counter_increment");
+}
+
+extern "C" int icap_embedding_scatter_add(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D, const void* dx,
+                                          const int64_t* ids, float* dwte, void* stream) {
+  ICAP_REQUIRE(dx && ids && dwte, "icap_embedding_scatter_add: null pointer");
+  const int64_t n = (int64_t)B * L * D;
+  if (n == 0) return ICAP_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(embed_scatter_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B,
+                                       P, L, D, CTP(dx), ids, dwte));
+  return check_launch("icap_embedding_scatter_add");
 }

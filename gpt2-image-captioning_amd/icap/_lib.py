@@ -87,6 +87,7 @@ SIGNATURES = {
     "icap_attention_bwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_decode": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, i64, f32, vp]),
     "icap_gpt2_embed": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, vp, f32, u64, u64, vp, vp]),
+    "icap_embedding_scatter_add": (C.c_int, [i32, i32, i32, i32, i32, vp, vp, vp, vp]),
     "icap_caption_prep": (C.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp]),
     "icap_cross_entropy_workspace_bytes": (sz, [i64]),
     "icap_cross_entropy": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, f32, vp, vp]),
@@ -103,7 +104,7 @@ SIGNATURES = {
     "icap_im2col_patches": (C.c_int, [i32, i32, i32, i32, i32, vp, vp, vp]),
     "icap_vit_embed": (C.c_int, [i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     "icap_l2norm_rows": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, vp]),
-    "icap_greedy_next": (C.c_int, [i32, i32, i64, vp, i64, i64, vp, vp, i64, i32, vp, vp, i32, i32, vp, vp]),
+    "icap_greedy_next": (C.c_int, [i32, i32, i64, vp, i64, i64, vp, vp, vp, i64, i32, vp, vp, i32, i32, vp, vp]),
     "icap_add_position": (C.c_int, [i32, i32, i32, i32, vp, i64, i64, vp, i32, vp, vp]),
 }
 

@@ -1,0 +1,229 @@
+"""The fused captioning train step: CLIP fwd (optional) -> mapper fwd -> GPT-2 fwd -> LM head + CE ->
+GPT-2 dX backward -> mapper backward -> (RCCL all-reduce) -> clip_grad_norm + AdamW + LR schedule.
+
+This is src/train.py:119-166 (one inner iteration) as an explicit schedule of libicap_hip.so kernels on
+one HIP stream, with all buffers preallocated so the whole step can be captured into a HIP graph and
+replayed (torch.cuda.CUDAGraph is only the capture/replay plumbing). Trainable parameters, their grads and
+the AdamW moments live in one flat fp32 buffer each (weights.FlatParams); the bf16 compute copy of the
+trainable weights is written by the AdamW kernel itself.
+"""
+
+from __future__ import annotations
+
+from types import SimpleNamespace
+from typing import Optional
+
+import torch
+
+from . import ops
+from .mapper import DWHelper, MLPMapperCore, TransformerMapperCore
+
+Tensor = torch.Tensor
+
+
+class CaptionTrainer:
+    def __init__(self, model, batch_size: int, caption_len: int, *, lr: float = 1e-4, weight_decay: float = 0.01,
+                 betas=(0.9, 0.999), eps: float = 1e-8, max_norm: float = 1.0, num_warmup_steps: int = 0,
+                 num_training_steps: int = 1, dropout: bool = True, seed: int = 0, clip_model=None,
+                 grad_accum_steps: int = 1, process_group=None):
+        self.model = model
+        self.dtype = model.compute_dtype
+        self.B, self.Lc = batch_size, caption_len
+        self.hp = SimpleNamespace(lr=lr, weight_decay=weight_decay, betas=betas, eps=eps, max_norm=max_norm,
+                                  num_warmup_steps=num_warmup_steps, num_training_steps=num_training_steps)
+        self.dropout = dropout
+        self.seed = seed
+        self.grad_accum_steps = grad_accum_steps
+        self.pg = process_group
+        self.world = 1
+        if process_group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            self.world = torch.distributed.get_world_size(process_group)
+        self.dev = model.device
+        flat = model.flat()
+        self.flat = flat
+        self.mcore = model.mapping_network.core(self.dtype, flat)
+        self.gcore = model.gpt.core(self.dtype)
+        self.clip = clip_model.core(self.dtype) if clip_model is not None else None
+        self.gpt_trainable = not model.freeze_gpt_weights
+        if self.gpt_trainable:
+            raise NotImplementedError("the fused trainer covers the reference default freeze_gpt_weights=True; "
+                                      "use ImageCaptioningModel.forward + autograd for unfrozen GPT-2")
+        B, Lc = batch_size, caption_len
+        P = model.total_prefix_length
+        self.P = P
+        self.mws = self.mcore.alloc(B, train=True)
+        self.gws = self.gcore.alloc_train(B, P, Lc)
+        D = self.gcore.D
+        M2 = self.mws.M
+        E = self.mcore.E
+        max_cols = max(4 * D, 3 * D, E, self.mcore.dw_cols())
+        # colsum also reduces the prefix_const / task-prefix grads over the batch: B rows x P*D columns
+        self.dwh = DWHelper(self.dtype, self.dev, max_rows=max(M2, B), max_cols=max_cols, ln_rows=M2, ln_D=D,
+                            colsum_cols=P * D)
+        self.mgrads = self.mcore.grads(flat)
+        if model.task_prefix_embeds is not None:
+            self.task_grad = flat.grad(model.task_prefix_embeds)
+            self.pre = torch.empty((B, P, D), dtype=self.dtype, device=self.dev)
+        # static inputs (graph-capture friendly)
+        self.ids = torch.zeros((B, Lc), dtype=torch.int64, device=self.dev)
+        self.mask = torch.ones((B, Lc), dtype=torch.int64, device=self.dev)
+        self.labels = torch.zeros((B, Lc), dtype=torch.int64, device=self.dev)
+        self.emb = torch.zeros((B, E), dtype=torch.float32, device=self.dev)
+        self.emb_c = torch.zeros((B, E), dtype=self.dtype, device=self.dev)
+        self.pixels = None
+        if self.clip is not None:
+            c = clip_model.config
+            self.pixels = torch.zeros((B, c.num_channels, c.image_size, c.image_size), dtype=torch.float32,
+                                      device=self.dev)
+            self.cws = self.clip.alloc(B)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        if flat.exp_avg is None:
+            flat.exp_avg = torch.zeros_like(flat.flat)
+            flat.exp_avg_sq = torch.zeros_like(flat.flat)
+        self.adam_state = torch.zeros(16, dtype=torch.float32, device=self.dev)
+        self.adam_ws = torch.empty(ops.adamw_workspace(flat.n), dtype=torch.uint8, device=self.dev)
+        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=self.dev)
+        self.graph = None
+        self.graph_opt = None
+        self._micro = 0
+        self._eager_steps = 0
+        self.gdr = self.gcore.drops(dropout, seed, self.counter, self.gws.M, B, self.gws.S)
+        p_map = 0.1 if isinstance(self.mcore, TransformerMapperCore) else 0.0
+        self.mdr = self.mcore.drops(dropout, p_map, seed, self.counter, B)
+
+    def share_state_with(self, other: "CaptionTrainer") -> None:
+        """Use `other`'s optimizer step counter and dropout counter (same model, another batch shape)."""
+        self.adam_state = other.adam_state
+        self.counter = other.counter
+        self.gdr = self.gcore.drops(self.dropout, self.seed, self.counter, self.gws.M, self.B, self.gws.S)
+        p_map = 0.1 if isinstance(self.mcore, TransformerMapperCore) else 0.0
+        self.mdr = self.mcore.drops(self.dropout, p_map, self.seed, self.counter, self.B)
+
+    # -- inputs -----------------------------------------------------------------------------------------------
+    def load_batch(self, ids: Tensor, mask: Tensor, labels: Tensor, emb: Optional[Tensor] = None,
+                   pixels: Optional[Tensor] = None) -> None:
+        self.ids.copy_(ids, non_blocking=True)
+        self.mask.copy_(mask, non_blocking=True)
+        self.labels.copy_(labels, non_blocking=True)
+        if pixels is not None:
+            if self.pixels is None:
+                raise ValueError("trainer was built without a CLIP tower; pass image embeddings")
+            self.pixels.copy_(pixels, non_blocking=True)
+        elif emb is not None:
+            self.emb.copy_(emb, non_blocking=True)
+
+    # -- the step ---------------------------------------------------------------------------------------------
+    def _fwd_bwd(self, zero: bool, grad_scale: float) -> None:
+        B, P, D = self.B, self.P, self.gcore.D
+        model = self.model
+        if zero:
+            self.flat.flat_grad.zero_()
+        if self.clip is not None:
+            emb = self.clip.run(self.cws, self.pixels)
+            ops.convert(emb, self.emb_c)
+        else:
+            ops.convert(self.emb, self.emb_c)
+        if self.dropout:
+            ops.counter_increment(self.counter)
+        mc, gc = self.mcore, self.gcore
+        mc.forward(self.mws, self.emb_c, self.mdr, train=True)
+        pre, pbs = mc.prefix_view(self.mws)
+        if model.task_prefix_embeds is not None:  # [image prefix ; task prefix] (src/models.py:269-283)
+            Pm = mc.P
+            ops.convert(_rows_view(pre, B, Pm * D, pbs), self.pre.view(B, P * D)[:, : Pm * D])
+            ops.broadcast_rows(model.task_prefix_embeds.data, self.pre.view(-1)[Pm * D:], B, P * D)
+            pre, pbs = self.pre, P * D
+        gc.forward_train(self.gws, pre, pbs, self.ids, self.mask, self.labels, self.gdr, fuse_dlogits=True,
+                         grad_scale=grad_scale)
+        S = self.gws.S
+        d_emb = gc.backward(self.gws, self.gdr, self.gws.key_mask, self.gws.logits)
+        d_pre = d_emb.view(B, S * D)[:, : P * D]
+        Pm = mc.P
+        if model.task_prefix_embeds is not None:
+            ops.colsum(d_emb.view(B, S * D)[:, Pm * D: P * D], self.task_grad.view(-1), self.dwh.cs_ws,
+                       accumulate=True, M=B, N=(P - Pm) * D)
+        if isinstance(mc, TransformerMapperCore):
+            Hl, Sm = mc.Hl, mc.S
+            ops.convert(d_pre[:, : Pm * D], self.mws.dout.view(B, Sm * D)[:, Hl * D:])
+            mc.backward(self.mws, self.emb_c, self.mdr, self.mgrads, self.dwh)
+        else:
+            mc.backward_from(d_pre[:, : Pm * D], S * D, self.mws, self.emb_c, self.mgrads, self.dwh)
+        self.loss_sum.add_(self.gws.loss)
+
+    def _optimizer(self) -> None:
+        hp, f = self.hp, self.flat
+        ops.adamw_step(f.flat, f.flat_grad, f.exp_avg, f.exp_avg_sq, self.adam_state, self.adam_ws, lr=hp.lr,
+                       betas=hp.betas, eps=hp.eps, weight_decay=hp.weight_decay, max_norm=hp.max_norm,
+                       num_warmup_steps=hp.num_warmup_steps, num_training_steps=hp.num_training_steps,
+                       bf16_out=f.flat_c)
+        self.mcore.refresh_transposes()
+
+    def _allreduce(self) -> None:
+        if self.world > 1:
+            torch.distributed.all_reduce(self.flat.flat_grad, group=self.pg)
+
+    def grad_scale(self) -> float:
+        return 1.0 / (self.grad_accum_steps * self.world)
+
+    def micro_step(self, use_graph: bool = False) -> bool:
+        """One micro-batch (forward + backward). Returns True when an optimizer step was taken
+        (every grad_accum_steps micro-batches, src/train.py:146-159). With use_graph the first call runs
+        eagerly (warm-up) and every later call replays one captured HIP graph of the whole step."""
+        self.model.sync_compute_copies()
+        first = self._micro == 0
+        if use_graph and self.graph is None and self._eager_steps >= 1 and self.grad_accum_steps == 1:
+            self.capture()
+        if self.graph is not None and self.grad_accum_steps == 1:
+            self.graph.replay()
+            if self.world > 1:
+                self._allreduce()
+                self.graph_opt.replay()
+            self._micro = 0
+            return True
+        self._fwd_bwd(first, self.grad_scale())
+        self._micro += 1
+        self._eager_steps += 1
+        if self._micro == self.grad_accum_steps:
+            self._allreduce()
+            self._optimizer()
+            self._micro = 0
+            return True
+        return False
+
+    def flush(self) -> None:
+        """Apply a pending partial accumulation (src/train.py:146-148 last-batch rule)."""
+        if self._micro:
+            self._allreduce()
+            self._optimizer()
+            self._micro = 0
+
+    def capture(self) -> None:
+        """Capture fwd+bwd(+optimizer when single-process) into HIP graphs (recording only: nothing executes;
+        call after at least one eager step so every kernel and attribute has been initialised)."""
+        if self.grad_accum_steps != 1:
+            return
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._fwd_bwd(True, self.grad_scale())
+            if self.world == 1:
+                self._optimizer()
+        self.graph = g
+        if self.world > 1:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                self._optimizer()
+            self.graph_opt = g2
+
+    def take_loss_sum(self) -> float:
+        v = float(self.loss_sum.item())
+        self.loss_sum.zero_()
+        return v
+
+    @property
+    def last_loss(self) -> Tensor:
+        return self.gws.loss
+
+
+def _rows_view(t: Tensor, B: int, n: int, stride: int) -> Tensor:
+    return t.as_strided((B, n), (stride, 1))

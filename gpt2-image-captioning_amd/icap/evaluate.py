@@ -1,0 +1,70 @@
+"""Validation loop (the caller side of greedy decode, src/eval.py:160-229,311-386).
+
+Generates one caption per unique image with ImageCaptioningModel.generate (KV-cached HIP
+decode) and writes the reference's predictions JSON ([{"image_id", "caption"}],
+eval.py:368-373). COCO metrics (BLEU/ROUGE-L/CIDEr via pycocoevalcap, eval.py:59-108) are
+computed only when pycocoevalcap is importable — it is outside the device hot path and is
+not installed in this image.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+from typing import Any, Dict
+
+import torch
+
+
+def generate_predictions(model, dataset, batch_size: int = 128, max_length: int = 50, temperature: float = 0.0,
+                         top_p: float = 0.9, device=None):
+    device = device or model.device
+    seen, idx = set(), []
+    for i in range(len(dataset)):  # one caption per image (eval.py:219-224)
+        iid = dataset.captions[i].image_id if hasattr(dataset, "captions") else dataset[i]["image_id"]
+        if iid not in seen:
+            seen.add(iid)
+            idx.append(i)
+    preds = []
+    for s in range(0, len(idx), batch_size):
+        items = [dataset[i] for i in idx[s:s + batch_size]]
+        emb = torch.stack([it["image_embedding"] for it in items]).to(device)
+        ids = model.generate(emb, max_length=max_length, temperature=temperature, top_p=top_p)
+        if hasattr(model.tokenizer, "batch_decode"):
+            texts = model.tokenizer.batch_decode(ids.cpu(), skip_special_tokens=True)
+        else:
+            texts = [" ".join(str(t) for t in row) for row in ids.cpu().tolist()]
+        preds += [{"image_id": it["image_id"], "caption": t} for it, t in zip(items, texts)]
+    return preds
+
+
+def compute_caption_metrics(preds, annotations_path: str) -> Dict[str, float]:
+    try:
+        from pycocoevalcap.bleu.bleu import Bleu
+        from pycocoevalcap.cider.cider import Cider
+        from pycocoevalcap.rouge.rouge import Rouge
+    except ImportError:
+        return {}
+    with open(annotations_path) as f:
+        coco = json.load(f)
+    gts: Dict[int, list] = {}
+    for a in coco["annotations"]:
+        gts.setdefault(a["image_id"], []).append(a["caption"])
+    res = {p["image_id"]: [p["caption"]] for p in preds}
+    gts = {k: gts[k] for k in res}
+    bleu, _ = Bleu(4).compute_score(gts, res)
+    rouge, _ = Rouge().compute_score(gts, res)
+    cider, _ = Cider().compute_score(gts, res)
+    return {"bleu_1": bleu[0], "bleu_4": bleu[3], "rouge_l": rouge, "cider": cider}
+
+
+def evaluate_epoch(model, dataset, annotations_path, epoch, split_name, batch_size, num_workers, max_length,
+                   temperature, top_p, device, output_dir) -> Dict[str, Any]:
+    model.eval()
+    preds = generate_predictions(model, dataset, batch_size, max_length, temperature, top_p, device)
+    os.makedirs(output_dir, exist_ok=True)
+    with open(os.path.join(output_dir, f"{split_name}_predictions_epoch_{epoch}.json"), "w") as f:
+        json.dump(preds, f)
+    m = compute_caption_metrics(preds, annotations_path) if annotations_path else {}
+    m["num_predictions"] = len(preds)
+    return m

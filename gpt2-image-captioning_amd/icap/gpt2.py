@@ -1,0 +1,560 @@
+"""GPT-2 LM (HF GPT2LMHeadModel surface) on the icap HIP kernels.
+
+Reference: the reference wraps HF GPT2LMHeadModel (src/models.py:211) and reaches
+its arithmetic through `gpt.forward(inputs_embeds=, labels=, attention_mask=)`
+(src/models.py:321-325, :395) and `gpt.transformer.wte` (src/models.py:212,261,466).
+This module keeps that surface. `GPT2Core` holds the weights in the two GEMM
+orientations the kernels want (forward: [out,in]; backward dX: HF Conv1D [in,out])
+and implements the forward, the dX(/dW) backward and the KV-cached decode step as
+explicit kernel schedules (no autograd, no torch compute).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from types import SimpleNamespace
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import ops
+from .ops import Dropout
+from .weights import det_tensor
+
+Tensor = torch.Tensor
+
+
+@dataclass
+class GPT2Config:  # HF/models/gpt2/configuration_gpt2.py:84-103
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    n_embd: int = 768
+    n_layer: int = 12
+    n_head: int = 12
+    layer_norm_epsilon: float = 1e-5
+    resid_pdrop: float = 0.1
+    embd_pdrop: float = 0.1
+    attn_pdrop: float = 0.1
+    eos_token_id: int = 50256
+
+    @classmethod
+    def medium(cls):  # BASELINE configs[3]
+        return cls(n_embd=1024, n_layer=24, n_head=16)
+
+
+def pad_vocab(v: int) -> int:
+    return (v + 127) // 128 * 128
+
+
+# --------------------------------------------------------------------------- parameter containers (HF names)
+
+
+class Conv1D(nn.Module):
+    """HF/pytorch_utils.py:95-121 storage: weight [in, out], bias [out]."""
+
+    def __init__(self, nx: int, nf: int):
+        super().__init__()
+        self.weight = nn.Parameter(torch.zeros(nx, nf))
+        self.bias = nn.Parameter(torch.zeros(nf))
+
+
+class _Attn(nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.c_attn = Conv1D(d, 3 * d)
+        self.c_proj = Conv1D(d, d)
+
+
+class _MLP(nn.Module):
+    def __init__(self, d):
+        super().__init__()
+        self.c_fc = Conv1D(d, 4 * d)
+        self.c_proj = Conv1D(4 * d, d)
+
+
+class _Block(nn.Module):
+    def __init__(self, d, eps):
+        super().__init__()
+        self.ln_1 = nn.LayerNorm(d, eps=eps)
+        self.attn = _Attn(d)
+        self.ln_2 = nn.LayerNorm(d, eps=eps)
+        self.mlp = _MLP(d)
+
+
+class _Transformer(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        d = cfg.n_embd
+        self.wte = nn.Embedding(cfg.vocab_size, d)
+        self.wpe = nn.Embedding(cfg.n_positions, d)
+        self.h = nn.ModuleList([_Block(d, cfg.layer_norm_epsilon) for _ in range(cfg.n_layer)])
+        self.ln_f = nn.LayerNorm(d, eps=cfg.layer_norm_epsilon)
+
+
+class GPT2LMHeadModel(nn.Module):
+    """Drop-in for the `gpt=` argument of ImageCaptioningModel (src/models.py:189,211).
+
+    `.forward(inputs_embeds=, labels=, attention_mask=)` runs the HIP forward (inference) and returns an object
+    with `.loss` and `.logits` like HF's CausalLMOutputWithCrossAttentions."""
+
+    def __init__(self, config: Optional[GPT2Config] = None):
+        super().__init__()
+        self.config = config or GPT2Config()
+        self.transformer = _Transformer(self.config)
+        self.lm_head = nn.Linear(self.config.n_embd, self.config.vocab_size, bias=False)
+        self.lm_head.weight = self.transformer.wte.weight  # tied (modeling_gpt2.py:638)
+        self._core: Optional["GPT2Core"] = None
+        self._core_key = None
+
+    @classmethod
+    def random_init(cls, config: Optional[GPT2Config] = None, seed: int = 0) -> "GPT2LMHeadModel":
+        """Deterministic random weights of the GPT-2 architecture (no pretrained checkpoint is available offline)."""
+        m = cls(config)
+        cfg = m.config
+        d, nl = cfg.n_embd, cfg.n_layer
+        proj_std = 0.02 / math.sqrt(2 * nl)
+        with torch.no_grad():
+            t = m.transformer
+            t.wte.weight.copy_(det_tensor(seed, "wte", (cfg.vocab_size, d), 0.02))
+            t.wpe.weight.copy_(det_tensor(seed, "wpe", (cfg.n_positions, d), 0.01))
+            t.ln_f.weight.copy_(det_tensor(seed, "ln_f.w", (d,), 0.05, 1.0))
+            t.ln_f.bias.copy_(det_tensor(seed, "ln_f.b", (d,), 0.02))
+            for i, blk in enumerate(t.h):
+                p = f"transformer.h.{i}."
+                blk.ln_1.weight.copy_(det_tensor(seed, p + "ln_1.w", (d,), 0.05, 1.0))
+                blk.ln_1.bias.copy_(det_tensor(seed, p + "ln_1.b", (d,), 0.02))
+                blk.attn.c_attn.weight.copy_(det_tensor(seed, p + "c_attn.w", (d, 3 * d), 0.02))
+                blk.attn.c_attn.bias.copy_(det_tensor(seed, p + "c_attn.b", (3 * d,), 0.02))
+                blk.attn.c_proj.weight.copy_(det_tensor(seed, p + "attn.c_proj.w", (d, d), proj_std))
+                blk.attn.c_proj.bias.copy_(det_tensor(seed, p + "attn.c_proj.b", (d,), 0.02))
+                blk.ln_2.weight.copy_(det_tensor(seed, p + "ln_2.w", (d,), 0.05, 1.0))
+                blk.ln_2.bias.copy_(det_tensor(seed, p + "ln_2.b", (d,), 0.02))
+                blk.mlp.c_fc.weight.copy_(det_tensor(seed, p + "c_fc.w", (d, 4 * d), 0.02))
+                blk.mlp.c_fc.bias.copy_(det_tensor(seed, p + "c_fc.b", (4 * d,), 0.02))
+                blk.mlp.c_proj.weight.copy_(det_tensor(seed, p + "mlp.c_proj.w", (4 * d, d), proj_std))
+                blk.mlp.c_proj.bias.copy_(det_tensor(seed, p + "mlp.c_proj.b", (d,), 0.02))
+        return m
+
+    @classmethod
+    def from_pretrained(cls, path: str) -> "GPT2LMHeadModel":
+        """Load an HF GPT-2 checkpoint from a LOCAL directory or file (model.safetensors / pytorch_model.bin +
+        config.json). There is no network access: hub names only resolve through a local HF cache."""
+        import json
+        import os
+
+        cand = path
+        if not os.path.exists(cand):
+            try:
+                from huggingface_hub import snapshot_download
+
+                cand = snapshot_download(path, local_files_only=True)
+            except Exception as e:  # noqa: BLE001
+                raise FileNotFoundError(
+                    f"GPT-2 checkpoint '{path}' is not available locally (offline); pass gpt= explicitly, e.g. "
+                    "icap.GPT2LMHeadModel.random_init()") from e
+        cfg = GPT2Config()
+        if os.path.isdir(cand):
+            cj = os.path.join(cand, "config.json")
+            if os.path.exists(cj):
+                with open(cj) as f:
+                    j = json.load(f)
+                for k in ("vocab_size", "n_positions", "n_embd", "n_layer", "n_head", "layer_norm_epsilon",
+                          "resid_pdrop", "embd_pdrop", "attn_pdrop", "eos_token_id"):
+                    if k in j:
+                        setattr(cfg, k, j[k])
+            st = os.path.join(cand, "model.safetensors")
+            cand = st if os.path.exists(st) else os.path.join(cand, "pytorch_model.bin")
+        if cand.endswith(".safetensors"):
+            from safetensors.torch import load_file
+
+            sd = load_file(cand)
+        else:
+            sd = torch.load(cand, map_location="cpu", weights_only=True)
+        sd = {(k if k.startswith(("transformer.", "lm_head.")) else "transformer." + k): v for k, v in sd.items()
+              if not k.endswith((".attn.bias", ".attn.masked_bias"))}
+        m = cls(cfg)
+        m.load_state_dict(sd, strict=False)
+        return m
+
+    def core(self, dtype: torch.dtype) -> "GPT2Core":
+        dev = self.transformer.wte.weight.device
+        key = (dtype, dev)
+        if self._core is None or self._core_key != key:
+            self._core = GPT2Core(self, dtype)
+            self._core_key = key
+        return self._core
+
+    def invalidate_core(self):
+        self._core = None
+
+    def forward(self, inputs_embeds: Tensor, labels: Optional[Tensor] = None, attention_mask: Optional[Tensor] = None,
+                compute_dtype: Optional[torch.dtype] = None, **_):
+        """Inference forward on the HIP path (modeling_gpt2.py:650-725 semantics, dropout off)."""
+        dt = compute_dtype or (inputs_embeds.dtype if inputs_embeds.dtype in (torch.float32, torch.bfloat16)
+                               else torch.float32)
+        core = self.core(dt)
+        return core.forward_infer(inputs_embeds, attention_mask, labels)
+
+
+# --------------------------------------------------------------------------- compute core
+
+
+class _LayerW(SimpleNamespace):
+    pass
+
+
+class GPT2Core:
+    """GEMM-layout weights + kernel schedules for one GPT2LMHeadModel in one compute dtype."""
+
+    def __init__(self, model: GPT2LMHeadModel, dtype: torch.dtype):
+        self.model = model
+        self.cfg = model.config
+        self.dtype = dtype
+        self.dev = model.transformer.wte.weight.device
+        from ._lib import require_device
+
+        require_device(self.dev)
+        c = self.cfg
+        self.D, self.H = c.n_embd, c.n_head
+        self.hd = self.D // self.H
+        self.V = c.vocab_size
+        self.Vp = pad_vocab(self.V)
+        self.layers: List[_LayerW] = []
+        self.refresh()
+
+    # -- weights ---------------------------------------------------------------------------------------
+    def _both(self, w: Tensor):
+        """HF Conv1D master [in,out] fp32 -> (fwd [out,in], bwd [in,out]) in the compute dtype."""
+        nin, nout = w.shape
+        fwd = torch.empty((nout, nin), dtype=self.dtype, device=self.dev)
+        if self.dtype == torch.float32:
+            bwd = w.data
+            ops.transpose(bwd, fwd)
+        else:
+            bwd = torch.empty((nin, nout), dtype=self.dtype, device=self.dev)
+            ops.convert(w.data, bwd)
+            ops.transpose(bwd, fwd)
+        return fwd, bwd
+
+    @torch.no_grad()
+    def refresh(self) -> None:
+        """(Re)build the compute copies from the fp32 masters (once when frozen; after each step when trained)."""
+        t = self.model.transformer
+        self.layers = []
+        for blk in t.h:
+            lw = _LayerW()
+            lw.w_attn_t, lw.w_attn = self._both(blk.attn.c_attn.weight)
+            lw.w_proj_t, lw.w_proj = self._both(blk.attn.c_proj.weight)
+            lw.w_fc_t, lw.w_fc = self._both(blk.mlp.c_fc.weight)
+            lw.w_mp_t, lw.w_mp = self._both(blk.mlp.c_proj.weight)
+            lw.b_attn, lw.b_proj = blk.attn.c_attn.bias.data, blk.attn.c_proj.bias.data
+            lw.b_fc, lw.b_mp = blk.mlp.c_fc.bias.data, blk.mlp.c_proj.bias.data
+            lw.ln1_g, lw.ln1_b = blk.ln_1.weight.data, blk.ln_1.bias.data
+            lw.ln2_g, lw.ln2_b = blk.ln_2.weight.data, blk.ln_2.bias.data
+            self.layers.append(lw)
+        self.lnf_g, self.lnf_b = t.ln_f.weight.data, t.ln_f.bias.data
+        D, V, Vp = self.D, self.V, self.Vp
+        self.wte = torch.zeros((Vp, D), dtype=self.dtype, device=self.dev)  # LM-head B operand + embedding table
+        ops.convert(t.wte.weight.data, self.wte[:V])
+        self.wte_t = torch.empty((D, Vp), dtype=self.dtype, device=self.dev)  # LM-head dX B operand
+        ops.transpose(self.wte, self.wte_t)
+        if self.dtype == torch.float32:
+            self.wpe = t.wpe.weight.data
+        else:
+            self.wpe = torch.empty_like(t.wpe.weight.data, dtype=self.dtype)
+            ops.convert(t.wpe.weight.data, self.wpe)
+        self.eps = self.cfg.layer_norm_epsilon
+
+    # -- workspaces --------------------------------------------------------------------------------------
+    def alloc_train(self, B: int, P: int, Lc: int, keep_for_dw: bool = False) -> SimpleNamespace:
+        S = P + Lc
+        M = B * S
+        D, H, dt, dev = self.D, self.H, self.dtype, self.dev
+        nl = self.cfg.n_layer
+        e = lambda *shape, dtype=dt: torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
+        ws = SimpleNamespace(B=B, P=P, Lc=Lc, S=S, M=M)
+        ws.x = [e(M, D) for _ in range(nl + 1)]
+        ws.h1 = [e(M, D) for _ in range(nl)]
+        ws.qkv = [e(M, 3 * D) for _ in range(nl)]
+        ws.z = [e(M, 4 * D) for _ in range(nl)]
+        ws.mean1 = [e(M, dtype=torch.float32) for _ in range(nl)]
+        ws.rstd1 = [e(M, dtype=torch.float32) for _ in range(nl)]
+        ws.mean2 = [e(M, dtype=torch.float32) for _ in range(nl)]
+        ws.rstd2 = [e(M, dtype=torch.float32) for _ in range(nl)]
+        ws.lse = [e(B * H * S, dtype=torch.float32) for _ in range(nl)]
+        ws.meanf, ws.rstdf = e(M, dtype=torch.float32), e(M, dtype=torch.float32)
+        if keep_for_dw:
+            ws.a1 = [e(M, D) for _ in range(nl)]
+            ws.o = [e(M, D) for _ in range(nl)]
+            ws.a2 = [e(M, D) for _ in range(nl)]
+            ws.f = [e(M, 4 * D) for _ in range(nl)]
+        else:
+            a, o, a2, f = e(M, D), e(M, D), e(M, D), e(M, 4 * D)
+            ws.a1, ws.o, ws.a2, ws.f = [a] * nl, [o] * nl, [a2] * nl, [f] * nl
+        ws.hf = e(M, D)
+        ws.logits = e(M, self.Vp)
+        ws.key_mask = e(M, dtype=torch.int32)
+        ws.labels_shift = e(M, dtype=torch.int32)
+        ws.n_valid = e(1, dtype=torch.int32)
+        ws.loss = e(1, dtype=torch.float32)
+        ws.ce_ws = e(ops.cross_entropy_workspace(M), dtype=torch.uint8)
+        # backward scratch
+        ws.dx, ws.dx2, ws.dxd = e(M, D), e(M, D), e(M, D)
+        ws.dff = e(M, 4 * D)
+        ws.dqkv = e(M, 3 * D)
+        ws.do, ws.da = e(M, D), e(M, D)
+        ws.dhf = e(M, D)
+        return ws
+
+    # -- dropout sites (distinct offsets so masks never coincide) -------------------------------------------
+    def drops(self, train: bool, seed: int, counter: Optional[Tensor], M: int, B: int, S: int):
+        c = self.cfg
+        if not train:
+            z = Dropout()
+            return SimpleNamespace(embd=z, attn=lambda l: z, ra=lambda l: z, rm=lambda l: z)
+        D, H = self.D, self.H
+        blk = 4 * M * D + B * H * S * S
+
+        def mk(p, off):
+            return Dropout(p, seed, off, counter)
+
+        return SimpleNamespace(
+            embd=mk(c.embd_pdrop, 0),
+            attn=lambda l: mk(c.attn_pdrop, M * D + l * blk),
+            ra=lambda l: mk(c.resid_pdrop, M * D + l * blk + B * H * S * S),
+            rm=lambda l: mk(c.resid_pdrop, M * D + l * blk + B * H * S * S + M * D),
+        )
+
+    # -- training forward ------------------------------------------------------------------------------------
+    def forward_train(self, ws, prefix: Tensor, prefix_bstride: int, ids: Tensor, mask: Optional[Tensor],
+                      labels: Optional[Tensor], dr, fuse_dlogits: bool, grad_scale: float = 1.0,
+                      dlogits: Optional[Tensor] = None) -> None:
+        """Embeddings -> 12 blocks -> ln_f -> LM head -> CE (modeling_gpt2.py:514-725 + loss_utils.py:49-71).
+        With fuse_dlogits the CE kernel also writes dlogits (in place over the logits, or into `dlogits`)."""
+        B, P, Lc, S, M = ws.B, ws.P, ws.Lc, ws.S, ws.M
+        D, H, hd = self.D, self.H, self.hd
+        ops.caption_prep(B, P, Lc, mask, labels, ws.key_mask, ws.labels_shift, ws.n_valid)
+        ops.gpt2_embed(prefix, prefix_bstride, self.wte, self.wpe, ids, ws.x[0], B=B, P=P, L_=Lc, D=D, drop=dr.embd)
+        self._blocks_fwd(ws, dr, B, S, M, causal_mask=ws.key_mask if mask is not None else None)
+        ops.layernorm_fwd(ws.x[-1], self.lnf_g, self.lnf_b, self.eps, ws.hf, ws.meanf, ws.rstdf)
+        ops.gemm(ws.hf, self.wte, ws.logits)
+        if labels is not None:
+            dl = (dlogits if dlogits is not None else ws.logits) if fuse_dlogits else None
+            ops.cross_entropy(ws.logits, self.V, ws.labels_shift, ws.n_valid, ws.loss, dl, ws.ce_ws, grad_scale)
+
+    def _blocks_fwd(self, ws, dr, B, S, M, causal_mask):
+        D, H, hd = self.D, self.H, self.hd
+        scale = 1.0 / math.sqrt(hd)
+        for l, lw in enumerate(self.layers):
+            x = ws.x[l]
+            ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, ws.a1[l], ws.mean1[l], ws.rstd1[l])
+            ops.gemm(ws.a1[l], lw.w_attn_t, ws.qkv[l], bias=lw.b_attn)
+            ops.attention_fwd(ws.qkv[l], ws.o[l], B=B, S=S, H=H, hd=hd, scale=scale, causal=True, key_mask=causal_mask,
+                              lse=ws.lse[l], drop=dr.attn(l))
+            ops.gemm(ws.o[l], lw.w_proj_t, ws.h1[l], bias=lw.b_proj, resid=x, drop=dr.ra(l))
+            ops.layernorm_fwd(ws.h1[l], lw.ln2_g, lw.ln2_b, self.eps, ws.a2[l], ws.mean2[l], ws.rstd2[l])
+            ops.gemm(ws.a2[l], lw.w_fc_t, ws.f[l], bias=lw.b_fc, act=L.ACT_GELU_NEW, aux=ws.z[l])
+            ops.gemm(ws.f[l], lw.w_mp_t, ws.x[l + 1], bias=lw.b_mp, resid=ws.h1[l], drop=dr.rm(l))
+
+    # -- backward (dX through the frozen GPT-2; + dW when trainable) ---------------------------------------------
+    def backward(self, ws, dr, causal_mask, dlogits: Tensor, grads=None, dw=None) -> Tensor:
+        """Returns d(inputs_embeds) [M, D] (embedding dropout applied). `grads`: object with per-layer fp32 grad
+        views (trainable GPT-2) and `dw`: a DWHelper; both None when GPT-2 is frozen."""
+        B, S, M = ws.B, ws.S, ws.M
+        D, H, hd = self.D, self.H, self.hd
+        scale = 1.0 / math.sqrt(hd)
+        nl = len(self.layers)
+        ops.gemm(dlogits, self.wte_t, ws.dhf)  # dh_f = dlogits . wte  (K = padded vocab)
+        if grads is not None:  # d(wte) from the tied LM head: dW[V,D] += dlogits^T . hf
+            dw.dW(dlogits, ws.hf, grads.wte, M=M, N=self.V)
+        ops.layernorm_bwd(ws.x[-1], self.lnf_g, ws.meanf, ws.rstdf, ws.dhf, ws.dx, dx_drop=ws.dxd,
+                          drop=dr.rm(nl - 1), dgamma=grads.lnf_g if grads else None,
+                          dbeta=grads.lnf_b if grads else None, workspace=dw.ln_ws if dw else None)
+        dres, dnew = ws.dx, ws.dx2
+        for l in reversed(range(nl)):
+            lw = self.layers[l]
+            g = grads.layers[l] if grads is not None else None
+            dy = ws.dxd if dr.rm(l).p > 0 else dres
+            if g is not None:
+                dw.dW(dy, ws.f[l], g.w_mp, M=M, transpose_out=True)
+                dw.db(dy, g.b_mp, M=M)
+            ops.gemm(dy, lw.w_mp, ws.dff, dact=L.ACT_GELU_NEW, dact_src=ws.z[l])
+            if g is not None:
+                dw.dW(ws.dff, ws.a2[l], g.w_fc, M=M, transpose_out=True)
+                dw.db(ws.dff, g.b_fc, M=M)
+            ops.gemm(ws.dff, lw.w_fc, ws.da)
+            ops.layernorm_bwd(ws.h1[l], lw.ln2_g, ws.mean2[l], ws.rstd2[l], ws.da, dnew, dres=dres, dx_drop=ws.dxd,
+                              drop=dr.ra(l), dgamma=g.ln2_g if g else None, dbeta=g.ln2_b if g else None,
+                              workspace=dw.ln_ws if dw else None)
+            dres, dnew = dnew, dres
+            dy = ws.dxd if dr.ra(l).p > 0 else dres
+            if g is not None:
+                dw.dW(dy, ws.o[l], g.w_proj, M=M, transpose_out=True)
+                dw.db(dy, g.b_proj, M=M)
+            ops.gemm(dy, lw.w_proj, ws.do)
+            ops.attention_bwd(ws.qkv[l], ws.do, ws.lse[l], ws.dqkv, B=B, S=S, H=H, hd=hd, scale=scale, causal=True,
+                              key_mask=causal_mask, drop=dr.attn(l))
+            if g is not None:
+                dw.dW(ws.dqkv, ws.a1[l], g.w_attn, M=M, transpose_out=True)
+                dw.db(ws.dqkv, g.b_attn, M=M)
+            ops.gemm(ws.dqkv, lw.w_attn, ws.da)
+            nxt = dr.rm(l - 1) if l > 0 else dr.embd
+            ops.layernorm_bwd(ws.x[l], lw.ln1_g, ws.mean1[l], ws.rstd1[l], ws.da, dnew, dres=dres, dx_drop=ws.dxd,
+                              drop=nxt, dgamma=g.ln1_g if g else None, dbeta=g.ln1_b if g else None,
+                              workspace=dw.ln_ws if dw else None)
+            dres, dnew = dnew, dres
+        return ws.dxd if dr.embd.p > 0 else dres
+
+    # -- inference ----------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def forward_infer(self, inputs_embeds: Tensor, attention_mask: Optional[Tensor], labels: Optional[Tensor]):
+        B, S, D = inputs_embeds.shape
+        x_in = inputs_embeds
+        if x_in.dtype != self.dtype or not x_in.is_contiguous():
+            x_in = inputs_embeds.to(self.dtype).contiguous()
+        ws = self.alloc_train(B, S, 0)
+        dr = self.drops(False, 0, None, ws.M, B, S)
+        mask = attention_mask.to(torch.int64) if attention_mask is not None else None
+        lab = labels.to(torch.int64) if labels is not None else None
+        # all S positions come in as "prefix" rows (ids unused): x = inputs_embeds + wpe
+        ops.caption_prep(B, S, 0, None, None, ws.key_mask, None, None)
+        if mask is not None:
+            ws.key_mask.copy_(mask.reshape(-1).to(torch.int32))
+        if lab is not None:
+            ops.caption_prep(B, 0, S, None, lab.contiguous(), None, ws.labels_shift, ws.n_valid)
+        ops.gpt2_embed(x_in, S * D, self.wte, self.wpe, None, ws.x[0], B=B, P=S, L_=0, D=D, drop=dr.embd)
+        self._blocks_fwd(ws, dr, B, S, ws.M, causal_mask=ws.key_mask if mask is not None else None)
+        ops.layernorm_fwd(ws.x[-1], self.lnf_g, self.lnf_b, self.eps, ws.hf, ws.meanf, ws.rstdf)
+        ops.gemm(ws.hf, self.wte, ws.logits)
+        loss = None
+        if lab is not None:
+            ops.cross_entropy(ws.logits, self.V, ws.labels_shift, ws.n_valid, ws.loss, None, ws.ce_ws)
+            loss = ws.loss[0].clone()
+        logits = ws.logits[:, : self.V].float().reshape(B, S, self.V)
+        return SimpleNamespace(loss=loss, logits=logits)
+
+    # -- KV-cached greedy decode (src/models.py:327-477, temperature 0) ----------------------------------------
+    def alloc_decode(self, B: int, P: int, max_length: int) -> SimpleNamespace:
+        D, dt, dev = self.D, self.dtype, self.dev
+        T = P + max_length
+        e = lambda *shape, dtype=dt: torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
+        ds = SimpleNamespace(B=B, P=P, T=T, max_length=max_length)
+        ds.cache = [e(T * B, 3 * D) for _ in self.layers]
+        ds.x = e(P * B, D)
+        ds.h1 = e(P * B, D)
+        ds.a = e(P * B, D)
+        ds.o = e(P * B, D)
+        ds.f = e(P * B, 4 * D)
+        ds.logits = e(B, self.Vp)
+        ds.finished = torch.zeros(B, dtype=torch.int32, device=dev)
+        ds.tokens = torch.full((B, max_length), self.cfg.eos_token_id, dtype=torch.int64, device=dev)
+        ds.km = torch.ones(P * B, dtype=torch.int32, device=dev)
+        return ds
+
+    def _decode_block(self, ds, rows: int, x: Tensor, pos0: int, npos: int, prefill: bool):
+        """One pass of all blocks over `rows` = npos*B position-major rows starting at position pos0."""
+        D, H, hd = self.D, self.H, self.hd
+        B = ds.B
+        scale = 1.0 / math.sqrt(hd)
+        a, o, h1, f = ds.a[:rows], ds.o[:rows], ds.h1[:rows], ds.f[:rows]
+        for l, lw in enumerate(self.layers):
+            ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, a, None, None, rows=rows)
+            qkv = ds.cache[l][pos0 * B: (pos0 + npos) * B]
+            ops.gemm(a, lw.w_attn_t, qkv, bias=lw.b_attn, M=rows)
+            if prefill:
+                ops.attention_fwd(ds.cache[l], o, B=B, S=npos, H=H, hd=hd, scale=scale, causal=True, rsb=1, rss=B)
+            else:
+                ops.attention_decode(ds.cache[l], o, B=B, H=H, hd=hd, pos=pos0, scale=scale)
+            ops.gemm(o, lw.w_proj_t, h1, bias=lw.b_proj, resid=x, M=rows)
+            ops.layernorm_fwd(h1, lw.ln2_g, lw.ln2_b, self.eps, a, None, None, rows=rows)
+            ops.gemm(a, lw.w_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows)
+            ops.gemm(f, lw.w_mp_t, x, bias=lw.b_mp, resid=h1, M=rows)
+
+    def _decode_head(self, ds, x_last: Tensor, step: int, pos_next: int):
+        D = self.D
+        B = ds.B
+        a = ds.a[:B]
+        ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
+        ops.gemm(a, self.wte, ds.logits, M=B)
+        nxt_x = ds.x[:B] if pos_next < ds.T else None
+        ops.greedy_next(ds.logits, self.V, self.cfg.eos_token_id, ds.finished, ds.tokens, step,
+                        self.wte if nxt_x is not None else None, self.wpe if nxt_x is not None else None,
+                        min(pos_next, self.cfg.n_positions - 1), D, nxt_x)
+
+    @torch.no_grad()
+    def greedy_decode(self, prefix: Tensor, max_length: int, check_every: int = 8) -> Tensor:
+        """prefix [B,P,D] (compute dtype) -> token ids [B, <=max_length] with the reference's EOS latch and
+        early exit (src/models.py:389-391,453-460). Exact to the reference's full-recompute loop: causal
+        attention makes cached keys/values of earlier positions identical to recomputed ones."""
+        B, P, D = prefix.shape
+        if max_length <= 0:
+            return torch.empty((B, 0), dtype=torch.long, device=prefix.device)
+        ds = self.alloc_decode(B, P, max_length)
+        pre = prefix if (prefix.dtype == self.dtype and prefix.stride(-1) == 1) else prefix.to(self.dtype).contiguous()
+        ops.add_position(pre, pre.stride(0), pre.stride(1), self.wpe, ds.x, B=B, npos=P, D=D, pos0=0)
+        self._decode_block(ds, P * B, ds.x, 0, P, prefill=True)
+        self._decode_head(ds, ds.x[(P - 1) * B: P * B], 0, P)
+        steps = 1
+        for s in range(1, max_length):
+            if s % check_every == 0 and bool(ds.finished.bool().all()):
+                break
+            pos = P + s - 1
+            self._decode_block(ds, B, ds.x[:B], pos, 1, prefill=False)
+            self._decode_head(ds, ds.x[:B], s, pos + 1)
+            steps = s + 1
+        toks = ds.tokens[:, :steps]
+        # reference loop length: stops before the first step at which every row had already finished
+        return self._truncate(toks, steps)
+
+    def _truncate(self, toks: Tensor, steps: int) -> Tensor:
+        B = toks.shape[0]
+        is_eos = toks == self.cfg.eos_token_id
+        first = torch.where(is_eos.any(1), is_eos.float().argmax(1), torch.full((B,), steps, device=toks.device))
+        n = int(min(steps, int(first.max().item()) + 1))
+        return toks[:, :n].clone()
+
+    @torch.no_grad()
+    def sample_decode(self, prefix: Tensor, max_length: int, temperature: float, top_p: float) -> Tensor:
+        """Temperature / nucleus sampling branch of src/models.py:400-449 over the KV-cached decoder. The logits
+        come from the HIP kernels; the top-p filter and multinomial draw use torch device ops on the [B, V]
+        last-position logits (not on the training hot path)."""
+        B, P, D = prefix.shape
+        if max_length <= 0:
+            return torch.empty((B, 0), dtype=torch.long, device=prefix.device)
+        ds = self.alloc_decode(B, P, max_length)
+        pre = prefix if (prefix.dtype == self.dtype and prefix.stride(-1) == 1) else prefix.to(self.dtype).contiguous()
+        ops.add_position(pre, pre.stride(0), pre.stride(1), self.wpe, ds.x, B=B, npos=P, D=D, pos0=0)
+        self._decode_block(ds, P * B, ds.x, 0, P, prefill=True)
+        x_last = ds.x[(P - 1) * B: P * B]
+        steps = 0
+        for s in range(max_length):
+            if s > 0:
+                if bool(ds.finished.bool().all()):
+                    break
+                pos = P + s - 1
+                self._decode_block(ds, B, ds.x[:B], pos, 1, prefill=False)
+                x_last = ds.x[:B]
+            a = ds.a[:B]
+            ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
+            ops.gemm(a, self.wte, ds.logits, M=B)
+            logits = ds.logits[:, : self.V].float() / temperature
+            fin = ds.finished.bool()
+            if top_p < 1.0:
+                logits[fin, :] = 0.0
+                sl, si = torch.sort(logits, descending=True)
+                cp = torch.cumsum(torch.softmax(sl, dim=-1), dim=-1)
+                rm = cp > top_p
+                rm[:, 1:] = rm[:, :-1].clone()
+                rm[:, 0] = False
+                logits = logits.masked_fill(rm.scatter(1, si, rm), float("-inf"))
+            nxt = torch.multinomial(torch.softmax(logits, dim=-1), 1).reshape(B).contiguous()
+            pos_next = P + s
+            nxt_x = ds.x[:B] if pos_next < ds.T else None
+            ops.greedy_next(ds.logits, self.V, self.cfg.eos_token_id, ds.finished, ds.tokens, s,
+                            self.wte if nxt_x is not None else None, self.wpe if nxt_x is not None else None,
+                            min(pos_next, self.cfg.n_positions - 1), D, nxt_x, forced=nxt)
+            steps = s + 1
+        return self._truncate(ds.tokens[:, :steps], steps)

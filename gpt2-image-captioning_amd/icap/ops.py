@@ -292,9 +292,10 @@ def l2norm_rows(x: Tensor, out: Tensor, rows: Optional[int] = None) -> Tensor:
 
 
 def greedy_next(logits: Tensor, V: int, eos: int, finished: Tensor, tokens: Tensor, step: int,
-                wte: Optional[Tensor], wpe: Optional[Tensor], pos: int, D: int, x: Optional[Tensor]) -> None:
+                wte: Optional[Tensor], wpe: Optional[Tensor], pos: int, D: int, x: Optional[Tensor],
+                forced: Optional[Tensor] = None) -> None:
     B = finished.shape[0]
-    call("icap_greedy_next", dtype_code(logits.dtype), B, V, logits.data_ptr(), _ld(logits), eos,
+    call("icap_greedy_next", dtype_code(logits.dtype), B, V, logits.data_ptr(), _ld(logits), eos, _p(forced),
          finished.data_ptr(), tokens.data_ptr(), _ld(tokens), step, _p(wte), _p(wpe), pos, D, _p(x), _stream())
 
 
@@ -303,3 +304,9 @@ def add_position(src: Tensor, src_bstride: int, src_tstride: int, wpe: Tensor, x
     call("icap_add_position", dtype_code(x.dtype), B, npos, D, src.data_ptr(), src_bstride, src_tstride,
          wpe.data_ptr(), pos0, x.data_ptr(), _stream())
     return x
+
+
+def embedding_scatter_add(dx: Tensor, ids: Tensor, dwte: Tensor, *, B: int, P: int, L_: int, D: int) -> Tensor:
+    call("icap_embedding_scatter_add", dtype_code(dx.dtype), B, P, L_, D, dx.data_ptr(), ids.data_ptr(),
+         dwte.data_ptr(), _stream())
+    return dwte

@@ -158,6 +158,10 @@ int icap_gpt2_embed(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D,
                     const void* prefix, int64_t prefix_bstride, const void* wte,
                     const void* wpe, const int64_t* ids, void* x, float drop_p,
                     uint64_t seed, uint64_t offset, const uint64_t* seed_ptr, void* stream);
+/* backward of the caption-token gather when GPT-2 is trained (freeze_gpt_weights=False): */
+/* dwte[ids[b,t]] += dx[b*(P+L) + P + t]  (fp32 atomics)                                    */
+int icap_embedding_scatter_add(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D,
+                               const void* dx, const int64_t* ids, float* dwte, void* stream);
 int icap_caption_prep(int32_t B, int32_t P, int32_t L, const int64_t* mask,
                       const int64_t* labels, int32_t* key_mask, int32_t* labels_shift,
                       int32_t* n_valid, void* stream);
@@ -241,11 +245,12 @@ int icap_l2norm_rows(int32_t dtype, int64_t rows, int64_t D, const void* x, int6
 /* ------------------------------------------------------------------------- */
 /* Greedy-decode step helpers (src/models.py:389-469).                        */
 /* ------------------------------------------------------------------------- */
-/* next[b] = finished[b] ? eos : argmax_v(logits[b, :V]) (first max on ties);  */
+/* next[b] = finished[b] ? eos : (forced ? forced[b] : argmax_v(logits[b, :V]))  */
+/* (argmax: first max on ties; forced: ids drawn by the top-p sampler);          */
 /* finished[b] |= next[b]==eos; tokens[b*ld_tokens + step] = next[b];          */
 /* x[b] = wte[next[b]] + wpe[pos] (the next step's input embedding).           */
 int icap_greedy_next(int32_t dtype, int32_t B, int64_t V, const void* logits, int64_t ld,
-                     int64_t eos, int32_t* finished, int64_t* tokens, int64_t ld_tokens,
+                     int64_t eos, const int64_t* forced, int32_t* finished, int64_t* tokens, int64_t ld_tokens,
                      int32_t step, const void* wte, const void* wpe, int32_t pos, int32_t D,
                      void* x, void* stream);
 /* x[(t*B + b)*D + d] = src[b*src_bstride + t*src_tstride + d] + wpe[(pos0+t)*D + d], t < npos */

@@ -1,0 +1,69 @@
+"""C-ABI checks that need no GPU: libicap_hip.so loads, exports every entry point include/icap.h declares,
+the ctypes binding mirrors the header (names, struct layouts via gcc offsetof), and host-only queries work."""
+
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from icap import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "icap.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(icap_\w+)\s*\(", src)))
+
+
+def test_header_functions_exported_and_bound():
+    lib = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in icap.h but not exported"
+        assert n in _lib.SIGNATURES, f"{n} declared in icap.h but not bound in _lib.SIGNATURES"
+    assert set(_lib.SIGNATURES) == set(names)
+
+
+def test_version_and_workspace_queries():
+    lib = _lib.load()
+    assert lib.icap_version() >= 1
+    assert lib.icap_layernorm_bwd_workspace_bytes(8320, 768) > 0
+    assert lib.icap_cross_entropy_workspace_bytes(100) == 400
+    assert lib.icap_colsum_workspace_bytes(3200, 3072) >= 3072 * 4
+    assert lib.icap_adamw_workspace_bytes(1000) >= 4
+
+
+@pytest.mark.parametrize("struct,cname", [(_lib.GemmArgs, "icap_gemm_args"), (_lib.AttnArgs, "icap_attn_args"),
+                                          (_lib.AdamWArgs, "icap_adamw_args")])
+def test_struct_layout_matches_header(struct, cname):
+    fields = [f for f, _ in struct._fields_]
+    prog = ["#include <stdio.h>", "#include <stddef.h>", '#include "icap.h"', "int main(void){",
+            f'printf("%zu\\n", sizeof({cname}));']
+    prog += [f'printf("%zu\\n", offsetof({cname}, {f}));' for f in fields]
+    prog += ["return 0;}"]
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write("\n".join(prog))
+        exe = os.path.join(d, "t")
+        subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe])
+        vals = [int(x) for x in subprocess.check_output([exe]).split()]
+    assert vals[0] == C.sizeof(struct)
+    for f, off in zip(fields, vals[1:]):
+        assert getattr(struct, f).offset == off, f
+
+
+def test_error_reporting_without_gpu():
+    # argument validation runs before any HIP call: a bad GEMM must fail with a message, not crash
+    a = _lib.GemmArgs()
+    a.M, a.N, a.K = 4, 4, 3  # K not a multiple of 4/8
+    a.A = a.B = a.C = 16
+    a.lda = a.ldb = a.ldc = 4
+    with pytest.raises(_lib.IcapError, match="K must be a multiple"):
+        _lib.call("icap_gemm", C.byref(a), None)

@@ -1,0 +1,106 @@
+"""CPU-only: every kernel launch of the product schedules stays inside live allocations (tests/dryrun.py).
+
+Runs the real host code of the train step, the autograd drop-in path, inference, greedy decode and the
+CLIP tower with the C-ABI calls recorded instead of launched, then checks each recorded pointer extent."""
+
+from types import SimpleNamespace
+
+import pytest
+import torch
+
+import icap.weights
+from dryrun import dry_run
+from icap import CaptionTrainer, GPT2Config, GPT2LMHeadModel, ImageCaptioningModel, MLPMappingNetwork
+from icap import TransformerMappingNetwork
+from icap.clip import CLIPVisionConfig, CLIPVisionTower
+
+CPU = torch.device("cpu")
+
+
+def tiny_model(mapper="transformer", freeze=True, dtype=torch.float32, task_prompt=None):
+    cfg = GPT2Config(vocab_size=512, n_positions=128, n_embd=128, n_layer=2, n_head=2, eos_token_id=511)
+    gpt = GPT2LMHeadModel(cfg)
+    if mapper == "transformer":
+        m = TransformerMappingNetwork(64, 128, 5, 4, 2)
+    else:
+        m = MLPMappingNetwork(5, 64, 128)
+    tok = SimpleNamespace(eos_token_id=511, encode=lambda s, return_tensors=None: torch.tensor([[1, 2, 3]]))
+    return ImageCaptioningModel(m, prefix_task_prompt=task_prompt, tokenizer=tok, gpt=gpt, freeze_gpt_weights=freeze,
+                                compute_dtype=dtype)
+
+
+def batch(B, L, vocab=512, E=64):
+    ids = torch.randint(0, vocab - 1, (B, L))
+    mask = torch.ones((B, L), dtype=torch.int64)
+    mask[:, L // 2:] = 0
+    labels = ids.clone()
+    labels[mask == 0] = -100
+    return ids, mask, labels, torch.randn(B, E)
+
+
+def _assert_clean(rec):
+    assert rec.calls, "nothing recorded"
+    bad = rec.check()
+    assert not bad, "\n".join(bad[:20])
+
+
+@pytest.mark.parametrize("mapper", ["transformer", "mlp"])
+@pytest.mark.parametrize("dropout", [False, True])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_trainer_step_in_bounds(mapper, dropout, dtype):
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model(mapper, dtype=dtype)
+        t = CaptionTrainer(model, 3, 12, num_training_steps=3, dropout=dropout)
+        t.load_batch(*batch(3, 12))
+        t.micro_step()
+        _assert_clean(rec)
+
+
+def test_trainer_task_prefix_in_bounds():
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model(task_prompt="A picture of")
+        t = CaptionTrainer(model, 4, 10, num_training_steps=3)
+        t.load_batch(*batch(4, 10))
+        t.micro_step()
+        _assert_clean(rec)
+
+
+@pytest.mark.parametrize("freeze", [True, False])
+def test_autograd_dropin_in_bounds(freeze):
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model(freeze=freeze)
+        ids, mask, labels, emb = batch(3, 12)
+        out = model(ids, emb, mask, labels)
+        out.loss.backward()
+        _assert_clean(rec)
+
+
+def test_inference_and_greedy_in_bounds():
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model()
+        ids, mask, labels, emb = batch(3, 12)
+        with torch.no_grad():
+            model(ids, emb, mask, labels)
+        model.generate(emb, max_length=9, temperature=0.0)
+        model.gpt(inputs_embeds=torch.randn(2, 7, 128), attention_mask=torch.ones(2, 7, dtype=torch.int64))
+        _assert_clean(rec)
+
+
+def test_gpt2_small_bench_shape_with_clip_in_bounds():
+    """The benchmarked configuration (GPT-2 small + ViT-B/32 + transformer mapper, bf16) at B=8."""
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        gpt = GPT2LMHeadModel(GPT2Config())
+        model = ImageCaptioningModel(TransformerMappingNetwork(512, 768, 15, 10), tokenizer=SimpleNamespace(
+            eos_token_id=50256), gpt=gpt, compute_dtype=torch.bfloat16)
+        tower = CLIPVisionTower(CLIPVisionConfig())
+        t = CaptionTrainer(model, 8, 50, num_training_steps=10, clip_model=tower)
+        ids, mask, labels, _ = batch(8, 50, vocab=50257, E=512)
+        t.load_batch(ids, mask, labels, pixels=torch.randn(8, 3, 224, 224))
+        t.micro_step()
+        model.generate(torch.randn(4, 512), max_length=3, temperature=0.0)
+        _assert_clean(rec)
