@@ -1,0 +1,243 @@
+"""Benchmark of the hot path on MI355X (contract: README / DESIGN.md "Measurement").
+
+Workload (BASELINE.json configs[1]): one training step of GPT-2 small (frozen) + CLIP ViT-B/32 image tower
+(frozen, forward on synthetic 224x224 pixels) + transformer mapping network (trained), bf16 storage / fp32
+accumulation, dropout 0.1 as in the reference's train mode, teacher-forced CE over 50-token COCO-shaped captions,
+clip_grad_norm(1.0) + AdamW + linear LR schedule; B=128 images per GPU (config.yml training.batch_size).
+Weights are the deterministic random init of that architecture (no checkpoints offline); data are synthetic.
+
+value = training images/s over all ranks. Also reported: greedy captions/s (50-token KV-cached decode,
+B=128 per GPU = config.yml validation.batch_size), the GEMM roofline (per-launch HIP-event timing of every MFMA
+GEMM of one step; algorithmic FLOPs), and the CPU baseline (oracle restatement of the reference step on a bounded
+sample, rank 0 only).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gpt2-image-captioning_amd")]
+
+import torch  # noqa: E402
+
+METRIC = "training images/sec + greedy captions/sec, GPT2-small+CLIP-B/32 at 1/2/4/8 GPU"
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+HBM_PEAK_GBS = 8000.0
+
+
+class GemmTimer:
+    """HIP-event timing of each GEMM launch on the launching stream (icap.ops.GEMM_TIMER hook)."""
+
+    def __init__(self):
+        self.rec = []
+
+    def launch(self, key, flops, fn):
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        fn()
+        e1.record(s)
+        self.rec.append((key, flops, e0, e1))
+
+    def summary(self, detail_path=None):
+        """Aggregate per kernel instantiation (what rocprof reports per kernel name); optional per-shape dump."""
+        torch.cuda.synchronize()
+        agg, shapes = {}, {}
+        for (kind, desc), fl, e0, e1 in self.rec:
+            ms = e0.elapsed_time(e1)
+            for d, k in ((agg, kind), (shapes, (kind, desc))):
+                a = d.setdefault(k, [0, 0.0, 0.0])
+                a[0] += 1
+                a[1] += fl
+                a[2] += ms
+        if detail_path:
+            with open(detail_path, "w") as f:
+                for (kind, desc), (n, fl, ms) in sorted(shapes.items(), key=lambda kv: -kv[1][2]):
+                    f.write(f"{kind:10s} {desc:60s} n={n:3d} total_ms={ms:8.3f} avg_us={ms / n * 1e3:9.1f} "
+                            f"TF/s={fl / (ms * 1e-3) / 1e12:8.1f}\n")
+        return agg
+
+
+def build(B, dev, dropout=True):
+    from types import SimpleNamespace
+
+    from icap import CaptionTrainer, GPT2LMHeadModel, ImageCaptioningModel, TransformerMappingNetwork
+    from icap.clip import CLIPVisionTower
+
+    gpt = GPT2LMHeadModel.random_init(seed=0)
+    mapper = TransformerMappingNetwork.random_init(seed=0)
+    model = ImageCaptioningModel(mapper, tokenizer=SimpleNamespace(eos_token_id=50256), gpt=gpt,
+                                 compute_dtype=torch.bfloat16).to(dev)
+    tower = CLIPVisionTower.random_init(seed=0).to(dev)
+    trainer = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10 ** 6, clip_model=tower, dropout=dropout,
+                             seed=1234)
+    return model, tower, trainer
+
+
+def synthetic_batch(B, seed, dev):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(0, 50256, (B, 50), generator=g)
+    mask = torch.zeros((B, 50), dtype=torch.int64)
+    ids[:, 13:] = 50256
+    mask[:, :14] = 1
+    labels = ids.clone()
+    labels[mask == 0] = -100
+    px = torch.randn((B, 3, 224, 224), generator=g)
+    return ids.to(dev), mask.to(dev), labels.to(dev), px.to(dev)
+
+
+def cpu_baseline(seconds_budget: float = 20.0):
+    """Oracle (torch-CPU restatement of src/train.py's step incl. CLIP fwd, dropout on) on a bounded sample."""
+    from oracle import icap_oracle as O
+
+    cores = min(len(os.sched_getaffinity(0)), 16)
+    torch.set_num_threads(cores)
+    B = 8
+    gsd, msd = O.gpt2_state_dict(O.GPT2Cfg(), 0), O.mapper_state_dict(O.MapperCfg(), 0)
+    csd = O.clip_vision_state_dict(O.ClipCfg(), 0)
+    ids, mask, labels, _ = O.synthetic_batch(B, 50, 13, seed=1)
+    px = torch.randn((B, 3, 224, 224), generator=torch.Generator().manual_seed(2))
+    batch = (ids, mask, labels, px)
+    O.train_steps(gsd, O.GPT2Cfg(), msd, O.MapperCfg(), [batch], total_steps=100, p_drop=0.1,
+                  clip=(csd, O.ClipCfg()))  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.train_steps(gsd, O.GPT2Cfg(), msd, O.MapperCfg(), [batch], total_steps=100, p_drop=0.1,
+                      clip=(csd, O.ClipCfg()))
+        n += 1
+        el = time.perf_counter() - t0
+        if el > seconds_budget or n >= 20:
+            break
+    return {"value": round(n * B / el, 3), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": f"{n} oracle train steps x batch {B} (CLIP-B/32 fwd on 224^2 pixels + mapper + GPT-2 small "
+                      f"fwd/bwd + AdamW, dropout 0.1, fp32, torch CPU {cores} threads) in {el:.1f}s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--decode-batch", type=int, default=128)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    B = args.batch
+
+    model, tower, trainer = build(B, dev)
+    ids, mask, labels, px = synthetic_batch(B, 1 + rank, dev)  # each rank: its own shard of samples
+    trainer.load_batch(ids, mask, labels, pixels=px)
+    use_graph = not args.no_graph
+    for _ in range(max(args.warmup, 1)):
+        trainer.micro_step(use_graph=use_graph)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.micro_step(use_graph=use_graph)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    loss = float(trainer.last_loss.item())
+    imgs_per_s = world * B * args.steps / el
+
+    # -- kernel roofline pass: every GEMM launch of one eager step, timed with HIP events ----------------------
+    from icap import ops
+
+    timer = GemmTimer()
+    ops.GEMM_TIMER = timer
+    torch.cuda.synchronize()
+    te0 = time.perf_counter()
+    trainer._fwd_bwd(True, trainer.grad_scale())
+    trainer._optimizer()
+    torch.cuda.synchronize()
+    eager_ms = (time.perf_counter() - te0) * 1e3
+    ops.GEMM_TIMER = None
+    agg = timer.summary(os.environ.get("ICAP_GEMM_DETAIL"))
+    gemm_ms = sum(v[2] for v in agg.values())
+    dom = max(agg, key=lambda k: agg[k][2])
+    n_l, fl, ms = agg[dom]
+    achieved = fl / (ms * 1e-3) / 1e12
+    all_fl = sum(v[1] for v in agg.values())
+
+    # -- greedy decode throughput ------------------------------------------------------------------------------
+    Bd = args.decode_batch
+    g = torch.Generator().manual_seed(5)
+    emb = torch.randn((Bd, 512), generator=g)
+    emb = (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
+    # one caption = 50 greedy tokens after the 15-token prefix: decode all 50 steps (the trained
+    # synthetic model emits EOS early; the reference loop would stop there), output identical either way
+    model.generate(emb, max_length=50, temperature=0.0, early_exit=False)  # warm-up
+    torch.cuda.synchronize()
+    td0 = time.perf_counter()
+    nd = 3
+    lens = []
+    for _ in range(nd):
+        out = model.generate(emb, max_length=50, temperature=0.0, early_exit=False)
+        lens.append(out.shape[1])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - td0
+    caps_per_s = world * Bd * nd / dt
+
+    if rank == 0:
+        res = {
+            "metric": METRIC, "value": round(imgs_per_s, 2), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (seeded COCO-shaped captions: 13 tokens + EOS, padded to 50; randn 224x224 pixels); "
+                    "deterministic random-init weights",
+            "config": {"workload": "train step: CLIP ViT-B/32 fwd (frozen) on 224x224 pixels -> transformer mapper "
+                                   "(8 layers, prefix 15, trained) -> GPT-2 small (frozen) fwd + dX bwd, LM head on "
+                                   "all 65 positions + CE, dropout 0.1, clip_grad_norm 1.0 + AdamW + linear LR",
+                       "per_gpu_batch": B, "global_batch": B * world, "seq_len": 65, "caption_len": 50,
+                       "parallelism": f"dp{world}", "graph": use_graph},
+            "final_loss": round(loss, 4),
+            "greedy_captions_per_s": round(caps_per_s, 1),
+            "greedy": {"batch_per_gpu": Bd, "decode_steps": 50, "returned_len": lens[-1], "kv_cache": True,
+                       "ms_per_batch": round(dt / nd * 1e3, 3)},
+            "roofline": {"bound": "mfma", "kernel": f"icap::gemm_kernel ({dom})", "achieved": round(achieved, 1),
+                         "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+                         "traffic": None, "launches_per_step": n_l,
+                         "avg_launch_us": round(ms / n_l * 1e3, 2),
+                         "alg_gflop_per_launch": round(fl / n_l / 1e9, 3),
+                         "all_gemm_ms_per_step": round(gemm_ms, 3), "all_gemm_tflop_per_step": round(all_fl / 1e12, 4),
+                         "eager_step_ms": round(eager_ms, 3),
+                         "timing": "HIP events around every GEMM launch of one eager step on its launch stream "
+                                   "(the timed region replays a HIP graph, which cannot host per-kernel events)"},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(res), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -13,7 +13,14 @@
 // index XOR-swizzled by (row & 7) so the ds_read_b128 fragment reads and the
 // ds_write_b128 staging writes are bank-conflict free
 // (cdna_hip_programming.md §5.5 T2). Global->LDS goes through registers
-// (loads for stage k+1 are issued before the MFMAs of stage k: T14).
+// (loads for stage k+1 are issued before the MFMAs of stage k: T14) with
+// buffer loads whose hardware range check zero-fills out-of-range rows and
+// K-tail chunks, so the main loop has no per-load branches (§5 trap (c)).
+//
+// Epilogue: each wave stages its 64x64 fp32 accumulators through LDS (two
+// 32-row halves) and re-reads them 4 consecutive columns per lane, so bias /
+// activation / dropout / residual / aux / beta are applied on coalesced 8- or
+// 16-byte vectors (16 lanes cover one 64-column row segment).
 //
 // bf16: v_mfma_f32_16x16x32_bf16 — lane l supplies row (l&15), k = 8(l>>4)..+7.
 // f32 (parity mode): v_mfma_f32_16x16x4_f32 (exact fp32 FMA chain) — one
@@ -30,6 +37,8 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int GBM = 128, GBN = 128, GROWB = 128, GNT = 256;
 constexpr int STAGE_BYTES = (GBM + GBN) * GROWB;  // 32 KiB
+constexpr int EPI_LD = 68;                         // fp32 row stride of the epilogue staging tile
+constexpr uint32_t OOB = 0x80000000u;              // buffer offset beyond any num_records -> loads 0
 
 __device__ __forceinline__ int lds_off(int row, int chunk) {
   return row * GROWB + ((chunk ^ (row & 7)) << 4);
@@ -51,6 +60,25 @@ __device__ __forceinline__ void mfma_chunk<float>(f32x4_t& acc, const uint4& a, 
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
 }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
+  const uint32_t n = bytes > 0x7fffffffull ? 0x7fffffffu : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
+}
+
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+template <typename T> struct vec4io;
+template <> struct vec4io<float> {
+  static __device__ __forceinline__ void ld(const float* p, float v[4]) { io<float>::ld4(p, v); }
+  static __device__ __forceinline__ void st(float* p, const float v[4]) { io<float>::st4(p, v); }
+};
+template <> struct vec4io<bf16_t> {
+  static __device__ __forceinline__ void ld(const bf16_t* p, float v[4]) { io<bf16_t>::ld4(p, v); }
+  static __device__ __forceinline__ void st(bf16_t* p, const float v[4]) { io<bf16_t>::st4(p, v); }
+};
 
 template <typename TI, typename TC>
 __global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tiles_n, uint32_t drop_thresh,
@@ -74,22 +102,33 @@ __global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tile
   const int64_t m0 = (int64_t)tm * GBM, n0 = (int64_t)tn * GBN;
 
   const int64_t M = p.M, N = p.N, K = p.K;
-  const char* Ag = reinterpret_cast<const char*>(p.A);
-  const char* Bg = reinterpret_cast<const char*>(p.B);
+  // tile-relative buffer descriptors: rows past M / N fall beyond num_records and load zeros
+  const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
+  const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
+  const int64_t mrows = M - m0 < GBM ? M - m0 : GBM;
+  const int64_t nrows = N - n0 < GBN ? N - n0 : GBN;
+  const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
+  const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
+  // per-thread staging coordinates (4 chunks of A and 4 of B per stage)
+  uint32_t a_off[4], b_off[4];
+  int kchunk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + i * GNT;
+    const int row = c >> 3;
+    kchunk[i] = (c & 7) * EPC;
+    a_off[i] = (uint32_t)((row * p.lda + kchunk[i]) * ES);
+    b_off[i] = (uint32_t)((row * p.ldb + kchunk[i]) * ES);
+  }
 
-  // staging: each thread moves 4 chunks of A and 4 of B per stage
   uint4 ra[4], rb[4];
   auto load_stage = [&](int64_t k0) {
+    const uint32_t kb = (uint32_t)(k0 * ES);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = tid + i * GNT;
-      const int row = c >> 3, kc = c & 7;
-      const int64_t gk = k0 + kc * EPC;
-      const int64_t gm = m0 + row, gn = n0 + row;
-      uint4 za = make_uint4(0, 0, 0, 0), zb = za;
-      if (gm < M && gk < K) za = *reinterpret_cast<const uint4*>(Ag + (gm * p.lda + gk) * ES);
-      if (gn < N && gk < K) zb = *reinterpret_cast<const uint4*>(Bg + (gn * p.ldb + gk) * ES);
-      ra[i] = za; rb[i] = zb;
+      const bool kin = k0 + kchunk[i] < K;
+      ra[i] = bload(ra_rsrc, kin ? a_off[i] + kb : OOB);
+      rb[i] = bload(rb_rsrc, kin ? b_off[i] + kb : OOB);
     }
   };
   auto store_stage = [&](int s) {
@@ -126,15 +165,9 @@ __global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tile
       const int ch = ks * 4 + fg;
       uint4 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * 64 + i * 16 + fr;
-        af[i] = *reinterpret_cast<const uint4*>(As + lds_off(row, ch));
-      }
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const uint4*>(As + lds_off(wm * 64 + i * 16 + fr, ch));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wn * 64 + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const uint4*>(Bs + lds_off(row, ch));
-      }
+      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const uint4*>(Bs + lds_off(wn * 64 + j * 16 + fr, ch));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -144,45 +177,92 @@ __global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tile
     __syncthreads();
   }
 
-  // ---- epilogue ----
+  // ---- epilogue (LDS-staged, 4 columns per lane) ----
   TC* C = reinterpret_cast<TC*>(p.C);
   TC* aux = reinterpret_cast<TC*>(p.aux);
   const TC* resid = reinterpret_cast<const TC*>(p.resid);
   const TC* dsrc = reinterpret_cast<const TC*>(p.dact_src);
   const bool use_drop = drop_thresh != 0u;
   const uint64_t seed = use_drop ? eff_seed(p.seed, p.seed_ptr) : 0ull;
+  float* cs = reinterpret_cast<float*>(smem) + wave * (32 * EPI_LD);
+  const int er = lane >> 4;         // row within a 4-row group
+  const int ec = (lane & 15) * 4;   // first of this lane's 4 columns in the 64-column wave tile
+  const int64_t col = n0 + wn * 64 + ec;
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias && p.dact == ICAP_ACT_NONE) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t col = n0 + wn * 64 + j * 16 + fr;
-    if (col >= N) continue;
-    const float bcol = p.bias ? p.bias[col] : 0.f;
+    for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
+  }
+  const bool full4 = (col + 4 <= N) && ((p.ldc & 3) == 0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+  for (int h = 0; h < 2; ++h) {
+    // stage rows [32h, 32h+32) of this wave's 64x64 accumulator tile
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int64_t row = m0 + wm * 64 + i * 16 + fg * 4 + v;
-        if (row >= M) continue;
-        float x = p.alpha * acc[i][j][v];
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) cs[(ii * 16 + fg * 4 + v) * EPI_LD + j * 16 + fr] = acc[2 * h + ii][j][v];
+    __syncthreads();
+#pragma unroll 2
+    for (int t = 0; t < 8; ++t) {
+      const int lr = t * 4 + er;  // 0..31
+      const int64_t row = m0 + wm * 64 + h * 32 + lr;
+      float x[4];
+      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * EPI_LD + ec);
+      if (row < M) {
+        const uint64_t didx = p.offset + (uint64_t)(row * N + col);
+        float a4[4], r4[4], c4[4];
         if (p.dact != ICAP_ACT_NONE) {
-          if (use_drop) x *= drop_scale(seed, p.offset + (uint64_t)(row * N + col), drop_thresh, inv_keep);
-          x *= act_bwd(p.dact, io<TC>::ld(dsrc + row * p.ld_dact + col));
-        } else {
-          x += bcol;
-          if (p.act != ICAP_ACT_NONE) {
-            const float y = act_fwd(p.act, x);
-            if (aux) io<TC>::st(aux + row * p.ldaux + col, p.act == ICAP_ACT_TANH ? y : x);
-            x = y;
-          } else if (aux) {
-            io<TC>::st(aux + row * p.ldaux + col, x);
+          if (full4 && (p.ld_dact & 3) == 0) vec4io<TC>::ld(dsrc + row * p.ld_dact + col, a4);
+          else for (int e = 0; e < 4; ++e) a4[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float y = p.alpha * x[e];
+            if (use_drop) y *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
+            x[e] = y * act_bwd(p.dact, a4[e]);
           }
-          if (use_drop) x *= drop_scale(seed, p.offset + (uint64_t)(row * N + col), drop_thresh, inv_keep);
-          if (resid) x += io<TC>::ld(resid + row * p.ldr + col);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = p.alpha * x[e] + bias4[e];
+          if (p.act != ICAP_ACT_NONE || aux) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float y = act_fwd(p.act, x[e]);
+              a4[e] = (p.act == ICAP_ACT_TANH) ? y : x[e];
+              x[e] = y;
+            }
+            if (aux) {
+              if (full4 && (p.ldaux & 3) == 0) vec4io<TC>::st(aux + row * p.ldaux + col, a4);
+              else for (int e = 0; e < 4; ++e) if (col + e < N) io<TC>::st(aux + row * p.ldaux + col + e, a4[e]);
+            }
+          }
+          if (use_drop) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
+          }
+          if (resid) {
+            if (full4 && (p.ldr & 3) == 0) vec4io<TC>::ld(resid + row * p.ldr + col, r4);
+            else for (int e = 0; e < 4; ++e) r4[e] = (col + e < N) ? io<TC>::ld(resid + row * p.ldr + col + e) : 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] += r4[e];
+          }
         }
         TC* cp = C + row * p.ldc + col;
-        if (p.beta != 0.f) x += p.beta * io<TC>::ld(cp);
-        io<TC>::st(cp, x);
+        if (full4) {
+          if (p.beta != 0.f) {
+            vec4io<TC>::ld(cp, c4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] += p.beta * c4[e];
+          }
+          vec4io<TC>::st(cp, x);
+        } else {
+          for (int e = 0; e < 4; ++e)
+            if (col + e < N) io<TC>::st(cp + e, p.beta != 0.f ? x[e] + p.beta * io<TC>::ld(cp + e) : x[e]);
+        }
       }
     }
+    __syncthreads();
   }
 }
 
@@ -204,6 +284,9 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   ICAP_REQUIRE(p.lda >= p.K && p.ldb >= p.K && p.ldc >= p.N, "icap_gemm: leading dimension too small");
   ICAP_REQUIRE((reinterpret_cast<uintptr_t>(p.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.B) & 15) == 0,
                "icap_gemm: A and B must be 16-byte aligned");
+  const int es = p.in_dtype == ICAP_BF16 ? 2 : 4;
+  ICAP_REQUIRE((int64_t)GBM * p.lda * es < 0x7fffffffll && (int64_t)GBN * p.ldb * es < 0x7fffffffll,
+               "icap_gemm: a 128-row operand panel must stay below 2 GiB");
   ICAP_REQUIRE(p.beta == 0.f || p.c_dtype == ICAP_F32, "icap_gemm: beta != 0 requires f32 C");
   ICAP_REQUIRE(p.dact == ICAP_ACT_NONE || p.dact_src != nullptr, "icap_gemm: dact requires dact_src");
   ICAP_REQUIRE(p.drop_p >= 0.f && p.drop_p < 1.f, "icap_gemm: drop_p out of range");

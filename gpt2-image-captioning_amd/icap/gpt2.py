@@ -340,7 +340,7 @@ class GPT2Core:
         ops.gpt2_embed(prefix, prefix_bstride, self.wte, self.wpe, ids, ws.x[0], B=B, P=P, L_=Lc, D=D, drop=dr.embd)
         self._blocks_fwd(ws, dr, B, S, M, causal_mask=ws.key_mask if mask is not None else None)
         ops.layernorm_fwd(ws.x[-1], self.lnf_g, self.lnf_b, self.eps, ws.hf, ws.meanf, ws.rstdf)
-        ops.gemm(ws.hf, self.wte, ws.logits)
+        ops.gemm(ws.hf, self.wte, ws.logits, alg_flops=2.0 * ws.M * self.V * self.D)
         if labels is not None:
             dl = (dlogits if dlogits is not None else ws.logits) if fuse_dlogits else None
             ops.cross_entropy(ws.logits, self.V, ws.labels_shift, ws.n_valid, ws.loss, dl, ws.ce_ws, grad_scale)
@@ -367,7 +367,7 @@ class GPT2Core:
         D, H, hd = self.D, self.H, self.hd
         scale = 1.0 / math.sqrt(hd)
         nl = len(self.layers)
-        ops.gemm(dlogits, self.wte_t, ws.dhf)  # dh_f = dlogits . wte  (K = padded vocab)
+        ops.gemm(dlogits, self.wte_t, ws.dhf, alg_flops=2.0 * M * D * self.V)  # dh_f = dlogits . wte (K padded)
         if grads is not None:  # d(wte) from the tied LM head: dW[V,D] += dlogits^T . hf
             dw.dW(dlogits, ws.hf, grads.wte, M=M, N=self.V)
         ops.layernorm_bwd(ws.x[-1], self.lnf_g, ws.meanf, ws.rstdf, ws.dhf, ws.dx, dx_drop=ws.dxd,
@@ -428,7 +428,7 @@ class GPT2Core:
         ops.gpt2_embed(x_in, S * D, self.wte, self.wpe, None, ws.x[0], B=B, P=S, L_=0, D=D, drop=dr.embd)
         self._blocks_fwd(ws, dr, B, S, ws.M, causal_mask=ws.key_mask if mask is not None else None)
         ops.layernorm_fwd(ws.x[-1], self.lnf_g, self.lnf_b, self.eps, ws.hf, ws.meanf, ws.rstdf)
-        ops.gemm(ws.hf, self.wte, ws.logits)
+        ops.gemm(ws.hf, self.wte, ws.logits, alg_flops=2.0 * ws.M * self.V * self.D)
         loss = None
         if lab is not None:
             ops.cross_entropy(ws.logits, self.V, ws.labels_shift, ws.n_valid, ws.loss, None, ws.ce_ws)
@@ -478,14 +478,14 @@ class GPT2Core:
         B = ds.B
         a = ds.a[:B]
         ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
-        ops.gemm(a, self.wte, ds.logits, M=B)
+        ops.gemm(a, self.wte, ds.logits, M=B, alg_flops=2.0 * B * self.V * self.D)
         nxt_x = ds.x[:B] if pos_next < ds.T else None
         ops.greedy_next(ds.logits, self.V, self.cfg.eos_token_id, ds.finished, ds.tokens, step,
                         self.wte if nxt_x is not None else None, self.wpe if nxt_x is not None else None,
                         min(pos_next, self.cfg.n_positions - 1), D, nxt_x)
 
     @torch.no_grad()
-    def greedy_decode(self, prefix: Tensor, max_length: int, check_every: int = 8) -> Tensor:
+    def greedy_decode(self, prefix: Tensor, max_length: int, check_every: int = 8, early_exit: bool = True) -> Tensor:
         """prefix [B,P,D] (compute dtype) -> token ids [B, <=max_length] with the reference's EOS latch and
         early exit (src/models.py:389-391,453-460). Exact to the reference's full-recompute loop: causal
         attention makes cached keys/values of earlier positions identical to recomputed ones."""
@@ -499,7 +499,7 @@ class GPT2Core:
         self._decode_head(ds, ds.x[(P - 1) * B: P * B], 0, P)
         steps = 1
         for s in range(1, max_length):
-            if s % check_every == 0 and bool(ds.finished.bool().all()):
+            if early_exit and s % check_every == 0 and bool(ds.finished.bool().all()):
                 break
             pos = P + s - 1
             self._decode_block(ds, B, ds.x[:B], pos, 1, prefill=False)
@@ -539,7 +539,7 @@ class GPT2Core:
                 x_last = ds.x[:B]
             a = ds.a[:B]
             ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
-            ops.gemm(a, self.wte, ds.logits, M=B)
+            ops.gemm(a, self.wte, ds.logits, M=B, alg_flops=2.0 * B * self.V * self.D)
             logits = ds.logits[:, : self.V].float() / temperature
             fin = ds.finished.bool()
             if top_p < 1.0:

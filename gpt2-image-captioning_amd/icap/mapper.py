@@ -58,9 +58,9 @@ class DWHelper:
         a = self._t(self.tA, dY, M, N, Mp)  # [N][Mp]
         b = self._t(self.tB, X, M, K, Mp)   # [K][Mp]
         if transpose_out:  # out[K,N] (HF Conv1D grad layout)
-            ops.gemm(b, a, out, beta=1.0, M=K, N=N, K=Mp)
+            ops.gemm(b, a, out, beta=1.0, M=K, N=N, K=Mp, alg_flops=2.0 * M * N * K)
         else:              # out[N,K] (nn.Linear grad layout)
-            ops.gemm(a, b, out, beta=1.0, M=N, N=K, K=Mp)
+            ops.gemm(a, b, out, beta=1.0, M=N, N=K, K=Mp, alg_flops=2.0 * M * N * K)
 
     def db(self, dY: Tensor, out: Tensor, M: int, N: Optional[int] = None) -> None:
         ops.colsum(dY, out, self.cs_ws, accumulate=True, M=M, N=N)

@@ -205,8 +205,9 @@ class ImageCaptioningModel(nn.Module):
     # -- decode -------------------------------------------------------------------------------------------------
     @torch.no_grad()
     def generate(self, image_embeddings: Tensor, max_length: int = 50, temperature: float = 1.0,
-                 top_p: float = 0.9) -> Tensor:
-        """src/models.py:327-477: greedy (temperature == 0) or top-p sampling, KV-cached."""
+                 top_p: float = 0.9, early_exit: bool = True) -> Tensor:
+        """src/models.py:327-477: greedy (temperature == 0) or top-p sampling, KV-cached. early_exit=False keeps
+        decoding all max_length steps on the device (output identical; used to time fixed-length captions)."""
         self.eval()
         self.sync_compute_copies()
         B = image_embeddings.shape[0]
@@ -218,7 +219,7 @@ class ImageCaptioningModel(nn.Module):
         P, D = self.total_prefix_length, self.gpt_embedding_size
         prefix = pre.as_strided((B, P, D), (pbs, D, 1))
         if temperature == 0:
-            return gc.greedy_decode(prefix, max_length)
+            return gc.greedy_decode(prefix, max_length, early_exit=early_exit)
         return gc.sample_decode(prefix, max_length, temperature, top_p)
 
     def generate_captions(self, image_embeddings: Tensor, **kwargs) -> List[str]:

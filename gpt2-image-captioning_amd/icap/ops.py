@@ -68,8 +68,10 @@ NO_DROP = Dropout()
 def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, act: int = L.ACT_NONE,
          aux: Optional[Tensor] = None, dact: int = L.ACT_NONE, dact_src: Optional[Tensor] = None,
          resid: Optional[Tensor] = None, alpha: float = 1.0, beta: float = 0.0, drop: Dropout = NO_DROP,
-         M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None) -> Tensor:
-    """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h."""
+         M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None,
+         alg_flops: Optional[float] = None) -> Tensor:
+    """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
+    alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64)."""
     M = A.shape[0] if M is None else M
     K = A.shape[1] if K is None else K
     N = B.shape[0] if N is None else N
@@ -93,8 +95,18 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     if resid is not None:
         a.resid, a.ldr = resid.data_ptr(), _ld(resid)
     a.drop_p, a.seed, a.offset, a.seed_ptr = drop.p, drop.seed, drop.offset, drop.ptr
-    call("icap_gemm", C.byref(a), _stream())
+    if GEMM_TIMER is None:
+        call("icap_gemm", C.byref(a), _stream())
+    else:  # per-launch HIP-event timing (bench.py kernel roofline pass; never inside a captured graph)
+        key = ("bf16" if a.in_dtype == L.BF16 else "f32") + "->" + ("bf16" if a.c_dtype == L.BF16 else "f32")
+        key = (key, f"{M}x{N}x{K} act{act} dact{dact} drop{int(drop.p > 0)} res{int(resid is not None)} "
+                    f"aux{int(aux is not None)} beta{beta:g}")
+        GEMM_TIMER.launch(key, 2.0 * M * N * K if alg_flops is None else alg_flops,
+                          lambda: call("icap_gemm", C.byref(a), _stream()))
     return out
+
+
+GEMM_TIMER = None  # set to an object with .launch(key, flops, fn) to time every GEMM launch
 
 
 def layernorm_fwd(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, y: Tensor, mean: Optional[Tensor],

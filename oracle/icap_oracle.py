@@ -450,16 +450,22 @@ def clip_and_adamw(params: Dict[str, Tensor], grads: Dict[str, Tensor], st: Adam
 
 
 def train_steps(gpt_sd, gcfg: GPT2Cfg, map_sd, mcfg: MapperCfg, batches, lr0: float = 1e-4, total_steps: int = 10,
-                warmup: int = 0, freeze_gpt: bool = True):
-    """The inner loop of src/train.py:119-166 with grad_accum_steps=1 and dropout off: forward, backward, clip,
-    AdamW, schedule. Returns (losses, grad_norms, map_sd, gpt_sd) after len(batches) steps."""
+                warmup: int = 0, freeze_gpt: bool = True, p_drop: float = 0.0, clip=None):
+    """The inner loop of src/train.py:119-166 with grad_accum_steps=1: forward, backward, clip, AdamW, schedule.
+    p_drop > 0 runs the reference's train-mode dropout (GPT-2 embd/attn/resid, mapper; nondeterministic).
+    clip=(clip_sd, ClipCfg): each batch's 4th element is pixels, embedded by the CLIP tower first (frozen,
+    src/embeddings/clip.py:132-137). Returns (losses, grad_norms, map_sd, gpt_sd) after len(batches) steps."""
     map_sd = {k: v.clone().requires_grad_(True) for k, v in map_sd.items()}
     gpt_sd = {k: v.clone().requires_grad_(not freeze_gpt) for k, v in gpt_sd.items()}
     st = AdamWState()
     losses, norms = [], []
+    train = p_drop > 0
     for ids, mask, labels, emb in batches:
-        prefix = mapper_forward(map_sd, mcfg, emb)
-        loss, _ = caption_forward(gpt_sd, gcfg, prefix, ids, mask, labels)
+        if clip is not None:
+            with torch.no_grad():
+                emb = clip_embed_normalized(clip[0], clip[1], emb)
+        prefix = mapper_forward(map_sd, mcfg, emb, train, p_drop)
+        loss, _ = caption_forward(gpt_sd, gcfg, prefix, ids, mask, labels, train, p_drop)
         trainable = dict(map_sd)
         if not freeze_gpt:
             trainable.update({"gpt." + k: v for k, v in gpt_sd.items()})
