@@ -238,6 +238,18 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(int B, int H, int hd, i
   }
 }
 
+// bf16 MFMA kernels (attention_mfma.hip); the fp32 parity mode and shapes they do not cover use the
+// LDS/VALU kernels of this file. ICAP_ATTN_VALU=1 forces the VALU kernels (A/B testing).
+bool mfma_attention_ok(const icap_attn_args* a, bool bwd);
+int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float inv_keep, hipStream_t s);
+static bool force_valu() {
+  static const bool f = [] {
+    const char* e = getenv("ICAP_ATTN_VALU");
+    return e && e[0] == '1';
+  }();
+  return f;
+}
+
 static size_t fwd_lds(int S, int hd) { return sizeof(float) * ((size_t)3 * S * (hd + 1) + (size_t)S * S); }
 static size_t bwd_lds(int S, int hd) { return sizeof(float) * ((size_t)4 * S * (hd + 1) + (size_t)2 * S * S); }
 constexpr size_t LDS_CAP = 160 * 1024;
@@ -272,6 +284,7 @@ extern "C" int icap_attention_fwd(const icap_attn_args* a, void* stream) {
   const float inv_keep = a->drop_p > 0.f ? 1.f / (1.f - a->drop_p) : 1.f;
   const size_t lds = fwd_lds(a->S, a->hd);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!force_valu() && mfma_attention_ok(a, false)) return mfma_attention_launch(a, false, thr, inv_keep, s);
   dim3 grid((unsigned)(a->B * a->H)), block(256);
   if (a->dtype == ICAP_BF16) {
     static bool once = (raise_lds_limit(attn_fwd_kernel<bf16_t>), true); (void)once;
@@ -292,6 +305,7 @@ extern "C" int icap_attention_bwd(const icap_attn_args* a, void* stream) {
   const float inv_keep = a->drop_p > 0.f ? 1.f / (1.f - a->drop_p) : 1.f;
   const size_t lds = bwd_lds(a->S, a->hd);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!force_valu() && mfma_attention_ok(a, true)) return mfma_attention_launch(a, true, thr, inv_keep, s);
   dim3 grid((unsigned)(a->B * a->H)), block(256);
   if (a->dtype == ICAP_BF16) {
     static bool once = (raise_lds_limit(attn_bwd_kernel<bf16_t>), true); (void)once;

@@ -160,17 +160,23 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t rows, int D, const 
   }
 }
 
-__global__ void ln_param_reduce(int nblk, int D, const float* __restrict__ partial, float* dgamma,
-                                float* dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float a = 0.f, b = 0.f;
-  for (int i = 0; i < nblk; ++i) {
-    a += partial[(int64_t)i * 2 * D + c];
-    b += partial[(int64_t)i * 2 * D + D + c];
+// grid (ceil(D/64), 2): blockIdx.y selects dgamma / dbeta; 4 waves split the partial rows, 64 lanes = 64 columns
+__global__ __launch_bounds__(256) void ln_param_reduce(int nblk, int D, const float* __restrict__ partial,
+                                                      float* dgamma, float* dbeta) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int which = blockIdx.y;
+  float a = 0.f;
+  if (c < D)
+    for (int i = ty; i < nblk; i += 4) a += partial[(int64_t)i * 2 * D + which * D + c];
+  red[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && c < D) {
+    const float s = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+    float* dst = which ? dbeta : dgamma;
+    if (dst) dst[c] += s;
   }
-  if (dgamma) dgamma[c] += a;
-  if (dbeta) dbeta[c] += b;
 }
 
 }  // namespace icap
@@ -234,7 +240,7 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
                        lddx, (float*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial);
   int rc = check_launch("icap_layernorm_bwd");
   if (rc != ICAP_OK || !want_params) return rc;
-  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, s, nb, (int)D, partial,
+  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 63) / 64), 2), dim3(256), 0, s, nb, (int)D, partial,
                      dgamma, dbeta);
   return check_launch("icap_layernorm_bwd(reduce)");
 }
