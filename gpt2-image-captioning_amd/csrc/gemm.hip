@@ -109,37 +109,32 @@ __global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tile
   const int64_t nrows = N - n0 < GBN ? N - n0 : GBN;
   const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
   const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
-  // per-thread staging coordinates (4 chunks of A and 4 of B per stage)
+  // LDS-DMA staging (buffer_load_dwordx4 ... lds): one wave-instruction writes 1 KiB = 8 LDS rows of
+  // 128 B linearly (lane l -> row l>>3, physical chunk l&7). The XOR swizzle therefore goes on the SOURCE:
+  // physical chunk pc of row r holds logical K-chunk pc ^ (r & 7) (cdna_hip_programming.md §5.4 rule 21).
+  // Wave w stages rows [32w, 32w+32) of A and of B: 4 + 4 instructions per stage, no VGPR round trip.
+  const int lrow = lane >> 3;
+  const int lchunk = ((lane & 7) ^ lrow) * EPC;  // logical K offset (elements) of this lane's 16 B
   uint32_t a_off[4], b_off[4];
-  int kchunk[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int c = tid + i * GNT;
-    const int row = c >> 3;
-    kchunk[i] = (c & 7) * EPC;
-    a_off[i] = (uint32_t)((row * p.lda + kchunk[i]) * ES);
-    b_off[i] = (uint32_t)((row * p.ldb + kchunk[i]) * ES);
+    const int row = wave * 32 + i * 8 + lrow;
+    a_off[i] = (uint32_t)((row * p.lda + lchunk) * ES);
+    b_off[i] = (uint32_t)((row * p.ldb + lchunk) * ES);
   }
-
-  uint4 ra[4], rb[4];
-  auto load_stage = [&](int64_t k0) {
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  auto load_stage = [&](int64_t k0, int s) {
     const uint32_t kb = (uint32_t)(k0 * ES);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bool kin = k0 + kchunk[i] < K;
-      ra[i] = bload(ra_rsrc, kin ? a_off[i] + kb : OOB);
-      rb[i] = bload(rb_rsrc, kin ? b_off[i] + kb : OOB);
-    }
-  };
-  auto store_stage = [&](int s) {
+    const bool kin = k0 + lchunk < K;
     char* As = smem + s * STAGE_BYTES;
     char* Bs = As + GBM * GROWB;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int c = tid + i * GNT;
-      const int row = c >> 3, kc = c & 7;
-      *reinterpret_cast<uint4*>(As + lds_off(row, kc)) = ra[i];
-      *reinterpret_cast<uint4*>(Bs + lds_off(row, kc)) = rb[i];
+      const int r0 = wave * 32 + i * 8;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_rsrc, (lds_ptr_t)(As + r0 * GROWB), 16, kin ? a_off[i] + kb : OOB,
+                                               0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb_rsrc, (lds_ptr_t)(Bs + r0 * GROWB), 16, kin ? b_off[i] + kb : OOB,
+                                               0, 0, 0);
     }
   };
 
@@ -150,31 +145,39 @@ __global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tile
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   const int nk = (int)((K + BKE - 1) / BKE);
-  load_stage(0);
-  store_stage(0);
+  load_stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int fr = lane & 15, fg = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_stage((int64_t)(kt + 1) * BKE);
     const char* As = smem + cur * STAGE_BYTES;
     const char* Bs = As + GBM * GROWB;
+    // all fragment reads of this stage first: hipcc waits vmcnt(0) before any LDS read that follows an
+    // LDS-DMA issue, so the next stage's DMA is issued only after the reads (and overlaps the MFMAs)
+    uint4 af[2][4], bfr[2][4];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + fg;
-      uint4 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const uint4*>(As + lds_off(wm * 64 + i * 16 + fr, ch));
+      for (int i = 0; i < 4; ++i) af[ks][i] = *reinterpret_cast<const uint4*>(As + lds_off(wm * 64 + i * 16 + fr, ch));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const uint4*>(Bs + lds_off(wn * 64 + j * 16 + fr, ch));
+      for (int j = 0; j < 4; ++j) bfr[ks][j] = *reinterpret_cast<const uint4*>(Bs + lds_off(wn * 64 + j * 16 + fr, ch));
+    }
+    // the other buffer was last read in iteration kt-1, which every wave finished before the barrier below
+    if (kt + 1 < nk) load_stage((int64_t)(kt + 1) * BKE, cur ^ 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mfma_chunk<TI>(acc[i][j], af[i], bfr[j]);
-    }
-    if (kt + 1 < nk) store_stage(cur ^ 1);
-    __syncthreads();
+        for (int j = 0; j < 4; ++j) mfma_chunk<TI>(acc[i][j], af[ks][i], bfr[ks][j]);
+    // keep the MFMAs above the wait: they are register-only, so without this fence hipcc sinks them below the
+    // vmcnt/barrier and the DMA is waited for right after it is issued (cdna_hip_programming.md §5.4 rule 18)
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage kt+1 has landed
+    __syncthreads();                                      // ... and every other wave's
   }
 
   // ---- epilogue (LDS-staged, 4 columns per lane) ----

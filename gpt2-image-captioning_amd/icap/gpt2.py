@@ -492,6 +492,8 @@ class GPT2Core:
         B, P, D = prefix.shape
         if max_length <= 0:
             return torch.empty((B, 0), dtype=torch.long, device=prefix.device)
+        if prefix.is_cuda and self.graph_decode:
+            return self._runner(B, P, max_length).run(prefix, early_exit, check_every)
         ds = self.alloc_decode(B, P, max_length)
         pre = prefix if (prefix.dtype == self.dtype and prefix.stride(-1) == 1) else prefix.to(self.dtype).contiguous()
         ops.add_position(pre, pre.stride(0), pre.stride(1), self.wpe, ds.x, B=B, npos=P, D=D, pos0=0)
@@ -508,6 +510,18 @@ class GPT2Core:
         toks = ds.tokens[:, :steps]
         # reference loop length: stops before the first step at which every row had already finished
         return self._truncate(toks, steps)
+
+    graph_decode = True  # replay captured HIP graphs of the decode chunks (per batch shape)
+
+    def _runner(self, B: int, P: int, max_length: int) -> "DecodeRunner":
+        if not hasattr(self, "_runners"):
+            self._runners = {}
+        key = (B, P, max_length)
+        if key not in self._runners:
+            if len(self._runners) >= 2:
+                self._runners.pop(next(iter(self._runners)))
+            self._runners[key] = DecodeRunner(self, B, P, max_length)
+        return self._runners[key]
 
     def _truncate(self, toks: Tensor, steps: int) -> Tensor:
         B = toks.shape[0]
@@ -558,3 +572,57 @@ class GPT2Core:
                             min(pos_next, self.cfg.n_positions - 1), D, nxt_x, forced=nxt)
             steps = s + 1
         return self._truncate(ds.tokens[:, :steps], steps)
+
+
+class DecodeRunner:
+    """Greedy decode of one batch shape as HIP-graph chunks: chunk 0 = prefill + token 0 (+ state reset),
+    chunk c = tokens [c*C, (c+1)*C). Between chunks the host reads the EOS latch once (early exit,
+    src/models.py:390-391); the returned ids are truncated to the reference loop's length either way."""
+
+    def __init__(self, core: GPT2Core, B: int, P: int, max_length: int, chunk: int = 8):
+        self.core, self.B, self.P, self.T = core, B, P, max_length
+        self.chunk = chunk
+        self.ds = core.alloc_decode(B, P, max_length)
+        self.prefix = torch.zeros((B, P, core.D), dtype=core.dtype, device=core.dev)
+        self.bounds = [(0, min(chunk, max_length))]
+        s = chunk
+        while s < max_length:
+            self.bounds.append((s, min(s + chunk, max_length)))
+            s += chunk
+        self.graphs = None
+
+    def _chunk(self, c: int) -> None:
+        core, ds, B, P, D = self.core, self.ds, self.B, self.P, self.core.D
+        s0, s1 = self.bounds[c]
+        if c == 0:
+            ds.finished.zero_()
+            ds.tokens.fill_(core.cfg.eos_token_id)
+            ops.add_position(self.prefix, P * D, D, core.wpe, ds.x, B=B, npos=P, D=D, pos0=0)
+            core._decode_block(ds, P * B, ds.x, 0, P, prefill=True)
+            core._decode_head(ds, ds.x[(P - 1) * B: P * B], 0, P)
+            s0 = 1
+        for s in range(s0, s1):
+            pos = P + s - 1
+            core._decode_block(ds, B, ds.x[:B], pos, 1, prefill=False)
+            core._decode_head(ds, ds.x[:B], s, pos + 1)
+
+    @torch.no_grad()
+    def run(self, prefix: Tensor, early_exit: bool = True, check_every: int = 8) -> Tensor:
+        self.prefix.copy_(prefix)
+        if self.graphs is None:
+            for c in range(len(self.bounds)):  # eager warm-up pass (initialises every kernel once)
+                self._chunk(c)
+            torch.cuda.synchronize(self.core.dev)
+            self.graphs = []
+            for c in range(len(self.bounds)):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._chunk(c)
+                self.graphs.append(g)
+        steps = 0
+        for c, g in enumerate(self.graphs):
+            g.replay()
+            steps = self.bounds[c][1]
+            if early_exit and c + 1 < len(self.graphs) and bool(self.ds.finished.bool().all()):
+                break
+        return self.core._truncate(self.ds.tokens[:, :steps], steps)
