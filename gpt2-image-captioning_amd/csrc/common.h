@@ -31,12 +31,13 @@ int check_launch(const char* what);
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }
-// round-to-nearest-even; NaN stays NaN (quiet bit forced)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+// round-to-nearest-even (gfx950 v_cvt_pk_bf16_f32); NaN stays NaN
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+// two floats -> packed bf16 pair (lo = a) in one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t f2bf2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
 }
 
 template <typename T> struct io;
@@ -61,10 +62,7 @@ template <> struct io<bf16_t> {
     v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
   }
   static __device__ __forceinline__ void st4(bf16_t* p, const float v[4]) {
-    uint2 t;
-    t.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    t.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    *reinterpret_cast<uint2*>(p) = t;
+    *reinterpret_cast<uint2*>(p) = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
   }
 };
 
@@ -109,8 +107,9 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
   switch (act) {
     case ICAP_ACT_GELU_NEW: {
       // HF activations.py NewGELUActivation: 0.5x(1+tanh(sqrt(2/pi)(x+0.044715x^3)))
-      const float c = 0.7978845608028654f;
-      return 0.5f * x * (1.f + tanhf(c * (x + 0.044715f * x * x * x)));
+      // 0.5(1+tanh(u)) == sigmoid(2u): one v_exp + one v_rcp instead of a libm tanhf
+      const float c2 = 2.f * 0.7978845608028654f;
+      return x * __builtin_amdgcn_rcpf(1.f + __expf(-c2 * (x + 0.044715f * x * x * x)));
     }
     case ICAP_ACT_RELU: return x > 0.f ? x : 0.f;
     case ICAP_ACT_QUICK_GELU: return x / (1.f + __expf(-1.702f * x));
@@ -123,12 +122,12 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
 __device__ __forceinline__ float act_bwd(int act, float a) {
   switch (act) {
     case ICAP_ACT_GELU_NEW: {
+      // s = sigmoid(2u) = 0.5(1+tanh u);  d/da = s + a * 2s(1-s) * du/da
       const float c = 0.7978845608028654f;
-      float x2 = a * a;
-      float u = c * (a + 0.044715f * x2 * a);
-      float t = tanhf(u);
-      float du = c * (1.f + 3.f * 0.044715f * x2);
-      return 0.5f * (1.f + t) + 0.5f * a * (1.f - t * t) * du;
+      const float x2 = a * a;
+      const float s = __builtin_amdgcn_rcpf(1.f + __expf(-2.f * c * (a + 0.044715f * x2 * a)));
+      const float du = c * (1.f + 3.f * 0.044715f * x2);
+      return s + 2.f * a * s * (1.f - s) * du;
     }
     case ICAP_ACT_RELU: return a > 0.f ? 1.f : 0.f;
     case ICAP_ACT_QUICK_GELU: {

@@ -80,10 +80,84 @@ template <> struct vec4io<bf16_t> {
   static __device__ __forceinline__ void st(bf16_t* p, const float v[4]) { io<bf16_t>::st4(p, v); }
 };
 
-template <typename TI, typename TC>
-__global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tiles_n, uint32_t drop_thresh,
-                                                     float inv_keep) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+// Epilogue of 4 consecutive columns [col, col+4) of row `row` (the order is the one include/icap.h documents).
+// x: alpha-unscaled fp32 accumulators; bias4: bias[col..col+3] (0 past N); full4: all 4 columns in range and
+// C/aux/resid/dact_src leading dimensions allow 4-wide vector access (checked per operand).
+template <typename TC>
+__device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64_t col, float x[4],
+                                     const float bias4[4], bool full4, uint64_t seed, uint32_t drop_thresh,
+                                     float inv_keep) {
+  const int64_t N = p.N;
+  TC* C = reinterpret_cast<TC*>(p.C);
+  TC* aux = reinterpret_cast<TC*>(p.aux);
+  const TC* resid = reinterpret_cast<const TC*>(p.resid);
+  const TC* dsrc = reinterpret_cast<const TC*>(p.dact_src);
+  const bool use_drop = drop_thresh != 0u;
+  const uint64_t didx = p.offset + (uint64_t)(row * N + col);
+  float a4[4], r4[4], c4[4];
+  // 4-wide vector access needs the leading dimension AND the base pointer aligned to 4 elements
+  constexpr uintptr_t VA = 4 * sizeof(TC) - 1;
+  full4 = full4 && (p.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(C) & VA) == 0;
+  if (p.dact != ICAP_ACT_NONE) {
+    if (full4 && (p.ld_dact & 3) == 0 && (reinterpret_cast<uintptr_t>(dsrc) & VA) == 0) vec4io<TC>::ld(dsrc + row * p.ld_dact + col, a4);
+    else for (int e = 0; e < 4; ++e) a4[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float y = p.alpha * x[e];
+      if (use_drop) y *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
+      x[e] = y * act_bwd(p.dact, a4[e]);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = p.alpha * x[e] + bias4[e];
+    if (p.act != ICAP_ACT_NONE || aux) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float y = act_fwd(p.act, x[e]);
+        a4[e] = (p.act == ICAP_ACT_TANH) ? y : x[e];
+        x[e] = y;
+      }
+      if (aux) {
+        if (full4 && (p.ldaux & 3) == 0 && (reinterpret_cast<uintptr_t>(aux) & VA) == 0) vec4io<TC>::st(aux + row * p.ldaux + col, a4);
+        else for (int e = 0; e < 4; ++e) if (col + e < N) io<TC>::st(aux + row * p.ldaux + col + e, a4[e]);
+      }
+    }
+    if (use_drop) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
+    }
+    if (resid) {
+      if (full4 && (p.ldr & 3) == 0 && (reinterpret_cast<uintptr_t>(resid) & VA) == 0) vec4io<TC>::ld(resid + row * p.ldr + col, r4);
+      else for (int e = 0; e < 4; ++e) r4[e] = (col + e < N) ? io<TC>::ld(resid + row * p.ldr + col + e) : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] += r4[e];
+    }
+  }
+  TC* cp = C + row * p.ldc + col;
+  if (full4) {
+    if (p.beta != 0.f) {
+      vec4io<TC>::ld(cp, c4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] += p.beta * c4[e];
+    }
+    vec4io<TC>::st(cp, x);
+  } else {
+    for (int e = 0; e < 4; ++e)
+      if (col + e < N) io<TC>::st(cp + e, p.beta != 0.f ? x[e] + p.beta * io<TC>::ld(cp + e) : x[e]);
+  }
+}
+
+// NST: LDS stages (2 = double-buffered, DMA of stage k+1 overlaps the MFMAs of stage k; 1 = single buffer, two
+// barriers per K step, latency hidden by MINB co-resident blocks per CU).
+// DIRECT: MFMA operand roles swapped (acc = C^T fragments), so each lane owns 4 consecutive output COLUMNS of one
+// row and the epilogue is applied straight from the accumulators with 8/16-byte vector accesses; otherwise the
+// accumulators are re-laid out through LDS (needs NST == 2 for the staging space).
+template <typename TI, typename TC, int NST, int MINB, bool DIRECT>
+__global__ __launch_bounds__(GNT, MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits, int nk_split,
+                                                        uint32_t drop_thresh, float inv_keep) {
+  // LDS-staged epilogue: rows per staging pass (per wave EPR x EPI_LD fp32 must fit the stage buffers)
+  constexpr int EPR = NST == 2 ? 32 : 16;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_BYTES];
   constexpr int ES = sizeof(TI);
   constexpr int EPC = 16 / ES;         // elements per 16-byte chunk
   constexpr int BKE = GROWB / ES;      // K elements per stage
@@ -98,7 +172,10 @@ __global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tile
   const int bid = blockIdx.x, nwg = gridDim.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tm = wgid / tiles_n, tn = wgid - tm * tiles_n;
+  // split-K: split-major order, so the blocks of one split (same K range) sit together on an XCD
+  const int tiles = (int)(gridDim.x / splits);
+  const int split = wgid / tiles, tile = wgid - split * tiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int64_t m0 = (int64_t)tm * GBM, n0 = (int64_t)tn * GBN;
 
   const int64_t M = p.M, N = p.N, K = p.K;
@@ -144,19 +221,14 @@ __global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tile
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (int)((K + BKE - 1) / BKE);
-  load_stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
+  const int nk_all = (int)((K + BKE - 1) / BKE);
+  const int kt0 = split * nk_split;
+  const int nk = (nk_all - kt0 < nk_split ? nk_all - kt0 : nk_split);  // >= 1 by the host's choice of splits
+  const int64_t kbase = (int64_t)kt0 * BKE;
   const int fr = lane & 15, fg = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const char* As = smem + cur * STAGE_BYTES;
+
+  auto read_frags = [&](const char* As, uint4 (&af)[2][4], uint4 (&bfr)[2][4]) {
     const char* Bs = As + GBM * GROWB;
-    // all fragment reads of this stage first: hipcc waits vmcnt(0) before any LDS read that follows an
-    // LDS-DMA issue, so the next stage's DMA is issued only after the reads (and overlaps the MFMAs)
-    uint4 af[2][4], bfr[2][4];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + fg;
@@ -165,113 +237,275 @@ __global__ __launch_bounds__(GNT, 2) void gemm_kernel(icap_gemm_args p, int tile
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[ks][j] = *reinterpret_cast<const uint4*>(Bs + lds_off(wn * 64 + j * 16 + fr, ch));
     }
-    // the other buffer was last read in iteration kt-1, which every wave finished before the barrier below
-    if (kt + 1 < nk) load_stage((int64_t)(kt + 1) * BKE, cur ^ 1);
+  };
+  auto mfmas = [&](const uint4 (&af)[2][4], const uint4 (&bfr)[2][4]) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mfma_chunk<TI>(acc[i][j], af[ks][i], bfr[ks][j]);
-    // keep the MFMAs above the wait: they are register-only, so without this fence hipcc sinks them below the
-    // vmcnt/barrier and the DMA is waited for right after it is issued (cdna_hip_programming.md §5.4 rule 18)
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage kt+1 has landed
-    __syncthreads();                                      // ... and every other wave's
+        for (int j = 0; j < 4; ++j) {
+          if (DIRECT) mfma_chunk<TI>(acc[i][j], bfr[ks][j], af[ks][i]);  // C^T fragment: lane = row, regs = 4 cols
+          else mfma_chunk<TI>(acc[i][j], af[ks][i], bfr[ks][j]);         // C fragment: lane = col, regs = 4 rows
+        }
+  };
+
+  if (NST == 2) {
+    load_stage(kbase, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      // all fragment reads of this stage first: hipcc waits vmcnt(0) before any LDS read that follows an
+      // LDS-DMA issue, so the next stage's DMA is issued only after the reads (and overlaps the MFMAs)
+      uint4 af[2][4], bfr[2][4];
+      read_frags(smem + cur * STAGE_BYTES, af, bfr);
+      // the other buffer was last read in iteration kt-1, which every wave finished before the barrier below
+      if (kt + 1 < nk) load_stage(kbase + (int64_t)(kt + 1) * BKE, cur ^ 1);
+      mfmas(af, bfr);
+      // keep the MFMAs above the wait: they are register-only, so without this fence hipcc sinks them below the
+      // vmcnt/barrier and the DMA is waited for right after it is issued (cdna_hip_programming.md §5.4 rule 18)
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage kt+1 has landed
+      __syncthreads();                                      // ... and every other wave's
+    }
+  } else {
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt > 0) __syncthreads();  // every wave has finished reading the previous stage
+      load_stage(kbase + (int64_t)kt * BKE, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      uint4 af[2][4], bfr[2][4];
+      read_frags(smem, af, bfr);
+      mfmas(af, bfr);
+    }
   }
 
-  // ---- epilogue (LDS-staged, 4 columns per lane) ----
-  TC* C = reinterpret_cast<TC*>(p.C);
-  TC* aux = reinterpret_cast<TC*>(p.aux);
-  const TC* resid = reinterpret_cast<const TC*>(p.resid);
-  const TC* dsrc = reinterpret_cast<const TC*>(p.dact_src);
-  const bool use_drop = drop_thresh != 0u;
-  const uint64_t seed = use_drop ? eff_seed(p.seed, p.seed_ptr) : 0ull;
-  float* cs = reinterpret_cast<float*>(smem) + wave * (32 * EPI_LD);
+  uint64_t seed = 0;
+  if (splits == 1 && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
+  // split-K partial slab of this split: raw fp32 [M, N] (N % 4 == 0 is guaranteed by the host)
+  float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
+
+  if (DIRECT) {
+    // ---- epilogue straight from the accumulators: lane owns row m0+wm*64+16i+fr, cols n0+wn*64+16j+4fg..+3
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 16 + 4 * fg;
+      const bool full4 = col + 4 <= N;
+      float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = m0 + wm * 64 + i * 16 + fr;
+        if (row < M && col < N) {
+          float x[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = make_float4(x[0], x[1], x[2], x[3]);
+          else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
+        }
+      }
+    }
+    return;
+  }
+
+  // ---- LDS-staged epilogue (4 columns per lane) ----
+  float* cs = reinterpret_cast<float*>(smem) + wave * (EPR * EPI_LD);
   const int er = lane >> 4;         // row within a 4-row group
   const int ec = (lane & 15) * 4;   // first of this lane's 4 columns in the 64-column wave tile
   const int64_t col = n0 + wn * 64 + ec;
+  const bool full4 = col + 4 <= N;
   float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (p.bias && p.dact == ICAP_ACT_NONE) {
+  if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
   }
-  const bool full4 = (col + 4 <= N) && ((p.ldc & 3) == 0);
+  if (NST == 1) __syncthreads();  // the single stage buffer is still being read by other waves
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    // stage rows [32h, 32h+32) of this wave's 64x64 accumulator tile
+  for (int h = 0; h < 64 / EPR; ++h) {
+    // stage rows [EPR h, EPR h + EPR) of this wave's 64x64 accumulator tile
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
+    for (int ii = 0; ii < EPR / 16; ++ii)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) cs[(ii * 16 + fg * 4 + v) * EPI_LD + j * 16 + fr] = acc[2 * h + ii][j][v];
+        for (int v = 0; v < 4; ++v)
+          cs[(ii * 16 + fg * 4 + v) * EPI_LD + j * 16 + fr] = acc[(EPR / 16) * h + ii][j][v];
     __syncthreads();
 #pragma unroll 2
-    for (int t = 0; t < 8; ++t) {
-      const int lr = t * 4 + er;  // 0..31
-      const int64_t row = m0 + wm * 64 + h * 32 + lr;
+    for (int t = 0; t < EPR / 4; ++t) {
+      const int lr = t * 4 + er;  // 0..EPR-1
+      const int64_t row = m0 + wm * 64 + h * EPR + lr;
       float x[4];
       *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * EPI_LD + ec);
-      if (row < M) {
-        const uint64_t didx = p.offset + (uint64_t)(row * N + col);
-        float a4[4], r4[4], c4[4];
-        if (p.dact != ICAP_ACT_NONE) {
-          if (full4 && (p.ld_dact & 3) == 0) vec4io<TC>::ld(dsrc + row * p.ld_dact + col, a4);
-          else for (int e = 0; e < 4; ++e) a4[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float y = p.alpha * x[e];
-            if (use_drop) y *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
-            x[e] = y * act_bwd(p.dact, a4[e]);
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) x[e] = p.alpha * x[e] + bias4[e];
-          if (p.act != ICAP_ACT_NONE || aux) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float y = act_fwd(p.act, x[e]);
-              a4[e] = (p.act == ICAP_ACT_TANH) ? y : x[e];
-              x[e] = y;
-            }
-            if (aux) {
-              if (full4 && (p.ldaux & 3) == 0) vec4io<TC>::st(aux + row * p.ldaux + col, a4);
-              else for (int e = 0; e < 4; ++e) if (col + e < N) io<TC>::st(aux + row * p.ldaux + col + e, a4[e]);
-            }
-          }
-          if (use_drop) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) x[e] *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
-          }
-          if (resid) {
-            if (full4 && (p.ldr & 3) == 0) vec4io<TC>::ld(resid + row * p.ldr + col, r4);
-            else for (int e = 0; e < 4; ++e) r4[e] = (col + e < N) ? io<TC>::ld(resid + row * p.ldr + col + e) : 0.f;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) x[e] += r4[e];
-          }
-        }
-        TC* cp = C + row * p.ldc + col;
-        if (full4) {
-          if (p.beta != 0.f) {
-            vec4io<TC>::ld(cp, c4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) x[e] += p.beta * c4[e];
-          }
-          vec4io<TC>::st(cp, x);
-        } else {
-          for (int e = 0; e < 4; ++e)
-            if (col + e < N) io<TC>::st(cp + e, p.beta != 0.f ? x[e] + p.beta * io<TC>::ld(cp + e) : x[e]);
-        }
+      if (row < M && col < N) {
+        if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
+        else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
       }
     }
     __syncthreads();
   }
 }
 
+// Skinny-M GEMM (M <= 128: greedy-decode steps over the batch, CLIP projection, mapper input Linear).
+// A weight-streaming, latency-bound problem: block = 8 waves over a 16*NT-column slab of B (= W rows) and a
+// 16*MT-row slab of A (grid.y walks M, so no block streams all of A through its CU: per-CU L2 bandwidth, not
+// HBM, bounded the all-rows form); the waves split the K steps round-robin and keep SK_U steps of MFMA
+// fragments in flight each (range-checked buffer loads straight from HBM/L2). The fp32 partial tiles are reduced
+// through LDS in two rounds before the shared epilogue. One launch, no slabs.
+// Accumulators use the C layout (lane = column, 4 consecutive rows per lane).
+constexpr int SK_WAVES = 8;
+template <typename TI, typename TC, int NT, int MT>
+__global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_args p, uint32_t drop_thresh,
+                                                                  float inv_keep) {
+  constexpr int ES = sizeof(TI);
+  constexpr int EPC = 16 / ES;        // K elements per lane chunk
+  constexpr int KSTEP = 4 * EPC;      // K elements per MFMA chunk step (4 lane groups)
+  constexpr int BN = 16 * NT;
+  constexpr int RLD = BN + 4;         // fp32 stride of the LDS partial tiles
+  constexpr int HALF = SK_WAVES / 2;
+  constexpr int BM = 16 * MT;
+  constexpr int SK_U = 16 / (MT + NT) < 2 ? 2 : 16 / (MT + NT);  // k-steps in flight per wave
+  __shared__ __attribute__((aligned(16))) float red[HALF][BM * RLD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int64_t M = p.M, N = p.N, K = p.K;
+  const int64_t n0 = (int64_t)blockIdx.x * BN, m0 = (int64_t)blockIdx.y * BM;
+  const int64_t nrows = N - n0 < BN ? N - n0 : BN;
+  const int64_t mrows = M - m0 < BM ? M - m0 : BM;
+  const __amdgpu_buffer_rsrc_t ra =
+      make_rsrc(reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES, (uint64_t)((mrows - 1) * p.lda + K) * ES);
+  const __amdgpu_buffer_rsrc_t rb =
+      make_rsrc(reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
+  f32x4_t acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  // rows past M / N lie beyond the descriptor range (zero-filled); K-tail chunks and steps past the end are
+  // redirected out of range (zero fragments: the MFMAs on them add nothing)
+  uint32_t aoff[MT], boff[NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) aoff[i] = (uint32_t)(((i * 16 + fr) * p.lda + fg * EPC) * ES);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) boff[j] = (uint32_t)(((j * 16 + fr) * p.ldb + fg * EPC) * ES);
+  const int64_t nks = (K + KSTEP - 1) / KSTEP;
+  for (int64_t base = wave; base < nks; base += SK_WAVES * SK_U) {
+    uint4 af[SK_U][MT], bfr[SK_U][NT];
+#pragma unroll
+    for (int u = 0; u < SK_U; ++u) {
+      const int64_t k0 = (base + (int64_t)u * SK_WAVES) * KSTEP;
+      const bool kin = k0 + fg * EPC < K;
+      const uint32_t kb = (uint32_t)(k0 * ES);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bfr[u][j] = bload(rb, kin ? boff[j] + kb : OOB);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[u][i] = bload(ra, kin ? aoff[i] + kb : OOB);
+    }
+    // all SK_U steps' loads are issued before the first MFMA waits (without this fence hipcc sinks each load
+    // to its use and every MFMA waits out a full memory latency)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < SK_U; ++u)
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) mfma_chunk<TI>(acc[i][j], af[u][i], bfr[u][j]);
+  }
+  // round 1: waves [HALF, 2 HALF) park their partials, waves [0, HALF) add them; round 2: the HALF sums -> LDS
+  auto park = [&](float* dst) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) dst[(i * 16 + fg * 4 + v) * RLD + j * 16 + fr] = acc[i][j][v];
+  };
+  if (wave >= HALF) park(red[wave - HALF]);
+  __syncthreads();
+  if (wave < HALF) {
+    const float* src = red[wave];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[i][j][v] += src[(i * 16 + fg * 4 + v) * RLD + j * 16 + fr];
+    park(red[wave]);  // same addresses this lane just read: no cross-lane hazard
+  }
+  __syncthreads();
+  const uint64_t seed = drop_thresh != 0u ? eff_seed(p.seed, p.seed_ptr) : 0ull;
+  constexpr int QPR = BN / 4;  // 4-column quads per row
+  for (int qd = threadIdx.x; qd < BM * QPR; qd += 64 * SK_WAVES) {
+    const int r = qd / QPR, c = (qd - r * QPR) * 4;
+    const int64_t row = m0 + r, col = n0 + c;
+    if (row >= M || col >= N) continue;
+    float x[4];
+    *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(&red[0][r * RLD + c]);
+#pragma unroll
+    for (int w = 1; w < HALF; ++w) {
+      const float4 v = *reinterpret_cast<const float4*>(&red[w][r * RLD + c]);
+      x[0] += v.x; x[1] += v.y; x[2] += v.z; x[3] += v.w;
+    }
+    float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias && p.dact == ICAP_ACT_NONE) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
+    }
+    epi4<TC>(p, row, col, x, bias4, col + 4 <= N, seed, drop_thresh, inv_keep);
+  }
+}
+
+// Split-K reduction: sum the fp32 partial slabs of `splits` K-ranges in a fixed order (deterministic) and
+// apply the full epilogue. One thread per 4 consecutive columns.
+template <typename TC>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(icap_gemm_args p, int splits, uint32_t drop_thresh,
+                                                         float inv_keep) {
+  const int64_t M = p.M, N = p.N;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n4 = N >> 2;
+  if (q >= M * n4) return;
+  const int64_t row = q / n4, col = (q - row * n4) * 4;
+  const float* ws = reinterpret_cast<const float*>(p.workspace) + row * N + col;
+  float x[4];
+  *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(ws);
+  for (int s = 1; s < splits; ++s) {
+    const float4 v = *reinterpret_cast<const float4*>(ws + (int64_t)s * M * N);
+    x[0] += v.x; x[1] += v.y; x[2] += v.z; x[3] += v.w;
+  }
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias && p.dact == ICAP_ACT_NONE) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias4[e] = p.bias[col + e];  // flat-parameter views: only 4-byte aligned
+  }
+  const uint64_t seed = drop_thresh != 0u ? eff_seed(p.seed, p.seed_ptr) : 0ull;
+  epi4<TC>(p, row, col, x, bias4, true, seed, drop_thresh, inv_keep);
+}
+
 }  // namespace icap
 
 using namespace icap;
+
+// kernel variant (see gemm_kernel): ICAP_GEMM_VARIANT=0..3 overrides the default, for A/B measurements only
+static int gemm_variant_override() {
+  static const int v = [] {
+    const char* e = getenv("ICAP_GEMM_VARIANT");
+    return e ? atoi(e) : -1;
+  }();
+  return v;
+}
+
+// Measured on MI355X (tools/gemm_bench.py, profiles/r01_gemm_variants.txt): short K (<= 16 stages) is bound by the
+// per-block prologue/epilogue, which co-resident blocks hide -> single LDS buffer, 3-4 blocks/CU (4 when the
+// epilogue is heavy); long K favours the double-buffered main loop at 2 blocks/CU.
+static int gemm_variant(const icap_gemm_args& p, int64_t nk_per_block) {
+  const int o = gemm_variant_override();
+  if (o >= 0) return o;
+  if (nk_per_block > 16) return 0;
+  const bool heavy = p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE || p.aux || p.drop_p > 0.f;
+  return heavy ? 5 : 4;
+}
 
 extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   ICAP_REQUIRE(a != nullptr, "icap_gemm: null args");
@@ -294,21 +528,76 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   ICAP_REQUIRE(p.dact == ICAP_ACT_NONE || p.dact_src != nullptr, "icap_gemm: dact requires dact_src");
   ICAP_REQUIRE(p.drop_p >= 0.f && p.drop_p < 1.f, "icap_gemm: drop_p out of range");
   const int64_t tiles_m = (p.M + GBM - 1) / GBM, tiles_n = (p.N + GBN - 1) / GBN;
-  ICAP_REQUIRE(tiles_m * tiles_n < (1ll << 31), "icap_gemm: too many tiles");
+  const int64_t tiles = tiles_m * tiles_n;
+  ICAP_REQUIRE(tiles < (1ll << 26), "icap_gemm: too many tiles");
+  ICAP_REQUIRE(p.split_k >= 0, "icap_gemm: split_k must be >= 0");
+  // split-K over K stages for launches that cannot fill the chip (decode-time M = batch, small projections):
+  // fp32 partial slabs in the caller's workspace + one deterministic reduce/epilogue pass.
+  const int64_t bke = 128 / es;
+  const int64_t nk = (p.K + bke - 1) / bke;
+  const int64_t slab = p.M * p.N * (int64_t)sizeof(float);
+  int64_t splits = 1;
+  if (p.split_k > 1) {
+    splits = p.split_k;
+  } else if (p.split_k == 0 && p.workspace && (p.N & 3) == 0 && nk >= 2 && (tiles <= 64 || (tiles < 256 && nk >= 16))) {
+    // decode-sized launches (<= 64 tiles): as many splits as fill ~2 blocks/CU; under-filled long-K launches
+    // (dW products over all tokens, K = 3200+): keep >= 4 stages per split so the slab traffic stays small
+    splits = (512 + tiles - 1) / tiles;
+    if (tiles > 64 && splits > nk / 4) splits = nk / 4;
+    if (splits > 32) splits = 32;
+    if (splits > p.workspace_bytes / slab) splits = p.workspace_bytes / slab;
+  }
+  if (splits > nk) splits = nk;
+  if (splits < 1) splits = 1;
+  const int64_t nk_split = nk > 0 ? (nk + splits - 1) / splits : 0;
+  if (nk_split > 0) splits = (nk + nk_split - 1) / nk_split;  // every split gets >= 1 stage
+  if (splits > 1) {
+    ICAP_REQUIRE((p.N & 3) == 0, "icap_gemm: split-K requires N % 4 == 0");
+    ICAP_REQUIRE(p.workspace && (reinterpret_cast<uintptr_t>(p.workspace) & 15) == 0 &&
+                     p.workspace_bytes >= splits * slab,
+                 "icap_gemm: split-K workspace missing, misaligned or too small");
+  }
   const uint32_t thr = p.drop_p > 0.f ? drop_threshold(p.drop_p) : 0u;
   const float inv_keep = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
-  dim3 grid((unsigned)(tiles_m * tiles_n)), block(GNT);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (p.M <= 128 && p.split_k == 0 && tiles <= 128 && gemm_variant_override() < 0) {
+    const int nt = p.N > 1536 ? 2 : 1;  // 32-column slabs once there are enough of them
+    const dim3 sgrid((unsigned)((p.N + 16 * nt - 1) / (16 * nt)), (unsigned)((p.M + 31) / 32)), sblock(64 * SK_WAVES);
+#define ICAP_SKINNY(TI, TC)                                                                                   \
+  if (nt == 2) hipLaunchKernelGGL((gemm_skinny_kernel<TI, TC, 2, 2>), sgrid, sblock, 0, s, p, thr, inv_keep);   \
+  else hipLaunchKernelGGL((gemm_skinny_kernel<TI, TC, 1, 2>), sgrid, sblock, 0, s, p, thr, inv_keep);
+    if (p.in_dtype == ICAP_BF16) {
+      if (p.c_dtype == ICAP_BF16) { ICAP_SKINNY(bf16_t, bf16_t) } else { ICAP_SKINNY(bf16_t, float) }
+    } else {
+      if (p.c_dtype == ICAP_BF16) { ICAP_SKINNY(float, bf16_t) } else { ICAP_SKINNY(float, float) }
+    }
+#undef ICAP_SKINNY
+    return check_launch("icap_gemm(skinny)");
+  }
+  dim3 grid((unsigned)(tiles * splits)), block(GNT);
+  const int sp = (int)splits, nks = (int)nk_split, tn = (int)tiles_n;
+  const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
+  const int variant = gemm_variant(p, nk_split);
+#define ICAP_GEMM_LAUNCH(TI, TC)                                                                              \
+  switch (variant) {                                                                                          \
+    case 0: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 2, false>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 1: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 2, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break;  \
+    case 2: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 3, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break;  \
+    case 3: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 4: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 3, false>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    default: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 4, false>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+  }
   if (p.in_dtype == ICAP_BF16) {
-    if (p.c_dtype == ICAP_BF16)
-      hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t>), grid, block, 0, s, p, (int)tiles_n, thr, inv_keep);
-    else
-      hipLaunchKernelGGL((gemm_kernel<bf16_t, float>), grid, block, 0, s, p, (int)tiles_n, thr, inv_keep);
+    if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(bf16_t, bf16_t) } else { ICAP_GEMM_LAUNCH(bf16_t, float) }
   } else {
+    if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(float, bf16_t) } else { ICAP_GEMM_LAUNCH(float, float) }
+  }
+#undef ICAP_GEMM_LAUNCH
+  if (splits > 1) {
     if (p.c_dtype == ICAP_BF16)
-      hipLaunchKernelGGL((gemm_kernel<float, bf16_t>), grid, block, 0, s, p, (int)tiles_n, thr, inv_keep);
+      hipLaunchKernelGGL((gemm_splitk_reduce<bf16_t>), rgrid, dim3(256), 0, s, p, sp, thr, inv_keep);
     else
-      hipLaunchKernelGGL((gemm_kernel<float, float>), grid, block, 0, s, p, (int)tiles_n, thr, inv_keep);
+      hipLaunchKernelGGL((gemm_splitk_reduce<float>), rgrid, dim3(256), 0, s, p, sp, thr, inv_keep);
   }
   return check_launch("icap_gemm");
 }

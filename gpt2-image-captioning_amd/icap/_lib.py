@@ -40,6 +40,7 @@ class GemmArgs(C.Structure):
         ("resid", vp), ("ldr", i64),
         ("drop_p", f32), ("seed", u64), ("offset", u64),
         ("seed_ptr", vp),
+        ("workspace", vp), ("workspace_bytes", i64), ("split_k", i32),
     ]
 
 

@@ -69,9 +69,10 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          aux: Optional[Tensor] = None, dact: int = L.ACT_NONE, dact_src: Optional[Tensor] = None,
          resid: Optional[Tensor] = None, alpha: float = 1.0, beta: float = 0.0, drop: Dropout = NO_DROP,
          M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None,
-         alg_flops: Optional[float] = None) -> Tensor:
+         alg_flops: Optional[float] = None, split_k: int = 0) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
-    alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64)."""
+    alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).
+    split_k: 0 = automatic split-K for launches of <= 64 output tiles, 1 = never, > 1 = forced."""
     M = A.shape[0] if M is None else M
     K = A.shape[1] if K is None else K
     N = B.shape[0] if N is None else N
@@ -95,6 +96,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     if resid is not None:
         a.resid, a.ldr = resid.data_ptr(), _ld(resid)
     a.drop_p, a.seed, a.offset, a.seed_ptr = drop.p, drop.seed, drop.offset, drop.ptr
+    ws = gemm_workspace(A.device)
+    a.workspace, a.workspace_bytes, a.split_k = ws.data_ptr(), ws.numel() * 4, split_k
     if GEMM_TIMER is None:
         call("icap_gemm", C.byref(a), _stream())
     else:  # per-launch HIP-event timing (bench.py kernel roofline pass; never inside a captured graph)
@@ -104,6 +107,21 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
         GEMM_TIMER.launch(key, 2.0 * M * N * K if alg_flops is None else alg_flops,
                           lambda: call("icap_gemm", C.byref(a), _stream()))
     return out
+
+
+GEMM_WORKSPACE_BYTES = 64 << 20
+_gemm_ws = {}
+
+
+def gemm_workspace(device) -> Tensor:
+    """Per-device fp32 split-K scratch (GEMMs of this package are ordered on one stream per device, so one
+    buffer serves them all). Allocate it before any graph capture with gemm_workspace(device)."""
+    key = (device.type, device.index)
+    ws = _gemm_ws.get(key)
+    if ws is None:
+        ws = torch.empty(GEMM_WORKSPACE_BYTES // 4, dtype=torch.float32, device=device)
+        _gemm_ws[key] = ws
+    return ws
 
 
 GEMM_TIMER = None  # set to an object with .launch(key, flops, fn) to time every GEMM launch

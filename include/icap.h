@@ -84,6 +84,11 @@ typedef struct {
   const void* resid; int64_t ldr;        /* residual added last, or NULL */
   float drop_p; uint64_t seed; uint64_t offset;
   const uint64_t* seed_ptr;               /* optional device seed counter */
+  /* split-K: fp32 scratch of >= splits*M*N*4 bytes (16-byte aligned) or NULL.   */
+  /* split_k: 0 = automatic (only launches of <= 64 output tiles, N % 4 == 0,   */
+  /* and only when the workspace is given), 1 = never, > 1 = forced.            */
+  /* The partial sums are reduced in a fixed order (deterministic).             */
+  void* workspace; int64_t workspace_bytes; int32_t split_k;
 } icap_gemm_args;
 int icap_gemm(const icap_gemm_args* a, void* stream);
 

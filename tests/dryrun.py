@@ -36,7 +36,8 @@ def accesses(name, args):
         out += [("A", g.A, _rows(g.M, g.lda, g.K, ei)), ("B", g.B, _rows(g.N, g.ldb, g.K, ei)),
                 ("C", g.C, _rows(g.M, g.ldc, g.N, ec)), ("bias", g.bias, g.N * 4),
                 ("aux", g.aux, _rows(g.M, g.ldaux, g.N, ec)), ("dact_src", g.dact_src, _rows(g.M, g.ld_dact, g.N, ec)),
-                ("resid", g.resid, _rows(g.M, g.ldr, g.N, ec)), ("seed_ptr", g.seed_ptr, 8)]
+                ("resid", g.resid, _rows(g.M, g.ldr, g.N, ec)), ("seed_ptr", g.seed_ptr, 8),
+                ("workspace", g.workspace, g.workspace_bytes)]
     elif name in ("icap_attention_fwd", "icap_attention_bwd"):
         t = a[0]._obj
         es = ES[t.dtype]

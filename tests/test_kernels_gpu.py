@@ -99,6 +99,35 @@ def test_gemm_epilogues(dev, act, dtype):
     assert rel_err(dZ, ref) < (1e-5 if dtype == torch.float32 else 1e-2)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_split_k_matches_single_pass(dev, dtype):
+    """split-K (fp32 partial slabs + reduce/epilogue kernel) == one-pass epilogue: same dropout mask, same
+    aux/activation/residual, beta accumulation, and the backward dact epilogue."""
+    M, N, K = 128, 768, 1024
+    A = rnd((M, K), dev, dtype, 0.1, seed=31)
+    B = rnd((N, K), dev, dtype, 0.1, seed=32)
+    bias = rnd((N,), dev, scale=0.5, seed=33)
+    resid = rnd((M, N), dev, dtype, seed=34)
+    drop = ops.Dropout(0.1, seed=77, offset=5)
+    outs = {}
+    for sk in (1, 3, 0):
+        C = torch.empty((M, N), device=dev, dtype=dtype)
+        aux = torch.empty((M, N), device=dev, dtype=dtype)
+        ops.gemm(A, B, C, bias=bias, act=L.ACT_GELU_NEW, aux=aux, resid=resid, drop=drop, split_k=sk)
+        dZ = torch.empty((M, N), device=dev, dtype=dtype)
+        ops.gemm(A, B, dZ, dact=L.ACT_GELU_NEW, dact_src=aux, drop=drop, alpha=0.5, split_k=sk)
+        Cb = rnd((M, N), dev, seed=35)
+        ops.gemm(A, B, Cb, alpha=2.0, beta=1.0, split_k=sk)
+        outs[sk] = (C, aux, dZ, Cb)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    for sk in (3, 0):
+        for x, y in zip(outs[sk], outs[1]):
+            assert rel_err(x, y) < tol
+        assert torch.equal(outs[sk][0] == resid, outs[1][0] == resid)  # identical dropout positions
+    z = A.double() @ B.double().t()
+    assert rel_err(outs[3][1], z + bias.double()) < tol
+
+
 def test_gemm_dropout_statistics(dev):
     M, N, K = 512, 512, 64
     A = torch.ones((M, K), device=dev)
@@ -268,3 +297,30 @@ def test_transpose_colsum_dropout(dev):
     assert not torch.equal(y, y2)
     m = y != 0
     assert torch.allclose(y[m], 2 * x[m])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_greedy_next_argmax(dev, dtype):
+    """icap_greedy_next == torch.argmax (NaN first, ties -> smallest index) + EOS/forced bookkeeping and the
+    fused next-token embedding (src/models.py:320-330 greedy loop)."""
+    B, V, ld, D, eos = 6, 50257, 50304, 64, 50256
+    g = torch.Generator().manual_seed(60)
+    lg = torch.randn((B, ld), generator=g).to(dtype)
+    lg[1, 1000] = lg[1, 40000] = 100.0        # tie -> 1000
+    lg[2, 50250] = 1e4                         # winner in the unaligned tail
+    lg[3, 7] = float("nan")                    # NaN wins
+    lg[4, V:] = 1e9                            # padding columns must be ignored
+    finished = torch.tensor([0, 0, 0, 0, 0, 1], dtype=torch.int32)
+    tokens = torch.zeros((B, 4), dtype=torch.int64)
+    wte = torch.randn((V, D), generator=g).to(dtype)
+    wpe = torch.randn((10, D), generator=g).to(dtype)
+    x = torch.empty((B, D), dtype=dtype)
+    lgd, fd, td, xd = lg.to(dev), finished.to(dev), tokens.to(dev), x.to(dev)
+    ops.greedy_next(lgd, V, eos, fd, td, 2, wte.to(dev), wpe.to(dev), 5, D, xd)
+    ref = torch.argmax(lg[:, :V].float(), dim=-1)
+    ref[5] = eos
+    assert td[:, 2].cpu().tolist() == ref.tolist()
+    assert td[:, 2].cpu()[1].item() == 1000 and td[:, 2].cpu()[3].item() == 7
+    assert fd.cpu().tolist() == [int(t == eos) or f for t, f in zip(ref.tolist(), finished.tolist())]
+    xr = (wte.float()[ref] + wpe.float()[5]).to(dtype)
+    assert torch.equal(xd.cpu(), xr)
