@@ -266,8 +266,7 @@ static int check_attn(const icap_attn_args* a, bool bwd) {
   ICAP_REQUIRE(a->qkv && (bwd ? (a->dout && a->dqkv && a->lse) : (a->out != nullptr)), "icap_attention: null pointer");
   ICAP_REQUIRE(a->ld_qkv % 4 == 0, "icap_attention: ld_qkv must be a multiple of 4");
   ICAP_REQUIRE(a->drop_p >= 0.f && a->drop_p < 1.f, "icap_attention: drop_p out of range");
-  const size_t need = bwd ? bwd_lds(a->S, a->hd) : fwd_lds(a->S, a->hd);
-  ICAP_REQUIRE(need <= LDS_CAP, "icap_attention: sequence/head too large for the LDS-resident kernel");
+
   return ICAP_OK;
 }
 
@@ -285,6 +284,7 @@ extern "C" int icap_attention_fwd(const icap_attn_args* a, void* stream) {
   const size_t lds = fwd_lds(a->S, a->hd);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!force_valu() && mfma_attention_ok(a, false)) return mfma_attention_launch(a, false, thr, inv_keep, s);
+  ICAP_REQUIRE(fwd_lds(a->S, a->hd) <= LDS_CAP, "icap_attention: sequence/head too large for the LDS-resident kernel");
   dim3 grid((unsigned)(a->B * a->H)), block(256);
   if (a->dtype == ICAP_BF16) {
     static bool once = (raise_lds_limit(attn_fwd_kernel<bf16_t>), true); (void)once;
@@ -306,6 +306,7 @@ extern "C" int icap_attention_bwd(const icap_attn_args* a, void* stream) {
   const size_t lds = bwd_lds(a->S, a->hd);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!force_valu() && mfma_attention_ok(a, true)) return mfma_attention_launch(a, true, thr, inv_keep, s);
+  ICAP_REQUIRE(bwd_lds(a->S, a->hd) <= LDS_CAP, "icap_attention: sequence/head too large for the LDS-resident kernel");
   dim3 grid((unsigned)(a->B * a->H)), block(256);
   if (a->dtype == ICAP_BF16) {
     static bool once = (raise_lds_limit(attn_bwd_kernel<bf16_t>), true); (void)once;

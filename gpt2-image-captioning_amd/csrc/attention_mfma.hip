@@ -303,6 +303,217 @@ __global__ __launch_bounds__(256) void bwd_kernel(icap_attn_args p, Geo g, uint3
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Backward v2 (needs the forward output O: delta[q] = rowsum(dO o O) = rowsum(P o dP), dropout included).
+// Q, K, V, dO of the head are staged ROW-major in LDS once (16-byte copies, rows padded to HD+8 halves so the
+// 16-row fragment reads hit 16 distinct 4-bank groups); no scalar transposes. Waves split by role:
+//   waves [0, nt)   : one 16-key tile each -> dV^T = dO^T P_drop, dK^T = Q^T dS over all queries,
+//   waves [nt, 2nt) : one 16-query tile each -> dQ^T = K^T dS^T over all keys,
+// where the first products (S = Q K^T, dP = dO V^T, in whichever orientation puts the contraction index of the
+// second product into the accumulator ROWS) come from row fragments, and the second products take the bf16
+// accumulator tile as the B operand directly (two 16-row tiles = one 32-deep k step; element j of lane group g
+// is row 4g+j / 16+4g+j-4) with the A operand read transposed by ds_read_b64_tr_b16 from the same row-major
+// image (cdna_hip_programming.md "An accumulator tile as the next MFMA's operand", T10). Outputs come out with
+// 4 consecutive head dims per lane (8-byte stores).
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_t* lds_v4s_ptr;
+
+template <int LDR>
+__device__ __forceinline__ uint4 rowfrag(const bf16_t* base, int r0, int k0, int lane) {
+  return *reinterpret_cast<const uint4*>(base + (r0 + (lane & 15)) * LDR + k0 + 8 * (lane >> 4));
+}
+// A operand [m = column c0 + (lane & 15)][k = 32-row block starting at r0] of a row-major LDS image, in the
+// k order of an accumulator-tile B operand (element j of group g = row r0 + 4g + j, j < 4; r0 + 16 + 4g + j - 4)
+template <int LDR>
+__device__ __forceinline__ uint4 trfrag(const bf16_t* base, int r0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const bf16_t* a0 = base + (r0 + 4 * g + (i >> 2)) * LDR + c0 + 4 * (i & 3);
+  const bf16_t* a1 = a0 + 16 * LDR;
+  const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(a0));
+  const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(a1));
+  uint4 r;
+  r.x = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
+  r.y = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
+  r.z = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
+  r.w = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
+  return r;
+}
+
+template <int HD>
+__global__ __launch_bounds__(HD == 64 ? 1024 : 512) void bwd2_kernel(icap_attn_args p, Geo g, uint32_t thr,
+                                                                     float inv_keep) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
+  constexpr int LDR = HD + 8;
+  constexpr int NKS = HD / 32;  // 32-deep k steps over the head dim
+  constexpr int NDT = HD / 16;  // 16-wide head-dim tiles of the outputs
+  constexpr int CPR = HD / 8;   // 16-byte chunks per row
+  const int Sp = g.Sp32, S = g.S;
+  const int bh = blockIdx.x;
+  const int b = bh / g.H, h = bh - b * g.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nt = g.Sp16 >> 4;
+  bf16_t* Qs = sm;
+  bf16_t* Ks = Qs + Sp * LDR;
+  bf16_t* Vs = Ks + Sp * LDR;
+  bf16_t* dOs = Vs + Sp * LDR;
+  float* lse_s = reinterpret_cast<float*>(dOs + Sp * LDR);
+  float* delta_s = lse_s + Sp;
+  const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
+  const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
+  const bf16_t* outp = reinterpret_cast<const bf16_t*>(p.out);
+  for (int r = threadIdx.x; r < Sp; r += blockDim.x) {
+    lse_s[r] = r < S ? p.lse[(int64_t)bh * S + r] : -INFINITY;
+    delta_s[r] = 0.f;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < Sp * CPR; idx += blockDim.x) {
+    const int r = idx / CPR, c = idx - r * CPR;
+    uint4 q = make_uint4(0, 0, 0, 0), k = q, v = q, d = q;
+    if (r < S) {
+      const int64_t row = trow(g, b, r);
+      const bf16_t* src = qkv + row * p.ld_qkv + h * HD + 8 * c;
+      q = *reinterpret_cast<const uint4*>(src);
+      k = *reinterpret_cast<const uint4*>(src + g.D);
+      v = *reinterpret_cast<const uint4*>(src + 2 * g.D);
+      d = *reinterpret_cast<const uint4*>(dout + row * p.ld_dout + h * HD + 8 * c);
+    }
+    *reinterpret_cast<uint4*>(Qs + r * LDR + 8 * c) = q;
+    *reinterpret_cast<uint4*>(Ks + r * LDR + 8 * c) = k;
+    *reinterpret_cast<uint4*>(Vs + r * LDR + 8 * c) = v;
+    *reinterpret_cast<uint4*>(dOs + r * LDR + 8 * c) = d;
+  }
+  // delta[q] = sum_d dO[q][d] O[q][d], one thread per query in a fixed order (deterministic)
+  for (int r = threadIdx.x; r < S; r += blockDim.x) {
+    const int64_t row = trow(g, b, r);
+    const bf16_t* orow = outp + row * p.ld_out + h * HD;
+    const bf16_t* drow = dout + row * p.ld_dout + h * HD;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPR; ++c) {
+      const uint4 o = *reinterpret_cast<const uint4*>(orow + 8 * c);
+      const uint4 d = *reinterpret_cast<const uint4*>(drow + 8 * c);
+      const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc += __uint_as_float(dw[e] << 16) * __uint_as_float(ow[e] << 16) +
+               __uint_as_float(dw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+    }
+    delta_s[r] = acc;
+  }
+  __syncthreads();
+  const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
+  const uint64_t dbase = p.offset + (uint64_t)bh * S * S;
+  bf16_t* dqkv = reinterpret_cast<bf16_t*>(p.dqkv);
+  const int npair = Sp >> 5;
+  if (wave < nt) {
+    // ---- dK, dV for keys [16 kt, 16 kt + 16): accumulators C[q][key] (lane = key, rows = 4 queries)
+    const int kt = wave;
+    const int key = kt * 16 + fr;
+    uint4 kf[NKS], vf[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      kf[ks] = rowfrag<LDR>(Ks, kt * 16, ks * 32, lane);
+      vf[ks] = rowfrag<LDR>(Vs, kt * 16, ks * 32, lane);
+    }
+    f32x4_t dv[NDT], dk[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) dv[dt] = dk[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int qp0 = p.causal ? (kt * 16) >> 5 : 0;  // earlier query pairs see none of these keys
+    for (int qp = qp0; qp < npair; ++qp) {
+      float pd[8], ds[8];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const int qt = 2 * qp + sub;
+        f32x4_t sc = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dp = sc;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          sc = mfma(rowfrag<LDR>(Qs, qt * 16, ks * 32, lane), kf[ks], sc);
+          dp = mfma(rowfrag<LDR>(dOs, qt * 16, ks * 32, lane), vf[ks], dp);
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int q = qt * 16 + 4 * fg + v;
+          const float lse = lse_s[q];
+          float pv = 0.f;
+          if (lse != -INFINITY && key_ok(p.causal, p.key_mask, g, b, q, key)) pv = __expf(sc[v] * p.scale - lse);
+          float ms = 1.f;
+          if (thr && q < S && key < S) ms = drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
+          pd[sub * 4 + v] = pv * ms;
+          ds[sub * 4 + v] = pv * (dp[v] * ms - delta_s[q]);
+        }
+      }
+      uint4 xp, xs;
+      xp.x = f2bf2(pd[0], pd[1]); xp.y = f2bf2(pd[2], pd[3]); xp.z = f2bf2(pd[4], pd[5]); xp.w = f2bf2(pd[6], pd[7]);
+      xs.x = f2bf2(ds[0], ds[1]); xs.y = f2bf2(ds[2], ds[3]); xs.z = f2bf2(ds[4], ds[5]); xs.w = f2bf2(ds[6], ds[7]);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        dv[dt] = mfma(trfrag<LDR>(dOs, qp * 32, dt * 16, lane), xp, dv[dt]);
+        dk[dt] = mfma(trfrag<LDR>(Qs, qp * 32, dt * 16, lane), xs, dk[dt]);
+      }
+    }
+    if (key < S) {
+      bf16_t* rowp = dqkv + trow(g, b, key) * p.ld_dqkv + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const int d0 = dt * 16 + 4 * fg;
+        *reinterpret_cast<uint2*>(rowp + g.D + d0) =
+            make_uint2(f2bf2(dk[dt][0] * p.scale, dk[dt][1] * p.scale), f2bf2(dk[dt][2] * p.scale, dk[dt][3] * p.scale));
+        *reinterpret_cast<uint2*>(rowp + 2 * g.D + d0) =
+            make_uint2(f2bf2(dv[dt][0], dv[dt][1]), f2bf2(dv[dt][2], dv[dt][3]));
+      }
+    }
+  } else if (wave < 2 * nt) {
+    // ---- dQ for queries [16 qt, 16 qt + 16): accumulators C[key][q] (lane = query, rows = 4 keys)
+    const int qt = wave - nt;
+    const int q = qt * 16 + fr;
+    uint4 qf[NKS], of[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      qf[ks] = rowfrag<LDR>(Qs, qt * 16, ks * 32, lane);
+      of[ks] = rowfrag<LDR>(dOs, qt * 16, ks * 32, lane);
+    }
+    const float lse = lse_s[q], de = delta_s[q];
+    f32x4_t dq[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) dq[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    const int kp1 = p.causal ? ((qt * 16 + 15) >> 5) + 1 : npair;  // later key pairs are all masked
+    for (int kp = 0; kp < kp1 && kp < npair; ++kp) {
+      float ds[8];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const int kt = 2 * kp + sub;
+        f32x4_t st = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dpt = st;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          st = mfma(rowfrag<LDR>(Ks, kt * 16, ks * 32, lane), qf[ks], st);
+          dpt = mfma(rowfrag<LDR>(Vs, kt * 16, ks * 32, lane), of[ks], dpt);
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int key = kt * 16 + 4 * fg + v;
+          float pv = 0.f;
+          if (lse != -INFINITY && key_ok(p.causal, p.key_mask, g, b, q, key)) pv = __expf(st[v] * p.scale - lse);
+          float ms = 1.f;
+          if (thr && q < S && key < S) ms = drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
+          ds[sub * 4 + v] = pv * (dpt[v] * ms - de);
+        }
+      }
+      uint4 xs;
+      xs.x = f2bf2(ds[0], ds[1]); xs.y = f2bf2(ds[2], ds[3]); xs.z = f2bf2(ds[4], ds[5]); xs.w = f2bf2(ds[6], ds[7]);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) dq[dt] = mfma(trfrag<LDR>(Ks, kp * 32, dt * 16, lane), xs, dq[dt]);
+    }
+    if (q < S) {
+      bf16_t* rowp = dqkv + trow(g, b, q) * p.ld_dqkv + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+        *reinterpret_cast<uint2*>(rowp + dt * 16 + 4 * fg) =
+            make_uint2(f2bf2(dq[dt][0] * p.scale, dq[dt][1] * p.scale), f2bf2(dq[dt][2] * p.scale, dq[dt][3] * p.scale));
+    }
+  }
+}
+
 }  // namespace amfma
 
 static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
@@ -318,6 +529,21 @@ amfma::Geo mfma_geo(const icap_attn_args* a) {
 size_t mfma_fwd_lds(const amfma::Geo& g) { return 2 * ((size_t)g.hd * g.ldT + 4 * 16 * (size_t)g.ldT); }
 size_t mfma_bwd_lds(const amfma::Geo& g) {
   return 2 * (3 * (size_t)g.hd * g.ldT + 2 * (size_t)g.Sp16 * g.ldT + 4 * 16 * (size_t)g.ldT);
+}
+
+size_t mfma_bwd2_lds(const amfma::Geo& g) {
+  return 2 * 4 * (size_t)g.Sp32 * (g.hd + 8) + 2 * sizeof(float) * (size_t)g.Sp32;
+}
+
+// v2 backward: needs O (delta), 16-byte aligned row segments, and 2 * Sp16/16 waves within the launch bound
+static bool mfma_bwd2_ok(const icap_attn_args* a) {
+  if (a->out == nullptr || (a->ld_out & 7) || (a->ld_dqkv & 7)) return false;
+  if ((reinterpret_cast<uintptr_t>(a->out) | reinterpret_cast<uintptr_t>(a->qkv) |
+       reinterpret_cast<uintptr_t>(a->dout) | reinterpret_cast<uintptr_t>(a->dqkv)) & 15)
+    return false;
+  const amfma::Geo g = mfma_geo(a);
+  const int waves = 2 * (g.Sp16 / 16);
+  return waves * 64 <= (a->hd == 64 ? 1024 : 512) && mfma_bwd2_lds(g) <= 160 * 1024;
 }
 
 bool mfma_attention_ok(const icap_attn_args* a, bool bwd) {
@@ -346,6 +572,18 @@ int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float
       hipLaunchKernelGGL(amfma::fwd_kernel<96>, grid, block, lds, s, *a, g, thr, inv_keep);
     }
   } else {
+    if (mfma_bwd2_ok(a)) {
+      const size_t lds2 = mfma_bwd2_lds(g);
+      const dim3 block2((unsigned)(64 * 2 * (g.Sp16 / 16)));
+      if (a->hd == 64) {
+        static bool once = (lds_limit(amfma::bwd2_kernel<64>), true); (void)once;
+        hipLaunchKernelGGL(amfma::bwd2_kernel<64>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+      } else {
+        static bool once = (lds_limit(amfma::bwd2_kernel<96>), true); (void)once;
+        hipLaunchKernelGGL(amfma::bwd2_kernel<96>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+      }
+      return check_launch("icap_attention_bwd(mfma v2)");
+    }
     const size_t lds = mfma_bwd_lds(g);
     if (a->hd == 64) {
       static bool once = (lds_limit(amfma::bwd_kernel<64>), true); (void)once;

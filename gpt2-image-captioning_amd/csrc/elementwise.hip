@@ -316,6 +316,70 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int64_t N, const
   if (ty == 0 && c < N) partial[(int64_t)blockIdx.y * N + c] = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
 }
 
+// 16-bit transpose with 16-byte accesses on both sides: 64x64 tile through LDS (row stride 68 halves, so the
+// column gathers of the write phase are at most 2-way bank conflicted). Needs cols % 8 == 0, lds/ldd % 8 == 0,
+// 16-byte aligned src/dst and rows_pad % 64 == 0 (checked by the host).
+__global__ __launch_bounds__(256) void transpose16_vec_kernel(int64_t rows, int64_t cols, const uint16_t* __restrict__ src,
+                                                              int64_t lds, uint16_t* __restrict__ dst, int64_t ldd) {
+  constexpr int TLD = 68;
+  __shared__ __attribute__((aligned(16))) uint16_t tile[64 * TLD];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = threadIdx.x + 256 * h;
+    const int r = idx >> 3, ch = idx & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + r < rows && c0 + 8 * ch < cols) v = *reinterpret_cast<const uint4*>(src + (r0 + r) * lds + c0 + 8 * ch);
+    uint2* t = reinterpret_cast<uint2*>(&tile[r * TLD + 8 * ch]);
+    t[0] = make_uint2(v.x, v.y);
+    t[1] = make_uint2(v.z, v.w);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int idx = threadIdx.x + 256 * h;
+    const int c = idx >> 3, rq = idx & 7;
+    if (c0 + c >= cols) continue;
+    uint32_t w[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      w[e] = (uint32_t)tile[(8 * rq + 2 * e) * TLD + c] | ((uint32_t)tile[(8 * rq + 2 * e + 1) * TLD + c] << 16);
+    *reinterpret_cast<uint4*>(dst + (c0 + c) * ldd + r0 + 8 * rq) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// column sums, 4 columns per lane (16-byte / 8-byte row segments), 4 waves over the rows of a chunk
+template <typename T>
+__global__ __launch_bounds__(256) void colsum4_kernel(int64_t M, int64_t N, const T* __restrict__ src, int64_t ld,
+                                                     int64_t rows_per_chunk, float* __restrict__ partial) {
+  __shared__ float4 red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  const int64_t m0 = (int64_t)blockIdx.y * rows_per_chunk;
+  int64_t m1 = m0 + rows_per_chunk;
+  if (m1 > M) m1 = M;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+#pragma unroll 4
+    for (int64_t m = m0 + w; m < m1; m += 4) {
+      float v[4];
+      io<T>::ld4(src + m * ld + c, v);
+      a[0] += v[0]; a[1] += v[1]; a[2] += v[2]; a[3] += v[3];
+    }
+  }
+  red[w][lane] = make_float4(a[0], a[1], a[2], a[3]);
+  __syncthreads();
+  if (w == 0 && c < N) {
+    float4 t = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 u = red[k][lane];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    *reinterpret_cast<float4*>(partial + (int64_t)blockIdx.y * N + c) = t;
+  }
+}
+
 __global__ void colsum_reduce_kernel(int64_t N, int nchunks, const float* __restrict__ partial, float* out, int acc) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= N) return;
@@ -616,7 +680,12 @@ extern "C" int icap_transpose(int32_t dtype, int64_t rows, int64_t cols, const v
   if (rows_pad == 0 || cols == 0) return ICAP_OK;
   dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows_pad + 63) / 64));
   ICAP_REQUIRE(grid.y < 65536, "icap_transpose: too many rows");
-  if (dtype == ICAP_BF16)
+  const bool vec = dtype == ICAP_BF16 && cols % 8 == 0 && lds % 8 == 0 && ldd % 8 == 0 && rows_pad % 64 == 0 &&
+                   (reinterpret_cast<uintptr_t>(src) & 15) == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(transpose16_vec_kernel, grid, dim3(256), 0, S_(stream), rows, cols, (const uint16_t*)src, lds,
+                       (uint16_t*)dst, ldd);
+  else if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(transpose_kernel<uint16_t>, grid, dim3(256), 0, S_(stream), rows, cols, (const uint16_t*)src,
                        lds, (uint16_t*)dst, ldd, rows_pad);
   else
@@ -626,7 +695,7 @@ extern "C" int icap_transpose(int32_t dtype, int64_t rows, int64_t cols, const v
 }
 
 static int64_t colsum_chunks(int64_t M) {
-  int64_t c = (M + 255) / 256;
+  int64_t c = (M + 31) / 32;
   if (c > 64) c = 64;
   if (c < 1) c = 1;
   return c;
@@ -643,9 +712,16 @@ extern "C" int icap_colsum(int32_t dtype, int64_t M, int64_t N, const void* src,
   const int64_t ch = colsum_chunks(M);
   const int64_t rpc = (M + ch - 1) / ch;
   float* partial = reinterpret_cast<float*>(workspace);
-  dim3 grid((unsigned)((N + 63) / 64), (unsigned)ch);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_kernel<T>, grid, dim3(256), 0, S_(stream), M, N, CTP(src), ld,
-                                       rpc > 0 ? rpc : 1, partial));
+  const int es = dtype == ICAP_BF16 ? 2 : 4;
+  if (N % 4 == 0 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(src) % (4 * es)) == 0) {
+    dim3 grid4((unsigned)((N + 255) / 256), (unsigned)ch);
+    DISPATCH_T(dtype, hipLaunchKernelGGL(colsum4_kernel<T>, grid4, dim3(256), 0, S_(stream), M, N, CTP(src), ld,
+                                         rpc > 0 ? rpc : 1, partial));
+  } else {
+    dim3 grid((unsigned)((N + 63) / 64), (unsigned)ch);
+    DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_kernel<T>, grid, dim3(256), 0, S_(stream), M, N, CTP(src), ld,
+                                         rpc > 0 ? rpc : 1, partial));
+  }
   int rc = check_launch("icap_colsum");
   if (rc) return rc;
   hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, S_(stream), N, (int)ch,

@@ -396,7 +396,7 @@ class GPT2Core:
                 dw.db(dy, g.b_proj, M=M)
             ops.gemm(dy, lw.w_proj, ws.do)
             ops.attention_bwd(ws.qkv[l], ws.do, ws.lse[l], ws.dqkv, B=B, S=S, H=H, hd=hd, scale=scale, causal=True,
-                              key_mask=causal_mask, drop=dr.attn(l))
+                              key_mask=causal_mask, drop=dr.attn(l), out=ws.o[l])
             if g is not None:
                 dw.dW(ws.dqkv, ws.a1[l], g.w_attn, M=M, transpose_out=True)
                 dw.db(ws.dqkv, g.b_attn, M=M)

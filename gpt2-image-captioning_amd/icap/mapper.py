@@ -379,7 +379,7 @@ class TransformerMapperCore:
             dwh.db(dy, gl.out_b, M=M)
             ops.gemm(dy, w.out_wt, ws.do)
             ops.attention_bwd(ws.qkv[l], ws.do, ws.lse[l], ws.dqkv, B=B, S=S, H=self.H, hd=self.hd, scale=scale,
-                              causal=False, drop=dr.attn(l))
+                              causal=False, drop=dr.attn(l), out=ws.o[l])
             dwh.dW(ws.dqkv, ws.a1[l], gl.in_w, M=M)
             dwh.db(ws.dqkv, gl.in_b, M=M)
             ops.gemm(ws.dqkv, w.in_wt, ws.da)

@@ -179,8 +179,11 @@ def attention_fwd(qkv: Tensor, out: Tensor, *, B: int, S: int, H: int, hd: int, 
 
 def attention_bwd(qkv: Tensor, dout: Tensor, lse: Tensor, dqkv: Tensor, *, B: int, S: int, H: int, hd: int,
                   scale: float, causal: bool = False, key_mask: Optional[Tensor] = None, drop: Dropout = NO_DROP,
-                  rsb: Optional[int] = None, rss: int = 1) -> Tensor:
+                  rsb: Optional[int] = None, rss: int = 1, out: Optional[Tensor] = None) -> Tensor:
+    """out: the forward's O (optional; enables the transpose-free bf16 MFMA backward)."""
     a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop)
+    if out is not None:
+        a.out, a.ld_out = out.data_ptr(), _ld(out)
     a.dout, a.ld_dout = dout.data_ptr(), _ld(dout)
     a.dqkv, a.ld_dqkv = dqkv.data_ptr(), _ld(dqkv)
     call("icap_attention_bwd", C.byref(a), _stream())

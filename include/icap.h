@@ -129,7 +129,8 @@ typedef struct {
   int32_t B, S, H, hd;
   int64_t row_stride_b, row_stride_s;
   const void* qkv; int64_t ld_qkv;
-  void* out; int64_t ld_out;
+  void* out; int64_t ld_out;  /* fwd: O (written). bwd: O of the forward (read, optional: with it the   */
+                              /* bf16 MFMA backward takes delta = rowsum(dO o O) and needs no transposes) */
   float* lse;               /* [B*H*S] fp32 log-sum-exp of scaled scores, or NULL */
   const int32_t* key_mask;  /* [B*S] or NULL */
   int32_t causal;

@@ -48,7 +48,8 @@ def accesses(name, args):
         if name == "icap_attention_fwd":
             out.append(("out", t.out, (maxrow * t.ld_out + D) * es))
         else:
-            out += [("dout", t.dout, (maxrow * t.ld_dout + D) * es), ("dqkv", t.dqkv, (maxrow * t.ld_dqkv + 3 * D) * es)]
+            out += [("dout", t.dout, (maxrow * t.ld_dout + D) * es), ("dqkv", t.dqkv, (maxrow * t.ld_dqkv + 3 * D) * es),
+                    ("out", t.out, (maxrow * t.ld_out + D) * es)]
     elif name == "icap_adamw_step":
         t = a[0]._obj
         n = t.n

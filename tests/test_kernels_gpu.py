@@ -208,11 +208,32 @@ def test_attention(dev, dtype, B, S, H, hd, causal, masked):
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert rel_err(out, o2) < tol
     dout = rnd((B * S, D), dev, dtype, seed=21)
-    dqkv = torch.empty_like(qkv)
-    ops.attention_bwd(qkv, dout, lse, dqkv, B=B, S=S, H=H, hd=hd, scale=scale, causal=causal, key_mask=key_mask)
     (gx,) = torch.autograd.grad(o2, x, dout.double())
     g = gx.permute(1, 3, 0, 2, 4).reshape(B * S, 3 * D)
-    assert rel_err(dqkv, g) < (1e-5 if dtype == torch.float32 else 2e-2)
+    # without O (transposing backward) and with O (delta = rowsum(dO o O), transpose-free MFMA backward)
+    for o_arg in (None, out):
+        dqkv = torch.empty_like(qkv)
+        ops.attention_bwd(qkv, dout, lse, dqkv, B=B, S=S, H=H, hd=hd, scale=scale, causal=causal,
+                          key_mask=key_mask, out=o_arg)
+        assert rel_err(dqkv, g) < (1e-5 if dtype == torch.float32 else 2e-2)
+
+
+@pytest.mark.parametrize("B,S,H,hd,causal", [(3, 65, 12, 64, True), (2, 25, 8, 96, False), (2, 128, 4, 64, True)])
+def test_attention_bwd_dropout_paths_agree(dev, B, S, H, hd, causal):
+    """bf16 backward with attention dropout: the O-based (v2) and the transposing (v1) backward see the same
+    counter-based mask (index (b*H+h)*S*S + q*S + k) and agree."""
+    D = H * hd
+    qkv = rnd((B * S, 3 * D), dev, torch.bfloat16, seed=23)
+    out = torch.empty((B * S, D), device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=dev)
+    drop = ops.Dropout(0.1, seed=99, offset=7)
+    scale = 1.0 / math.sqrt(hd)
+    ops.attention_fwd(qkv, out, B=B, S=S, H=H, hd=hd, scale=scale, causal=causal, lse=lse, drop=drop)
+    dout = rnd((B * S, D), dev, torch.bfloat16, seed=24)
+    d1, d2 = torch.empty_like(qkv), torch.empty_like(qkv)
+    ops.attention_bwd(qkv, dout, lse, d1, B=B, S=S, H=H, hd=hd, scale=scale, causal=causal, drop=drop)
+    ops.attention_bwd(qkv, dout, lse, d2, B=B, S=S, H=H, hd=hd, scale=scale, causal=causal, drop=drop, out=out)
+    assert rel_err(d2, d1) < 2e-2
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
@@ -324,3 +345,17 @@ def test_greedy_next_argmax(dev, dtype):
     assert fd.cpu().tolist() == [int(t == eos) or f for t, f in zip(ref.tolist(), finished.tolist())]
     xr = (wte.float()[ref] + wpe.float()[5]).to(dtype)
     assert torch.equal(xd.cpu(), xr)
+
+
+@pytest.mark.parametrize("rows,cols,rows_pad", [(3200, 768, 3200), (77, 136, 128), (130, 96, 192)])
+def test_transpose_colsum_bf16_vector_paths(dev, rows, cols, rows_pad):
+    """16-byte transpose / 4-column colsum fast paths (dW operand staging of the mapper, bias grads)."""
+    x = rnd((rows, cols), dev, torch.bfloat16, seed=51)
+    t = torch.full((cols, rows_pad), 3.0, device=dev, dtype=torch.bfloat16)
+    ops.transpose(x, t, rows_pad=rows_pad)
+    assert torch.equal(t[:, :rows], x.t())
+    assert torch.all(t[:, rows:] == 0)
+    cs = torch.zeros(cols, device=dev)
+    ws = torch.empty(ops.colsum_workspace(rows, cols), dtype=torch.uint8, device=dev)
+    ops.colsum(x, cs, ws, accumulate=False)
+    assert rel_err(cs, x.double().sum(0)) < 1e-5
