@@ -514,6 +514,116 @@ __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void bwd2_kernel(icap_attn_a
   }
 }
 
+// Forward v2: K and V of the head staged row-major in LDS (16-byte copies); one wave per 16-query tile.
+// S^T = K Q^T puts the keys of a query in the accumulator ROWS (lane = query), so the masked softmax reduces
+// over registers plus the 4 lane groups, and P^T (bf16, dropout applied) is the B operand of O^T = V^T P^T
+// directly, with V^T read transposed (ds_read_b64_tr_b16) from the row-major image. Fully masked causal key
+// tiles are skipped. Output rows come out 4 head dims per lane (8-byte stores).
+template <int HD>
+__global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint32_t thr, float inv_keep) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
+  constexpr int LDR = HD + 8;
+  constexpr int NKS = HD / 32;
+  constexpr int NDT = HD / 16;
+  constexpr int CPR = HD / 8;
+  const int Sp = g.Sp32, S = g.S;
+  const int bh = blockIdx.x;
+  const int b = bh / g.H, h = bh - b * g.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  bf16_t* Ks = sm;
+  bf16_t* Vs = Ks + Sp * LDR;
+  const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
+  for (int idx = threadIdx.x; idx < Sp * CPR; idx += blockDim.x) {
+    const int r = idx / CPR, c = idx - r * CPR;
+    uint4 k = make_uint4(0, 0, 0, 0), v = k;
+    if (r < S) {
+      const bf16_t* src = qkv + trow(g, b, r) * p.ld_qkv + g.D + h * HD + 8 * c;
+      k = *reinterpret_cast<const uint4*>(src);
+      v = *reinterpret_cast<const uint4*>(src + g.D);
+    }
+    *reinterpret_cast<uint4*>(Ks + r * LDR + 8 * c) = k;
+    *reinterpret_cast<uint4*>(Vs + r * LDR + 8 * c) = v;
+  }
+  __syncthreads();
+  const int qt = wave;
+  const int q = qt * 16 + fr;
+  // Q fragments of this query tile straight from HBM/L2 (B operand: rows = queries)
+  uint4 qf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) qf[ks] = gfrag(qkv, p.ld_qkv, h * HD, g, b, qt * 16, ks * 32, lane);
+  const int npair = Sp >> 5;
+  const int kp1 = p.causal ? ((qt * 16 + 15) >> 5) + 1 : npair;
+  const int np = kp1 < npair ? kp1 : npair;
+  f32x4_t st[MAXKT];  // up to 8 key tiles of 16
+#pragma unroll
+  for (int t = 0; t < MAXKT; ++t) st[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < MAXKT; ++t) {
+    if (t < 2 * np) {
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) st[t] = mfma(rowfrag<LDR>(Ks, t * 16, ks * 32, lane), qf[ks], st[t]);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int key = t * 16 + 4 * fg + v;
+        const float x = key_ok(p.causal, p.key_mask, g, b, q, key) ? st[t][v] * p.scale : -INFINITY;
+        st[t][v] = x;
+        m = fmaxf(m, x);
+      }
+    }
+  }
+  // row max / sum over the 4 lane groups that share this query
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int t = 0; t < MAXKT; ++t) {
+    if (t < 2 * np) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float e = (m == -INFINITY) ? 0.f : __expf(st[t][v] - m);
+        st[t][v] = e;
+        l += e;
+      }
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  if (fg == 0 && q < S && p.lse) p.lse[(int64_t)bh * S + q] = l > 0.f ? m + logf(l) : -INFINITY;
+  const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
+  const uint64_t dbase = p.offset + (uint64_t)bh * S * S;
+  f32x4_t o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kp = 0; kp < MAXKT / 2; ++kp) {
+    if (kp < np) {
+      float pv[8];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int key = (2 * kp + sub) * 16 + 4 * fg + v;
+          float x = st[2 * kp + sub][v] * inv;
+          if (thr && q < S && key < S) x *= drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
+          pv[sub * 4 + v] = x;
+        }
+      uint4 xp;
+      xp.x = f2bf2(pv[0], pv[1]); xp.y = f2bf2(pv[2], pv[3]); xp.z = f2bf2(pv[4], pv[5]); xp.w = f2bf2(pv[6], pv[7]);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) o[dt] = mfma(trfrag<LDR>(Vs, kp * 32, dt * 16, lane), xp, o[dt]);
+    }
+  }
+  if (q < S) {
+    bf16_t* rowp = reinterpret_cast<bf16_t*>(p.out) + trow(g, b, q) * p.ld_out + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+      *reinterpret_cast<uint2*>(rowp + dt * 16 + 4 * fg) = make_uint2(f2bf2(o[dt][0], o[dt][1]), f2bf2(o[dt][2], o[dt][3]));
+  }
+}
+
 }  // namespace amfma
 
 static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
@@ -529,6 +639,15 @@ amfma::Geo mfma_geo(const icap_attn_args* a) {
 size_t mfma_fwd_lds(const amfma::Geo& g) { return 2 * ((size_t)g.hd * g.ldT + 4 * 16 * (size_t)g.ldT); }
 size_t mfma_bwd_lds(const amfma::Geo& g) {
   return 2 * (3 * (size_t)g.hd * g.ldT + 2 * (size_t)g.Sp16 * g.ldT + 4 * 16 * (size_t)g.ldT);
+}
+
+size_t mfma_fwd2_lds(const amfma::Geo& g) { return 2 * 2 * (size_t)g.Sp32 * (g.hd + 8); }
+
+static bool mfma_fwd2_ok(const icap_attn_args* a) {
+  if ((a->ld_out & 3) || (a->ld_qkv & 7)) return false;
+  if ((reinterpret_cast<uintptr_t>(a->out) & 7) || (reinterpret_cast<uintptr_t>(a->qkv) & 15)) return false;
+  const amfma::Geo g = mfma_geo(a);
+  return (g.Sp16 / 16) * 64 <= 512;
 }
 
 size_t mfma_bwd2_lds(const amfma::Geo& g) {
@@ -562,6 +681,18 @@ static void lds_limit(K kernel) {
 int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float inv_keep, hipStream_t s) {
   const amfma::Geo g = mfma_geo(a);
   dim3 grid((unsigned)(a->B * a->H)), block(256);
+  if (!bwd && mfma_fwd2_ok(a)) {
+    const size_t lds2 = mfma_fwd2_lds(g);
+    const dim3 block2((unsigned)(64 * (g.Sp16 / 16)));
+    if (a->hd == 64) {
+      static bool once = (lds_limit(amfma::fwd2_kernel<64>), true); (void)once;
+      hipLaunchKernelGGL(amfma::fwd2_kernel<64>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+    } else {
+      static bool once = (lds_limit(amfma::fwd2_kernel<96>), true); (void)once;
+      hipLaunchKernelGGL(amfma::fwd2_kernel<96>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+    }
+    return check_launch("icap_attention_fwd(mfma v2)");
+  }
   if (!bwd) {
     const size_t lds = mfma_fwd_lds(g);
     if (a->hd == 64) {

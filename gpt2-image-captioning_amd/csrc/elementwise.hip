@@ -380,12 +380,25 @@ __global__ __launch_bounds__(256) void colsum4_kernel(int64_t M, int64_t N, cons
   }
 }
 
-__global__ void colsum_reduce_kernel(int64_t N, int nchunks, const float* __restrict__ partial, float* out, int acc) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
+// 64 columns per block, 16 waves over the chunk partials in a fixed order (deterministic)
+__global__ __launch_bounds__(1024) void colsum_reduce_kernel(int64_t N, int nchunks, const float* __restrict__ partial,
+                                                            float* out, int acc) {
+  __shared__ float red[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + tx;
   float a = 0.f;
-  for (int i = 0; i < nchunks; ++i) a += partial[(int64_t)i * N + c];
-  out[c] = acc ? out[c] + a : a;
+  if (c < N) {
+#pragma unroll 4
+    for (int i = ty; i < nchunks; i += 16) a += partial[(int64_t)i * N + c];
+  }
+  red[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && c < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][tx];
+    out[c] = acc ? out[c] + s : s;
+  }
 }
 
 template <typename TS, typename TD>
@@ -724,7 +737,7 @@ extern "C" int icap_colsum(int32_t dtype, int64_t M, int64_t N, const void* src,
   }
   int rc = check_launch("icap_colsum");
   if (rc) return rc;
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, S_(stream), N, (int)ch,
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, S_(stream), N, (int)ch,
                      partial, out, accumulate);
   return check_launch("icap_colsum(reduce)");
 }

@@ -35,9 +35,7 @@ namespace icap {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int GBM = 128, GBN = 128, GROWB = 128, GNT = 256;
-constexpr int STAGE_BYTES = (GBM + GBN) * GROWB;  // 32 KiB
-constexpr int EPI_LD = 68;                         // fp32 row stride of the epilogue staging tile
+constexpr int GBM = 128, GBN = 128, GROWB = 128, GNT = 256;  // default 128x128 tile, 128-byte LDS rows
 constexpr uint32_t OOB = 0x80000000u;              // buffer offset beyond any num_records -> loads 0
 
 __device__ __forceinline__ int lds_off(int row, int chunk) {
@@ -64,6 +62,12 @@ __device__ __forceinline__ void mfma_chunk<float>(f32x4_t& acc, const uint4& a, 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
   const uint32_t n = bytes > 0x7fffffffull ? 0x7fffffffu : (uint32_t)bytes;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
+}
+
+// 16-byte LDS-DMA of one wave: lane l's 16 bytes land at lds + 16 l
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(lds), 16, off, 0, 0, 0);
 }
 
 __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
@@ -147,17 +151,25 @@ __device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64
   }
 }
 
-// NST: LDS stages (2 = double-buffered, DMA of stage k+1 overlaps the MFMAs of stage k; 1 = single buffer, two
-// barriers per K step, latency hidden by MINB co-resident blocks per CU).
-// DIRECT: MFMA operand roles swapped (acc = C^T fragments), so each lane owns 4 consecutive output COLUMNS of one
-// row and the epilogue is applied straight from the accumulators with 8/16-byte vector accesses; otherwise the
-// accumulators are re-laid out through LDS (needs NST == 2 for the staging space).
-template <typename TI, typename TC, int NST, int MINB, bool DIRECT>
-__global__ __launch_bounds__(GNT, MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits, int nk_split,
-                                                        uint32_t drop_thresh, float inv_keep) {
-  // LDS-staged epilogue: rows per staging pass (per wave EPR x EPI_LD fp32 must fit the stage buffers)
-  constexpr int EPR = NST == 2 ? 32 : 16;
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_BYTES];
+// Block geometry: WM x WN waves, each owning a (16 TM) x (16 TN) sub-tile of MFMA 16x16 accumulators, so the
+// block tile is BM = 16 WM TM by BN = 16 WN TN. One pipeline stage holds 128 bytes of K per row (bf16: 64 K,
+// f32: 32 K) for the BM rows of A and the BN rows of B in LDS.
+// NST: LDS stages (2 = double-buffered: the LDS-DMA of stage k+1 overlaps the MFMAs of stage k; 1 = single
+// buffer, two barriers per K step, latency hidden by MINB co-resident blocks per CU).
+// Configurations in use: 128x128 / 4 waves (NST 1 or 2) and 256x256 / 8 waves (NST 2, 128 KiB, 1 block per CU:
+// 4x the MFMA work per staged byte and per exposed load latency).
+template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
+                                                                  int nk_split, uint32_t drop_thresh, float inv_keep) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
+  constexpr int STB = (BM + BN) * GROWB;    // bytes per stage
+  constexpr int EPR = NST == 2 ? 32 : 16;   // rows per LDS-staged epilogue pass
+  constexpr int ELD = 16 * TN + 4;          // fp32 row stride of the epilogue staging tile
+  static_assert(NW * EPR * ELD * 4 <= NST * STB, "epilogue staging must fit the stage buffers");
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "each wave stages whole 8-row DMA pieces");
+  constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW);  // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[NST * STB];
   constexpr int ES = sizeof(TI);
   constexpr int EPC = 16 / ES;         // elements per 16-byte chunk
   constexpr int BKE = GROWB / ES;      // K elements per stage
@@ -165,7 +177,7 @@ __global__ __launch_bounds__(GNT, MINB) void gemm_kernel(icap_gemm_args p, int t
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave - wm * WN;
 
   // bijective XCD-aware remap: blocks sharing an XCD get consecutive tiles
   // (consecutive tiles share the A row panel).
@@ -176,50 +188,42 @@ __global__ __launch_bounds__(GNT, MINB) void gemm_kernel(icap_gemm_args p, int t
   const int tiles = (int)(gridDim.x / splits);
   const int split = wgid / tiles, tile = wgid - split * tiles;
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-  const int64_t m0 = (int64_t)tm * GBM, n0 = (int64_t)tn * GBN;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
   const int64_t M = p.M, N = p.N, K = p.K;
   // tile-relative buffer descriptors: rows past M / N fall beyond num_records and load zeros
   const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
   const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
-  const int64_t mrows = M - m0 < GBM ? M - m0 : GBM;
-  const int64_t nrows = N - n0 < GBN ? N - n0 : GBN;
+  const int64_t mrows = M - m0 < BM ? M - m0 : BM;
+  const int64_t nrows = N - n0 < BN ? N - n0 : BN;
   const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
   const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
   // LDS-DMA staging (buffer_load_dwordx4 ... lds): one wave-instruction writes 1 KiB = 8 LDS rows of
   // 128 B linearly (lane l -> row l>>3, physical chunk l&7). The XOR swizzle therefore goes on the SOURCE:
   // physical chunk pc of row r holds logical K-chunk pc ^ (r & 7) (cdna_hip_programming.md §5.4 rule 21).
-  // Wave w stages rows [32w, 32w+32) of A and of B: 4 + 4 instructions per stage, no VGPR round trip.
   const int lrow = lane >> 3;
   const int lchunk = ((lane & 7) ^ lrow) * EPC;  // logical K offset (elements) of this lane's 16 B
-  uint32_t a_off[4], b_off[4];
+  uint32_t a_off[APW], b_off[BPW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = wave * 32 + i * 8 + lrow;
-    a_off[i] = (uint32_t)((row * p.lda + lchunk) * ES);
-    b_off[i] = (uint32_t)((row * p.ldb + lchunk) * ES);
-  }
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  for (int i = 0; i < APW; ++i) a_off[i] = (uint32_t)(((wave * APW + i) * 8 + lrow) * p.lda + lchunk) * ES;
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) b_off[i] = (uint32_t)(((wave * BPW + i) * 8 + lrow) * p.ldb + lchunk) * ES;
   auto load_stage = [&](int64_t k0, int s) {
     const uint32_t kb = (uint32_t)(k0 * ES);
     const bool kin = k0 + lchunk < K;
-    char* As = smem + s * STAGE_BYTES;
-    char* Bs = As + GBM * GROWB;
+    char* As = smem + s * STB;
+    char* Bs = As + BM * GROWB;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r0 = wave * 32 + i * 8;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_rsrc, (lds_ptr_t)(As + r0 * GROWB), 16, kin ? a_off[i] + kb : OOB,
-                                               0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb_rsrc, (lds_ptr_t)(Bs + r0 * GROWB), 16, kin ? b_off[i] + kb : OOB,
-                                               0, 0, 0);
-    }
+    for (int i = 0; i < APW; ++i) dma16(ra_rsrc, As + (wave * APW + i) * 8 * GROWB, kin ? a_off[i] + kb : OOB);
+#pragma unroll
+    for (int i = 0; i < BPW; ++i) dma16(rb_rsrc, Bs + (wave * BPW + i) * 8 * GROWB, kin ? b_off[i] + kb : OOB);
   };
 
-  f32x4_t acc[4][4];
+  f32x4_t acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   const int nk_all = (int)((K + BKE - 1) / BKE);
   const int kt0 = split * nk_split;
@@ -227,27 +231,26 @@ __global__ __launch_bounds__(GNT, MINB) void gemm_kernel(icap_gemm_args p, int t
   const int64_t kbase = (int64_t)kt0 * BKE;
   const int fr = lane & 15, fg = lane >> 4;
 
-  auto read_frags = [&](const char* As, uint4 (&af)[2][4], uint4 (&bfr)[2][4]) {
-    const char* Bs = As + GBM * GROWB;
+  auto read_frags = [&](const char* As, uint4 (&af)[2][TM], uint4 (&bfr)[2][TN]) {
+    const char* Bs = As + BM * GROWB;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + fg;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[ks][i] = *reinterpret_cast<const uint4*>(As + lds_off(wm * 64 + i * 16 + fr, ch));
+      for (int i = 0; i < TM; ++i)
+        af[ks][i] = *reinterpret_cast<const uint4*>(As + lds_off(wm * 16 * TM + i * 16 + fr, ch));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[ks][j] = *reinterpret_cast<const uint4*>(Bs + lds_off(wn * 64 + j * 16 + fr, ch));
+      for (int j = 0; j < TN; ++j)
+        bfr[ks][j] = *reinterpret_cast<const uint4*>(Bs + lds_off(wn * 16 * TN + j * 16 + fr, ch));
     }
   };
-  auto mfmas = [&](const uint4 (&af)[2][4], const uint4 (&bfr)[2][4]) {
+  auto mfmas = [&](const uint4 (&af)[2][TM], const uint4 (&bfr)[2][TN]) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (DIRECT) mfma_chunk<TI>(acc[i][j], bfr[ks][j], af[ks][i]);  // C^T fragment: lane = row, regs = 4 cols
-          else mfma_chunk<TI>(acc[i][j], af[ks][i], bfr[ks][j]);         // C fragment: lane = col, regs = 4 rows
-        }
+        for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[i][j], af[ks][i], bfr[ks][j]);  // lane = col, regs = 4 rows
   };
 
   if (NST == 2) {
@@ -258,8 +261,8 @@ __global__ __launch_bounds__(GNT, MINB) void gemm_kernel(icap_gemm_args p, int t
       const int cur = kt & 1;
       // all fragment reads of this stage first: hipcc waits vmcnt(0) before any LDS read that follows an
       // LDS-DMA issue, so the next stage's DMA is issued only after the reads (and overlaps the MFMAs)
-      uint4 af[2][4], bfr[2][4];
-      read_frags(smem + cur * STAGE_BYTES, af, bfr);
+      uint4 af[2][TM], bfr[2][TN];
+      read_frags(smem + cur * STB, af, bfr);
       // the other buffer was last read in iteration kt-1, which every wave finished before the barrier below
       if (kt + 1 < nk) load_stage(kbase + (int64_t)(kt + 1) * BKE, cur ^ 1);
       mfmas(af, bfr);
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(GNT, MINB) void gemm_kernel(icap_gemm_args p, int t
       load_stage(kbase + (int64_t)kt * BKE, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      uint4 af[2][4], bfr[2][4];
+      uint4 af[2][TM], bfr[2][TN];
       read_frags(smem, af, bfr);
       mfmas(af, bfr);
     }
@@ -286,35 +289,13 @@ __global__ __launch_bounds__(GNT, MINB) void gemm_kernel(icap_gemm_args p, int t
   // split-K partial slab of this split: raw fp32 [M, N] (N % 4 == 0 is guaranteed by the host)
   float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
 
-  if (DIRECT) {
-    // ---- epilogue straight from the accumulators: lane owns row m0+wm*64+16i+fr, cols n0+wn*64+16j+4fg..+3
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t col = n0 + wn * 64 + j * 16 + 4 * fg;
-      const bool full4 = col + 4 <= N;
-      float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t row = m0 + wm * 64 + i * 16 + fr;
-        if (row < M && col < N) {
-          float x[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-          if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = make_float4(x[0], x[1], x[2], x[3]);
-          else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
-        }
-      }
-    }
-    return;
-  }
-
-  // ---- LDS-staged epilogue (4 columns per lane) ----
-  float* cs = reinterpret_cast<float*>(smem) + wave * (EPR * EPI_LD);
-  const int er = lane >> 4;         // row within a 4-row group
-  const int ec = (lane & 15) * 4;   // first of this lane's 4 columns in the 64-column wave tile
-  const int64_t col = n0 + wn * 64 + ec;
+  // ---- LDS-staged epilogue: each wave re-reads its accumulators 4 consecutive columns per lane ----
+  float* cs = reinterpret_cast<float*>(smem) + wave * (EPR * ELD);
+  constexpr int LPR = 4 * TN;       // lanes per staged row (4 columns each)
+  constexpr int RPI = 64 / LPR;     // rows per wave instruction
+  const int er = lane / LPR;
+  const int ec = (lane - er * LPR) * 4;
+  const int64_t col = n0 + wn * 16 * TN + ec;
   const bool full4 = col + 4 <= N;
   float bias4[4] = {0.f, 0.f, 0.f, 0.f};
   if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
@@ -323,22 +304,336 @@ __global__ __launch_bounds__(GNT, MINB) void gemm_kernel(icap_gemm_args p, int t
   }
   if (NST == 1) __syncthreads();  // the single stage buffer is still being read by other waves
 #pragma unroll
-  for (int h = 0; h < 64 / EPR; ++h) {
-    // stage rows [EPR h, EPR h + EPR) of this wave's 64x64 accumulator tile
+  for (int h = 0; h < 16 * TM / EPR; ++h) {
+    // stage rows [EPR h, EPR h + EPR) of this wave's accumulator tile
 #pragma unroll
     for (int ii = 0; ii < EPR / 16; ++ii)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int v = 0; v < 4; ++v)
-          cs[(ii * 16 + fg * 4 + v) * EPI_LD + j * 16 + fr] = acc[(EPR / 16) * h + ii][j][v];
+          cs[(ii * 16 + fg * 4 + v) * ELD + j * 16 + fr] = acc[(EPR / 16) * h + ii][j][v];
     __syncthreads();
 #pragma unroll 2
-    for (int t = 0; t < EPR / 4; ++t) {
-      const int lr = t * 4 + er;  // 0..EPR-1
-      const int64_t row = m0 + wm * 64 + h * EPR + lr;
+    for (int t = 0; t < EPR / RPI; ++t) {
+      const int lr = t * RPI + er;  // 0..EPR-1
+      const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
       float x[4];
-      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * EPI_LD + ec);
+      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
+      if (row < M && col < N) {
+        if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
+        else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Double-buffered variant with the two stages in two distinct __shared__ objects and the K loop unrolled by two,
+// so each stage's buffer is a compile-time object: hipcc's LDS-DMA alias tracking then lets the fragment reads of
+// one buffer run while the DMA into the other is in flight (with one array it waits vmcnt(0) before every read
+// after a DMA issue). Fragment reads are issued in MFMA-group order (k half 0: rows of A in two halves, then
+// k half 1), so the LDS reads of the next group overlap the MFMAs of the current one.
+template <typename TI, typename TC, int MINB, int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm2b_kernel(icap_gemm_args p, int tiles_n, int splits,
+                                                                    int nk_split, uint32_t drop_thresh,
+                                                                    float inv_keep) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
+  constexpr int STB = (BM + BN) * GROWB;    // bytes per stage
+  constexpr int EPR = 16;                   // rows per LDS-staged epilogue pass
+  constexpr int ELD = 16 * TN + 4;          // fp32 row stride of the epilogue staging tile
+  static_assert(NW * EPR * ELD * 4 <= STB, "epilogue staging must fit one stage buffer");
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "each wave stages whole 8-row DMA pieces");
+  static_assert(TM % 2 == 0, "A fragments are read in two halves");
+  constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW);  // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem0[STB];
+  __shared__ __attribute__((aligned(16))) char smem1[STB];
+  constexpr int ES = sizeof(TI);
+  constexpr int EPC = 16 / ES;
+  constexpr int BKE = GROWB / ES;
+  constexpr int HM = TM / 2;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles = (int)(gridDim.x / splits);
+  const int split = wgid / tiles, tile = wgid - split * tiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t M = p.M, N = p.N, K = p.K;
+  const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
+  const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
+  const int64_t mrows = M - m0 < BM ? M - m0 : BM;
+  const int64_t nrows = N - n0 < BN ? N - n0 : BN;
+  const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
+  const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
+  const int lrow = lane >> 3;
+  const int lchunk = ((lane & 7) ^ lrow) * EPC;
+  uint32_t a_off[APW], b_off[BPW];
+#pragma unroll
+  for (int i = 0; i < APW; ++i) a_off[i] = (uint32_t)(((wave * APW + i) * 8 + lrow) * p.lda + lchunk) * ES;
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) b_off[i] = (uint32_t)(((wave * BPW + i) * 8 + lrow) * p.ldb + lchunk) * ES;
+  auto load_stage = [&](int64_t k0, char* As) {
+    const uint32_t kb = (uint32_t)(k0 * ES);
+    const bool kin = k0 + lchunk < K;
+    char* Bs = As + BM * GROWB;
+#pragma unroll
+    for (int i = 0; i < APW; ++i) dma16(ra_rsrc, As + (wave * APW + i) * 8 * GROWB, kin ? a_off[i] + kb : OOB);
+#pragma unroll
+    for (int i = 0; i < BPW; ++i) dma16(rb_rsrc, Bs + (wave * BPW + i) * 8 * GROWB, kin ? b_off[i] + kb : OOB);
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nk_all = (int)((K + BKE - 1) / BKE);
+  const int kt0 = split * nk_split;
+  const int nk = (nk_all - kt0 < nk_split ? nk_all - kt0 : nk_split);
+  const int64_t kbase = (int64_t)kt0 * BKE;
+  const int fr = lane & 15, fg = lane >> 4;
+  auto rdA = [&](const char* As, int i, int ks) {
+    return *reinterpret_cast<const uint4*>(As + lds_off(wm * 16 * TM + i * 16 + fr, ks * 4 + fg));
+  };
+  auto rdB = [&](const char* As, int j, int ks) {
+    return *reinterpret_cast<const uint4*>(As + BM * GROWB + lds_off(wn * 16 * TN + j * 16 + fr, ks * 4 + fg));
+  };
+  // one K stage from `cur` while the next one streams into `nxt`
+  auto step = [&](const char* cur, char* nxt, int kt) {
+    uint4 b[TN], a0[HM], a1[HM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b[j] = rdB(cur, j, 0);
+#pragma unroll
+    for (int i = 0; i < HM; ++i) a0[i] = rdA(cur, i, 0);
+    if (kt + 1 < nk) load_stage(kbase + (int64_t)(kt + 1) * BKE, nxt);
+#pragma unroll
+    for (int i = 0; i < HM; ++i) a1[i] = rdA(cur, HM + i, 0);
+#pragma unroll
+    for (int i = 0; i < HM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[i][j], a0[i], b[j]);
+#pragma unroll
+    for (int i = 0; i < HM; ++i) a0[i] = rdA(cur, i, 1);
+#pragma unroll
+    for (int i = 0; i < HM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[HM + i][j], a1[i], b[j]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b[j] = rdB(cur, j, 1);
+#pragma unroll
+    for (int i = 0; i < HM; ++i) a1[i] = rdA(cur, HM + i, 1);
+#pragma unroll
+    for (int i = 0; i < HM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[i][j], a0[i], b[j]);
+#pragma unroll
+    for (int i = 0; i < HM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[HM + i][j], a1[i], b[j]);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into nxt has landed
+    __syncthreads();                                      // ... every wave's, and cur is free again
+  };
+
+  load_stage(kbase, smem0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(smem0, smem1, kt);
+    if (kt + 1 < nk) step(smem1, smem0, kt + 1);
+  }
+
+  uint64_t seed = 0;
+  if (splits == 1 && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
+  float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
+  float* cs = reinterpret_cast<float*>(smem0) + wave * (EPR * ELD);
+  constexpr int LPR = 4 * TN;
+  constexpr int RPI = 64 / LPR;
+  const int er = lane / LPR;
+  const int ec = (lane - er * LPR) * 4;
+  const int64_t col = n0 + wn * 16 * TN + ec;
+  const bool full4 = col + 4 <= N;
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < 16 * TM / EPR; ++h) {
+#pragma unroll
+    for (int ii = 0; ii < EPR / 16; ++ii)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          cs[(ii * 16 + fg * 4 + v) * ELD + j * 16 + fr] = acc[(EPR / 16) * h + ii][j][v];
+    __syncthreads();
+#pragma unroll 2
+    for (int t = 0; t < EPR / RPI; ++t) {
+      const int lr = t * RPI + er;
+      const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
+      float x[4];
+      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
+      if (row < M && col < N) {
+        if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
+        else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Three-stage ring: stages k+1 and k+2 stream in (LDS-DMA) while stage k is consumed, so a load has two stage
+// computes to land (PMC: the two-stage kernels leave MFMA busy at ~44 %, parked on the DMA of the next stage).
+// Three distinct __shared__ buffers with the K loop unrolled by three keep every buffer a compile-time object
+// (no hipcc vmcnt(0) before the fragment reads); the stage hand-off is a counted vmcnt (the newest stage may stay
+// in flight) plus a raw s_barrier (a __syncthreads() would drain every DMA: cdna_hip_programming.md "Pipelining
+// across barriers").
+template <typename TI, typename TC, int MINB, int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm3b_kernel(icap_gemm_args p, int tiles_n, int splits,
+                                                                    int nk_split, uint32_t drop_thresh,
+                                                                    float inv_keep) {
+  constexpr int NW = WM * WN;
+  constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
+  constexpr int STB = (BM + BN) * GROWB;
+  constexpr int EPR = 16;
+  constexpr int ELD = 16 * TN + 4;
+  static_assert(NW * EPR * ELD * 4 <= STB, "epilogue staging must fit one stage buffer");
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "each wave stages whole 8-row DMA pieces");
+  constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW);
+  constexpr int DPS = APW + BPW;  // DMA instructions per wave per stage (the vmcnt unit)
+  __shared__ __attribute__((aligned(16))) char smem0[STB];
+  __shared__ __attribute__((aligned(16))) char smem1[STB];
+  __shared__ __attribute__((aligned(16))) char smem2[STB];
+  constexpr int ES = sizeof(TI);
+  constexpr int EPC = 16 / ES;
+  constexpr int BKE = GROWB / ES;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave - wm * WN;
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles = (int)(gridDim.x / splits);
+  const int split = wgid / tiles, tile = wgid - split * tiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t M = p.M, N = p.N, K = p.K;
+  const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
+  const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
+  const int64_t mrows = M - m0 < BM ? M - m0 : BM;
+  const int64_t nrows = N - n0 < BN ? N - n0 : BN;
+  const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
+  const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
+  const int lrow = lane >> 3;
+  const int lchunk = ((lane & 7) ^ lrow) * EPC;
+  uint32_t a_off[APW], b_off[BPW];
+#pragma unroll
+  for (int i = 0; i < APW; ++i) a_off[i] = (uint32_t)(((wave * APW + i) * 8 + lrow) * p.lda + lchunk) * ES;
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) b_off[i] = (uint32_t)(((wave * BPW + i) * 8 + lrow) * p.ldb + lchunk) * ES;
+  const int nk_all = (int)((K + BKE - 1) / BKE);
+  const int kt0 = split * nk_split;
+  const int nk = (nk_all - kt0 < nk_split ? nk_all - kt0 : nk_split);
+  const int64_t kbase = (int64_t)kt0 * BKE;
+  // stage kt -> buffer; stages past nk issue nothing
+  auto load_stage = [&](int kt, char* As) {
+    if (kt >= nk) return;
+    const int64_t k0 = kbase + (int64_t)kt * BKE;
+    const uint32_t kb = (uint32_t)(k0 * ES);
+    const bool kin = k0 + lchunk < K;
+    char* Bs = As + BM * GROWB;
+#pragma unroll
+    for (int i = 0; i < APW; ++i) dma16(ra_rsrc, As + (wave * APW + i) * 8 * GROWB, kin ? a_off[i] + kb : OOB);
+#pragma unroll
+    for (int i = 0; i < BPW; ++i) dma16(rb_rsrc, Bs + (wave * BPW + i) * 8 * GROWB, kin ? b_off[i] + kb : OOB);
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  auto step = [&](const char* cur, char* nxt2, int kt) {
+    uint4 af[2][TM], bfr[2][TN];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[ks][i] = *reinterpret_cast<const uint4*>(cur + lds_off(wm * 16 * TM + i * 16 + fr, ks * 4 + fg));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[ks][j] =
+            *reinterpret_cast<const uint4*>(cur + BM * GROWB + lds_off(wn * 16 * TN + j * 16 + fr, ks * 4 + fg));
+    }
+    load_stage(kt + 2, nxt2);  // into the buffer every wave finished reading one barrier ago
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[i][j], af[ks][i], bfr[ks][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    // stage kt+1 must have landed; stage kt+2 (issued above) may stay in flight
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  load_stage(0, smem0);
+  load_stage(1, smem1);
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; kt += 3) {
+    step(smem0, smem2, kt);
+    if (kt + 1 >= nk) break;
+    step(smem1, smem0, kt + 1);
+    if (kt + 2 >= nk) break;
+    step(smem2, smem1, kt + 2);
+  }
+
+  uint64_t seed = 0;
+  if (splits == 1 && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
+  float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
+  float* cs = reinterpret_cast<float*>(smem0) + wave * (EPR * ELD);
+  constexpr int LPR = 4 * TN;
+  constexpr int RPI = 64 / LPR;
+  const int er = lane / LPR;
+  const int ec = (lane - er * LPR) * 4;
+  const int64_t col = n0 + wn * 16 * TN + ec;
+  const bool full4 = col + 4 <= N;
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < 16 * TM / EPR; ++h) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) cs[(fg * 4 + v) * ELD + j * 16 + fr] = acc[h][j][v];
+    __syncthreads();
+#pragma unroll 2
+    for (int t = 0; t < EPR / RPI; ++t) {
+      const int lr = t * RPI + er;
+      const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
+      float x[4];
+      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
       if (row < M && col < N) {
         if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
         else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
@@ -575,17 +870,29 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     return check_launch("icap_gemm(skinny)");
   }
   dim3 grid((unsigned)(tiles * splits)), block(GNT);
-  const int sp = (int)splits, nks = (int)nk_split, tn = (int)tiles_n;
+  const int sp = (int)splits, nks = (int)nk_split;
+  int tn = (int)tiles_n;
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
   const int variant = gemm_variant(p, nk_split);
-#define ICAP_GEMM_LAUNCH(TI, TC)                                                                              \
-  switch (variant) {                                                                                          \
-    case 0: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 2, false>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 1: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 2, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break;  \
-    case 2: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 3, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break;  \
-    case 3: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 4: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 3, false>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    default: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 4, false>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+  // the grid was sized for 128x128 tiles above
+  if (variant == 6 || variant == 8) {  // 256x256
+    const int64_t tm2 = (p.M + 255) / 256, tn2 = (p.N + 255) / 256;
+    grid = dim3((unsigned)(tm2 * tn2 * splits));
+    tn = (int)tn2;
+  } else if (variant == 9) {  // 256x128
+    const int64_t tm2 = (p.M + 255) / 256;
+    grid = dim3((unsigned)(tm2 * tiles_n * splits));
+  }
+#define ICAP_GEMM_LAUNCH(TI, TC)                                                                               \
+  switch (variant) {                                                                                           \
+    case 0: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 4: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 3, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 5: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 4, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 6: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 1, 2, 4, 8, 4>), grid, dim3(512), 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 7: hipLaunchKernelGGL((gemm2b_kernel<TI, TC, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 8: hipLaunchKernelGGL((gemm2b_kernel<TI, TC, 1, 2, 4, 8, 4>), grid, dim3(512), 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 9: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 4, 2, 4, 4>), grid, dim3(512), 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    default: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
   }
   if (p.in_dtype == ICAP_BF16) {
     if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(bf16_t, bf16_t) } else { ICAP_GEMM_LAUNCH(bf16_t, float) }

@@ -89,30 +89,45 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t rows, int D, const 
 #pragma unroll
     for (int e = 0; e < 4; ++e) dg[t][e] = db[t][e] = 0.f;
 
-  for (int64_t r = (int64_t)blockIdx.x * 4 + wv; r < rows; r += nw) {
+  // rows are processed with the NEXT row's x / dy / dres already in flight (each wave owns ~rows/nw rows,
+  // so without the prefetch every row pays a full memory latency before its two reductions)
+  float xv[LN_MAXV][4], dv[LN_MAXV][4], rv[LN_MAXV][4];
+  auto load_row = [&](int64_t r) {
+#pragma unroll
+    for (int t = 0; t < LN_MAXV; ++t) {
+      const int g = lane + 64 * t;
+      if (g < D4) {
+        io<T>::ld4(x + r * ldx + 4 * g, xv[t]);
+        io<T>::ld4(dy + r * lddy + 4 * g, dv[t]);
+        if (dres) io<T>::ld4(dres + r * lddres + 4 * g, rv[t]);
+      }
+    }
+  };
+  int64_t r = (int64_t)blockIdx.x * 4 + wv;
+  if (r < rows) load_row(r);
+  for (; r < rows; r += nw) {
     const float mean = mean_in[r], rs = rstd_in[r];
-    float xh[LN_MAXV][4], gy[LN_MAXV][4];
+    float xh[LN_MAXV][4], gy[LN_MAXV][4], dres4[LN_MAXV][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int t = 0; t < LN_MAXV; ++t) {
       const int g = lane + 64 * t;
       if (g < D4) {
-        float xv[4], dv[4];
-        io<T>::ld4(x + r * ldx + 4 * g, xv);
-        io<T>::ld4(dy + r * lddy + 4 * g, dv);
         const float4 gm = *reinterpret_cast<const float4*>(gamma + 4 * g);
         const float gmv[4] = {gm.x, gm.y, gm.z, gm.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          xh[t][e] = (xv[e] - mean) * rs;
-          gy[t][e] = dv[e] * gmv[e];
+          xh[t][e] = (xv[t][e] - mean) * rs;
+          gy[t][e] = dv[t][e] * gmv[e];
           s1 += gy[t][e];
           s2 += gy[t][e] * xh[t][e];
-          dg[t][e] += dv[e] * xh[t][e];
-          db[t][e] += dv[e];
+          dg[t][e] += dv[t][e] * xh[t][e];
+          db[t][e] += dv[t][e];
+          dres4[t][e] = dres ? rv[t][e] : 0.f;
         }
       }
     }
+    if (r + nw < rows) load_row(r + nw);
     const float m1 = wave_sum(s1) * invD;
     const float m2 = wave_sum(s2) * invD;
 #pragma unroll
@@ -121,13 +136,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t rows, int D, const 
       if (g < D4) {
         float o[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = rs * (gy[t][e] - m1 - xh[t][e] * m2);
-        if (dres) {
-          float rv[4];
-          io<T>::ld4(dres + r * lddres + 4 * g, rv);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] += rv[e];
-        }
+        for (int e = 0; e < 4; ++e) o[e] = rs * (gy[t][e] - m1 - xh[t][e] * m2) + dres4[t][e];
         io<T>::st4(dx + r * lddx + 4 * g, o);
         if (dx_drop) {
           const uint64_t base = offset + (uint64_t)(r * D + 4 * g);
@@ -160,20 +169,25 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t rows, int D, const 
   }
 }
 
-// grid (ceil(D/64), 2): blockIdx.y selects dgamma / dbeta; 4 waves split the partial rows, 64 lanes = 64 columns
-__global__ __launch_bounds__(256) void ln_param_reduce(int nblk, int D, const float* __restrict__ partial,
-                                                      float* dgamma, float* dbeta) {
-  __shared__ float red[4][64];
+// grid (ceil(D/64), 2): blockIdx.y selects dgamma / dbeta; 16 waves split the partial rows (fixed order, so the
+// result is deterministic), 64 lanes = 64 columns
+__global__ __launch_bounds__(1024) void ln_param_reduce(int nblk, int D, const float* __restrict__ partial,
+                                                       float* dgamma, float* dbeta) {
+  __shared__ float red[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   const int which = blockIdx.y;
   float a = 0.f;
-  if (c < D)
-    for (int i = ty; i < nblk; i += 4) a += partial[(int64_t)i * 2 * D + which * D + c];
+  if (c < D) {
+#pragma unroll 4
+    for (int i = ty; i < nblk; i += 16) a += partial[(int64_t)i * 2 * D + which * D + c];
+  }
   red[ty][tx] = a;
   __syncthreads();
   if (ty == 0 && c < D) {
-    const float s = red[0][tx] + red[1][tx] + red[2][tx] + red[3][tx];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][tx];
     float* dst = which ? dbeta : dgamma;
     if (dst) dst[c] += s;
   }
@@ -240,7 +254,7 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
                        lddx, (float*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial);
   int rc = check_launch("icap_layernorm_bwd");
   if (rc != ICAP_OK || !want_params) return rc;
-  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 63) / 64), 2), dim3(256), 0, s, nb, (int)D, partial,
+  hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 63) / 64), 2), dim3(1024), 0, s, nb, (int)D, partial,
                      dgamma, dbeta);
   return check_launch("icap_layernorm_bwd(reduce)");
 }
