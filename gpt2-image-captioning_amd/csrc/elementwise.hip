@@ -65,25 +65,58 @@ __global__ void embed_scatter_kernel(int B, int P, int L, int D, const T* __rest
   }
 }
 
-__global__ void caption_prep_kernel(int B, int P, int L, const int64_t* __restrict__ mask,
-                                    const int64_t* __restrict__ labels, int32_t* key_mask, int32_t* lab_shift,
-                                    int32_t* n_valid) {
-  __shared__ float red[4];
-  const int S = P + L;
-  float cnt = 0.f;
-  for (int i = threadIdx.x; i < B * S; i += blockDim.x) {
+// One 1024-thread block; thread k owns the contiguous rows [k*per, (k+1)*per) so the target compaction is an
+// exclusive scan of per-thread counts (wave shuffles + one LDS pass) and keeps row order.
+__global__ __launch_bounds__(1024) void caption_prep_kernel(int B, int P, int L, const int64_t* __restrict__ mask,
+                                                           const int64_t* __restrict__ labels, int32_t* key_mask,
+                                                           int32_t* lab_shift, int32_t* n_valid, int32_t* row_slot,
+                                                           int32_t* lab_c) {
+  __shared__ int wsum[16];
+  const int S = P + L, n = B * S;
+  const int per = (n + 1023) / 1024;
+  const int i0 = threadIdx.x * per;
+  const int i1 = i0 + per < n ? i0 + per : n;
+  auto label_at = [&](int i) {
+    const int b = i / S, tn = i - b * S + 1;
+    return (tn < S && tn >= P && labels) ? (int)labels[(int64_t)b * L + tn - P] : -100;
+  };
+  int cnt = 0;
+  for (int i = i0; i < i1; ++i) {
     const int b = i / S, t = i - b * S;
     if (key_mask) key_mask[i] = (t < P || mask == nullptr) ? 1 : (mask[(int64_t)b * L + t - P] != 0 ? 1 : 0);
-    if (lab_shift) {
-      int lab = -100;
-      const int tn = t + 1;
-      if (tn < S && tn >= P && labels) lab = (int)labels[(int64_t)b * L + tn - P];
-      lab_shift[i] = lab;
-      cnt += (lab != -100) ? 1.f : 0.f;
+    const int lab = label_at(i);
+    if (lab_shift) lab_shift[i] = lab;
+    cnt += lab != -100 ? 1 : 0;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int woff = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    woff += k < w ? wsum[k] : 0;
+    tot += wsum[k];
+  }
+  if (row_slot) {
+    int slot = woff + incl - cnt;
+    for (int i = i0; i < i1; ++i) {
+      const int lab = label_at(i);
+      if (lab != -100) {
+        row_slot[i] = slot;
+        if (lab_c) lab_c[slot] = lab;
+        ++slot;
+      } else {
+        row_slot[i] = -1;
+      }
     }
   }
-  const float tot = block_sum256(cnt, red);
-  if (threadIdx.x == 0 && n_valid) *n_valid = (int32_t)(tot + 0.5f);
+  if (threadIdx.x == 0 && n_valid) *n_valid = tot;
 }
 
 // ---------------------------------------------------------------- cross entropy
@@ -91,9 +124,10 @@ template <typename T>
 __global__ __launch_bounds__(256) void ce_kernel(int64_t V, const T* __restrict__ logits, int64_t ld,
                                                 const int32_t* __restrict__ labels,
                                                 const int32_t* __restrict__ n_valid, float* __restrict__ loss_rows,
-                                                T* dlogits, float grad_scale) {
+                                                T* dlogits, float grad_scale, const int32_t* __restrict__ rows_dev) {
   __shared__ float redm[4], reds[4];
   const int64_t r = blockIdx.x;
+  if (rows_dev && r >= *rows_dev) return;  // compacted targets: this row does not exist
   const int y = labels[r];
   const T* x = logits + r * ld;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -155,8 +189,9 @@ __global__ __launch_bounds__(256) void ce_kernel(int64_t V, const T* __restrict_
 }
 
 __global__ void ce_reduce_kernel(int64_t rows, const float* __restrict__ loss_rows, const int32_t* n_valid,
-                                 float* loss) {
+                                 float* loss, const int32_t* __restrict__ rows_dev) {
   __shared__ double red[256];
+  if (rows_dev && *rows_dev < rows) rows = *rows_dev;
   double a = 0.0;
   for (int64_t i = threadIdx.x; i < rows; i += 256) a += (double)loss_rows[i];
   red[threadIdx.x] = a;
@@ -611,10 +646,13 @@ extern "C" int icap_gpt2_embed(int32_t dtype, int32_t B, int32_t P, int32_t L, i
 }
 
 extern "C" int icap_caption_prep(int32_t B, int32_t P, int32_t L, const int64_t* mask, const int64_t* labels,
-                                 int32_t* key_mask, int32_t* labels_shift, int32_t* n_valid, void* stream) {
+                                 int32_t* key_mask, int32_t* labels_shift, int32_t* n_valid, int32_t* row_slot,
+                                 int32_t* labels_compact, void* stream) {
   ICAP_REQUIRE(B >= 0 && P >= 0 && L >= 0, "icap_caption_prep: bad geometry");
-  hipLaunchKernelGGL(caption_prep_kernel, dim3(1), dim3(256), 0, S_(stream), B, P, L, mask, labels, key_mask,
-                     labels_shift, n_valid);
+  ICAP_REQUIRE((int64_t)B * (P + L) < (1ll << 30), "icap_caption_prep: too many rows");
+  ICAP_REQUIRE((row_slot == nullptr) == (labels_compact == nullptr), "icap_caption_prep: row_slot and labels_compact go together");
+  hipLaunchKernelGGL(caption_prep_kernel, dim3(1), dim3(1024), 0, S_(stream), B, P, L, mask, labels, key_mask,
+                     labels_shift, n_valid, row_slot, labels_compact);
   return check_launch("icap_caption_prep");
 }
 
@@ -624,17 +662,17 @@ extern "C" size_t icap_cross_entropy_workspace_bytes(int64_t rows) {
 
 extern "C" int icap_cross_entropy(int32_t dtype, int64_t rows, int64_t V, const void* logits, int64_t ld,
                                   const int32_t* labels, const int32_t* n_valid, float* loss, void* dlogits,
-                                  float grad_scale, void* workspace, void* stream) {
+                                  float grad_scale, void* workspace, const int32_t* rows_dev, void* stream) {
   ICAP_REQUIRE(logits && labels && n_valid && loss && workspace, "icap_cross_entropy: null pointer");
   ICAP_REQUIRE(V > 0 && ld >= V && ld % 4 == 0, "icap_cross_entropy: ld must be >= V and a multiple of 4");
   if (rows <= 0) return ICAP_OK;
   ICAP_REQUIRE(rows < (1ll << 31), "icap_cross_entropy: too many rows");
   float* lrows = reinterpret_cast<float*>(workspace);
   DISPATCH_T(dtype, hipLaunchKernelGGL(ce_kernel<T>, dim3((unsigned)rows), dim3(256), 0, S_(stream), V, CTP(logits),
-                                       ld, labels, n_valid, lrows, TP(dlogits), grad_scale));
+                                       ld, labels, n_valid, lrows, TP(dlogits), grad_scale, rows_dev));
   int rc = check_launch("icap_cross_entropy");
   if (rc) return rc;
-  hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(256), 0, S_(stream), rows, lrows, n_valid, loss);
+  hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(256), 0, S_(stream), rows, lrows, n_valid, loss, rows_dev);
   return check_launch("icap_cross_entropy(reduce)");
 }
 

@@ -187,14 +187,19 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   // split-K: split-major order, so the blocks of one split (same K range) sit together on an XCD
   const int tiles = (int)(gridDim.x / splits);
   const int split = wgid / tiles, tile = wgid - split * tiles;
-  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  // row tiles fastest when the row count is device-side: the live tiles (low rows) then spread over every XCD
+  const int tiles_m = tiles / tiles_n;
+  const int tm = p.m_dev ? tile % tiles_m : tile / tiles_n;
+  const int tn = p.m_dev ? tile / tiles_m : tile - tm * tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
   const int64_t M = p.M, N = p.N, K = p.K;
+  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;  // device row count
+  if (m0 >= Mv) return;
   // tile-relative buffer descriptors: rows past M / N fall beyond num_records and load zeros
   const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
   const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
-  const int64_t mrows = M - m0 < BM ? M - m0 : BM;
+  const int64_t mrows = Mv - m0 < BM ? Mv - m0 : BM;
   const int64_t nrows = N - n0 < BN ? N - n0 : BN;
   const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
   const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
@@ -320,7 +325,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
       float x[4];
       *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
-      if (row < M && col < N) {
+      if (row < Mv && col < N) {
         if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
         else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
       }
@@ -363,12 +368,17 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm2b_kernel(icap_gemm_ar
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int tiles = (int)(gridDim.x / splits);
   const int split = wgid / tiles, tile = wgid - split * tiles;
-  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  // row tiles fastest when the row count is device-side: the live tiles (low rows) then spread over every XCD
+  const int tiles_m = tiles / tiles_n;
+  const int tm = p.m_dev ? tile % tiles_m : tile / tiles_n;
+  const int tn = p.m_dev ? tile / tiles_m : tile - tm * tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t M = p.M, N = p.N, K = p.K;
+  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;  // device row count
+  if (m0 >= Mv) return;
   const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
   const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
-  const int64_t mrows = M - m0 < BM ? M - m0 : BM;
+  const int64_t mrows = Mv - m0 < BM ? Mv - m0 : BM;
   const int64_t nrows = N - n0 < BN ? N - n0 : BN;
   const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
   const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
@@ -482,7 +492,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm2b_kernel(icap_gemm_ar
       const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
       float x[4];
       *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
-      if (row < M && col < N) {
+      if (row < Mv && col < N) {
         if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
         else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
       }
@@ -526,12 +536,17 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm3b_kernel(icap_gemm_ar
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int tiles = (int)(gridDim.x / splits);
   const int split = wgid / tiles, tile = wgid - split * tiles;
-  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  // row tiles fastest when the row count is device-side: the live tiles (low rows) then spread over every XCD
+  const int tiles_m = tiles / tiles_n;
+  const int tm = p.m_dev ? tile % tiles_m : tile / tiles_n;
+  const int tn = p.m_dev ? tile / tiles_m : tile - tm * tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t M = p.M, N = p.N, K = p.K;
+  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;  // device row count
+  if (m0 >= Mv) return;
   const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
   const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
-  const int64_t mrows = M - m0 < BM ? M - m0 : BM;
+  const int64_t mrows = Mv - m0 < BM ? Mv - m0 : BM;
   const int64_t nrows = N - n0 < BN ? N - n0 : BN;
   const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
   const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
@@ -634,7 +649,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm3b_kernel(icap_gemm_ar
       const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
       float x[4];
       *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
-      if (row < M && col < N) {
+      if (row < Mv && col < N) {
         if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
         else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
       }
@@ -665,8 +680,10 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   __shared__ __attribute__((aligned(16))) float red[HALF][BM * RLD];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int64_t M = p.M, N = p.N, K = p.K;
+  const int64_t N = p.N, K = p.K;
   const int64_t n0 = (int64_t)blockIdx.x * BN, m0 = (int64_t)blockIdx.y * BM;
+  const int64_t M = p.m_dev && (int64_t)*p.m_dev < p.M ? (int64_t)*p.m_dev : p.M;  // device row count
+  if (m0 >= M) return;
   const int64_t nrows = N - n0 < BN ? N - n0 : BN;
   const int64_t mrows = M - m0 < BM ? M - m0 : BM;
   const __amdgpu_buffer_rsrc_t ra =
@@ -762,6 +779,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(icap_gemm_args p, int 
   const int64_t n4 = N >> 2;
   if (q >= M * n4) return;
   const int64_t row = q / n4, col = (q - row * n4) * 4;
+  if (p.m_dev && row >= (int64_t)*p.m_dev) return;
   const float* ws = reinterpret_cast<const float*>(p.workspace) + row * N + col;
   float x[4];
   *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(ws);
@@ -802,11 +820,21 @@ static int gemm_variant(const icap_gemm_args& p, int64_t nk_per_block) {
   return heavy ? 5 : 4;
 }
 
-extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
-  ICAP_REQUIRE(a != nullptr, "icap_gemm: null args");
-  const icap_gemm_args& p = *a;
+namespace {
+// What icap_gemm launches for one call (shared by the launcher and icap_gemm_kernel_name).
+struct GemmPlan {
+  bool skinny = false;
+  int nt = 1;            // skinny: 16-column slabs per block
+  int variant = 0;       // tile kernel (see ICAP_GEMM_LAUNCH)
+  int splits = 1, nk_split = 0, tiles_n = 0;
+  dim3 grid, block;
+  uint32_t thr = 0;
+  float inv_keep = 1.f;
+};
+}  // namespace
+
+static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
-  if (p.M == 0 || p.N == 0) return ICAP_OK;
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16, "icap_gemm: bad in_dtype");
   ICAP_REQUIRE(p.c_dtype == ICAP_F32 || p.c_dtype == ICAP_BF16, "icap_gemm: bad c_dtype");
@@ -817,8 +845,8 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   ICAP_REQUIRE((reinterpret_cast<uintptr_t>(p.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.B) & 15) == 0,
                "icap_gemm: A and B must be 16-byte aligned");
   const int es = p.in_dtype == ICAP_BF16 ? 2 : 4;
-  ICAP_REQUIRE((int64_t)GBM * p.lda * es < 0x7fffffffll && (int64_t)GBN * p.ldb * es < 0x7fffffffll,
-               "icap_gemm: a 128-row operand panel must stay below 2 GiB");
+  ICAP_REQUIRE((int64_t)256 * p.lda * es < 0x7fffffffll && (int64_t)256 * p.ldb * es < 0x7fffffffll,
+               "icap_gemm: a 256-row operand panel must stay below 2 GiB");
   ICAP_REQUIRE(p.beta == 0.f || p.c_dtype == ICAP_F32, "icap_gemm: beta != 0 requires f32 C");
   ICAP_REQUIRE(p.dact == ICAP_ACT_NONE || p.dact_src != nullptr, "icap_gemm: dact requires dact_src");
   ICAP_REQUIRE(p.drop_p >= 0.f && p.drop_p < 1.f, "icap_gemm: drop_p out of range");
@@ -826,6 +854,15 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const int64_t tiles = tiles_m * tiles_n;
   ICAP_REQUIRE(tiles < (1ll << 26), "icap_gemm: too many tiles");
   ICAP_REQUIRE(p.split_k >= 0, "icap_gemm: split_k must be >= 0");
+  pl.thr = p.drop_p > 0.f ? drop_threshold(p.drop_p) : 0u;
+  pl.inv_keep = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
+  if (p.M <= 128 && p.split_k == 0 && tiles <= 128 && gemm_variant_override() < 0) {
+    pl.skinny = true;
+    pl.nt = p.N > 1536 ? 2 : 1;  // 32-column slabs once there are enough of them
+    pl.grid = dim3((unsigned)((p.N + 16 * pl.nt - 1) / (16 * pl.nt)), (unsigned)((p.M + 31) / 32));
+    pl.block = dim3(64 * SK_WAVES);
+    return ICAP_OK;
+  }
   // split-K over K stages for launches that cannot fill the chip (decode-time M = batch, small projections):
   // fp32 partial slabs in the caller's workspace + one deterministic reduce/epilogue pass.
   const int64_t bke = 128 / es;
@@ -852,14 +889,69 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
                      p.workspace_bytes >= splits * slab,
                  "icap_gemm: split-K workspace missing, misaligned or too small");
   }
-  const uint32_t thr = p.drop_p > 0.f ? drop_threshold(p.drop_p) : 0u;
-  const float inv_keep = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
+  pl.splits = (int)splits;
+  pl.nk_split = (int)nk_split;
+  pl.variant = gemm_variant(p, nk_split);
+  pl.tiles_n = (int)tiles_n;
+  pl.block = dim3(GNT);
+  pl.grid = dim3((unsigned)(tiles * splits));
+  if (pl.variant == 6 || pl.variant == 8) {  // 256x256
+    const int64_t tm2 = (p.M + 255) / 256, tn2 = (p.N + 255) / 256;
+    pl.grid = dim3((unsigned)(tm2 * tn2 * splits));
+    pl.tiles_n = (int)tn2;
+    pl.block = dim3(512);
+  } else if (pl.variant == 9) {  // 256x128
+    const int64_t tm2 = (p.M + 255) / 256;
+    pl.grid = dim3((unsigned)(tm2 * tiles_n * splits));
+    pl.block = dim3(512);
+  }
+  return ICAP_OK;
+}
+
+// "TI, TC, template ints" of each variant (keep in sync with ICAP_GEMM_LAUNCH)
+static const char* variant_kernel(int v) {
+  switch (v) {
+    case 0: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4>";
+    case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4>";
+    case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4>";
+    case 6: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 8, 4>";
+    case 7: return "gemm2b_kernel<%s, %s, 2, 2, 2, 4, 4>";
+    case 8: return "gemm2b_kernel<%s, %s, 1, 2, 4, 8, 4>";
+    case 9: return "gemm3b_kernel<%s, %s, 1, 4, 2, 4, 4>";
+    default: return "gemm3b_kernel<%s, %s, 1, 2, 2, 4, 4>";
+  }
+}
+
+extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
+  static thread_local char buf[160];
+  if (a == nullptr) return nullptr;
+  GemmPlan pl;
+  if (gemm_plan(*a, pl) != ICAP_OK) return nullptr;
+  const char* ti = a->in_dtype == ICAP_BF16 ? "unsigned short" : "float";
+  const char* tc = a->c_dtype == ICAP_BF16 ? "unsigned short" : "float";
+  char fmt[96];
+  if (pl.skinny) snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2>", pl.nt);
+  else snprintf(fmt, sizeof fmt, "%s", variant_kernel(pl.variant));
+  char inner[128];
+  snprintf(inner, sizeof inner, fmt, ti, tc);
+  snprintf(buf, sizeof buf, "icap::%s", inner);
+  return buf;
+}
+
+extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
+  ICAP_REQUIRE(a != nullptr, "icap_gemm: null args");
+  const icap_gemm_args& p = *a;
+  if (p.M == 0 || p.N == 0) return ICAP_OK;
+  GemmPlan pl;
+  const int prc = gemm_plan(p, pl);
+  if (prc != ICAP_OK) return prc;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (p.M <= 128 && p.split_k == 0 && tiles <= 128 && gemm_variant_override() < 0) {
-    const int nt = p.N > 1536 ? 2 : 1;  // 32-column slabs once there are enough of them
-    const dim3 sgrid((unsigned)((p.N + 16 * nt - 1) / (16 * nt)), (unsigned)((p.M + 31) / 32)), sblock(64 * SK_WAVES);
+  const uint32_t thr = pl.thr;
+  const float inv_keep = pl.inv_keep;
+  if (pl.skinny) {
+    const dim3 sgrid = pl.grid, sblock = pl.block;
 #define ICAP_SKINNY(TI, TC)                                                                                   \
-  if (nt == 2) hipLaunchKernelGGL((gemm_skinny_kernel<TI, TC, 2, 2>), sgrid, sblock, 0, s, p, thr, inv_keep);   \
+  if (pl.nt == 2) hipLaunchKernelGGL((gemm_skinny_kernel<TI, TC, 2, 2>), sgrid, sblock, 0, s, p, thr, inv_keep); \
   else hipLaunchKernelGGL((gemm_skinny_kernel<TI, TC, 1, 2>), sgrid, sblock, 0, s, p, thr, inv_keep);
     if (p.in_dtype == ICAP_BF16) {
       if (p.c_dtype == ICAP_BF16) { ICAP_SKINNY(bf16_t, bf16_t) } else { ICAP_SKINNY(bf16_t, float) }
@@ -869,29 +961,18 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
 #undef ICAP_SKINNY
     return check_launch("icap_gemm(skinny)");
   }
-  dim3 grid((unsigned)(tiles * splits)), block(GNT);
-  const int sp = (int)splits, nks = (int)nk_split;
-  int tn = (int)tiles_n;
+  const dim3 grid = pl.grid, block = pl.block;
+  const int sp = pl.splits, nks = pl.nk_split, tn = pl.tiles_n;
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
-  const int variant = gemm_variant(p, nk_split);
-  // the grid was sized for 128x128 tiles above
-  if (variant == 6 || variant == 8) {  // 256x256
-    const int64_t tm2 = (p.M + 255) / 256, tn2 = (p.N + 255) / 256;
-    grid = dim3((unsigned)(tm2 * tn2 * splits));
-    tn = (int)tn2;
-  } else if (variant == 9) {  // 256x128
-    const int64_t tm2 = (p.M + 255) / 256;
-    grid = dim3((unsigned)(tm2 * tiles_n * splits));
-  }
 #define ICAP_GEMM_LAUNCH(TI, TC)                                                                               \
-  switch (variant) {                                                                                           \
+  switch (pl.variant) {                                                                                        \
     case 0: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
     case 4: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 3, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
     case 5: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 4, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 6: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 1, 2, 4, 8, 4>), grid, dim3(512), 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 6: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 1, 2, 4, 8, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
     case 7: hipLaunchKernelGGL((gemm2b_kernel<TI, TC, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 8: hipLaunchKernelGGL((gemm2b_kernel<TI, TC, 1, 2, 4, 8, 4>), grid, dim3(512), 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 9: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 4, 2, 4, 4>), grid, dim3(512), 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 8: hipLaunchKernelGGL((gemm2b_kernel<TI, TC, 1, 2, 4, 8, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    case 9: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 4, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
     default: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
   }
   if (p.in_dtype == ICAP_BF16) {
@@ -900,7 +981,7 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(float, bf16_t) } else { ICAP_GEMM_LAUNCH(float, float) }
   }
 #undef ICAP_GEMM_LAUNCH
-  if (splits > 1) {
+  if (sp > 1) {
     if (p.c_dtype == ICAP_BF16)
       hipLaunchKernelGGL((gemm_splitk_reduce<bf16_t>), rgrid, dim3(256), 0, s, p, sp, thr, inv_keep);
     else

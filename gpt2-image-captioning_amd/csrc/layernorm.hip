@@ -13,7 +13,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t rows, int D, const 
                                                     const float* __restrict__ gamma,
                                                     const float* __restrict__ beta, float eps,
                                                     T* __restrict__ y, int64_t ldy, float* mean_out,
-                                                    float* rstd_out) {
+                                                    float* rstd_out, const int32_t* __restrict__ y_rowmap) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   const int D4 = D >> 2;
@@ -44,10 +44,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t rows, int D, const 
     }
     const float var = wave_sum(s2) * invD;
     const float rs = 1.f / sqrtf(var + eps);
+    const int64_t yr = y_rowmap ? (int64_t)y_rowmap[r] : r;
 #pragma unroll
     for (int t = 0; t < LN_MAXV; ++t) {
       const int g = lane + 64 * t;
-      if (g < D4) {
+      if (g < D4 && yr >= 0) {
         const float4 gm = *reinterpret_cast<const float4*>(gamma + 4 * g);
         const float4 bt = *reinterpret_cast<const float4*>(beta + 4 * g);
         float o[4];
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t rows, int D, const 
         o[1] = (v[t][1] - mean) * rs * gm.y + bt.y;
         o[2] = (v[t][2] - mean) * rs * gm.z + bt.z;
         o[3] = (v[t][3] - mean) * rs * gm.w + bt.w;
-        io<T>::st4(y + r * ldy + 4 * g, o);
+        io<T>::st4(y + yr * ldy + 4 * g, o);
       }
     }
     if (lane == 0) {
@@ -75,7 +76,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t rows, int D, const 
                                                     T* __restrict__ dx, int64_t lddx, T* __restrict__ dx_drop,
                                                     uint32_t thr, float inv_keep, uint64_t seed0,
                                                     const uint64_t* seed_ptr, uint64_t offset,
-                                                    float* __restrict__ partial) {
+                                                    float* __restrict__ partial,
+                                                    const int32_t* __restrict__ dy_rowmap) {
   __shared__ float red[4][2][LN_MAXV * 256];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -93,12 +95,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t rows, int D, const 
   // so without the prefetch every row pays a full memory latency before its two reductions)
   float xv[LN_MAXV][4], dv[LN_MAXV][4], rv[LN_MAXV][4];
   auto load_row = [&](int64_t r) {
+    const int64_t dyr = dy_rowmap ? (int64_t)dy_rowmap[r] : r;
 #pragma unroll
     for (int t = 0; t < LN_MAXV; ++t) {
       const int g = lane + 64 * t;
       if (g < D4) {
         io<T>::ld4(x + r * ldx + 4 * g, xv[t]);
-        io<T>::ld4(dy + r * lddy + 4 * g, dv[t]);
+        if (dyr >= 0) io<T>::ld4(dy + dyr * lddy + 4 * g, dv[t]);
+        else dv[t][0] = dv[t][1] = dv[t][2] = dv[t][3] = 0.f;
         if (dres) io<T>::ld4(dres + r * lddres + 4 * g, rv[t]);
       }
     }
@@ -206,7 +210,7 @@ static int ln_blocks(int64_t rows, int cap) {
 
 extern "C" int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
                                   const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
-                                  float* mean, float* rstd, void* stream) {
+                                  float* mean, float* rstd, const int32_t* y_rowmap, void* stream) {
   ICAP_REQUIRE(D > 0 && D % 4 == 0 && D <= 4 * 64 * LN_MAXV, "icap_layernorm_fwd: D must be a multiple of 4, <= 1024");
   ICAP_REQUIRE(x && y && gamma && beta, "icap_layernorm_fwd: null pointer");
   ICAP_REQUIRE(ldx % 4 == 0 && ldy % 4 == 0, "icap_layernorm_fwd: strides must be multiples of 4");
@@ -215,10 +219,10 @@ extern "C" int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const 
   const int nb = ln_blocks(rows, 4096);
   if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, rows, (int)D,
-                       (const bf16_t*)x, ldx, gamma, beta, eps, (bf16_t*)y, ldy, mean, rstd);
+                       (const bf16_t*)x, ldx, gamma, beta, eps, (bf16_t*)y, ldy, mean, rstd, y_rowmap);
   else
     hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const float*)x,
-                       ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd);
+                       ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd, y_rowmap);
   return check_launch("icap_layernorm_fwd");
 }
 
@@ -231,7 +235,7 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
                                   const void* dy, int64_t lddy, const void* dres, int64_t lddres,
                                   void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
                                   uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
-                                  void* workspace, void* stream) {
+                                  void* workspace, const int32_t* dy_rowmap, void* stream) {
   ICAP_REQUIRE(D > 0 && D % 4 == 0 && D <= 4 * 64 * LN_MAXV, "icap_layernorm_bwd: D must be a multiple of 4, <= 1024");
   ICAP_REQUIRE(x && gamma && mean && rstd && dy && dx, "icap_layernorm_bwd: null pointer");
   ICAP_REQUIRE((dgamma == nullptr && dbeta == nullptr) || workspace != nullptr,
@@ -247,11 +251,11 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
   if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const bf16_t*)x, ldx,
                        gamma, mean, rstd, (const bf16_t*)dy, lddy, (const bf16_t*)dres, lddres, (bf16_t*)dx,
-                       lddx, (bf16_t*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial);
+                       lddx, (bf16_t*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial, dy_rowmap);
   else
     hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const float*)x, ldx,
                        gamma, mean, rstd, (const float*)dy, lddy, (const float*)dres, lddres, (float*)dx,
-                       lddx, (float*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial);
+                       lddx, (float*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial, dy_rowmap);
   int rc = check_launch("icap_layernorm_bwd");
   if (rc != ICAP_OK || !want_params) return rc;
   hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 63) / 64), 2), dim3(1024), 0, s, nb, (int)D, partial,

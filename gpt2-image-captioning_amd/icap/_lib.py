@@ -41,6 +41,7 @@ class GemmArgs(C.Structure):
         ("drop_p", f32), ("seed", u64), ("offset", u64),
         ("seed_ptr", vp),
         ("workspace", vp), ("workspace_bytes", i64), ("split_k", i32),
+        ("m_dev", vp),
     ]
 
 
@@ -80,18 +81,19 @@ SIGNATURES = {
     "icap_version": (C.c_int, []),
     "icap_device_arch_ok": (C.c_int, []),
     "icap_gemm": (C.c_int, [C.POINTER(GemmArgs), vp]),
-    "icap_layernorm_fwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, f32, vp, i64, vp, vp, vp]),
+    "icap_gemm_kernel_name": (C.c_char_p, [C.POINTER(GemmArgs)]),
+    "icap_layernorm_fwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, f32, vp, i64, vp, vp, vp, vp]),
     "icap_layernorm_bwd_workspace_bytes": (sz, [i64, i64]),
     "icap_layernorm_bwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, vp,
-                                     f32, u64, u64, vp, vp, vp, vp, vp]),
+                                     f32, u64, u64, vp, vp, vp, vp, vp, vp]),
     "icap_attention_fwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_bwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_decode": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, i64, f32, vp]),
     "icap_gpt2_embed": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, vp, f32, u64, u64, vp, vp]),
     "icap_embedding_scatter_add": (C.c_int, [i32, i32, i32, i32, i32, vp, vp, vp, vp]),
-    "icap_caption_prep": (C.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+    "icap_caption_prep": (C.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
     "icap_cross_entropy_workspace_bytes": (sz, [i64]),
-    "icap_cross_entropy": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, f32, vp, vp]),
+    "icap_cross_entropy": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, f32, vp, vp, vp]),
     "icap_adamw_workspace_bytes": (sz, [i64]),
     "icap_adamw_step": (C.c_int, [C.POINTER(AdamWArgs), vp, vp]),
     "icap_sqnorm": (C.c_int, [i64, vp, vp, vp, vp]),

@@ -25,7 +25,7 @@ class CaptionTrainer:
     def __init__(self, model, batch_size: int, caption_len: int, *, lr: float = 1e-4, weight_decay: float = 0.01,
                  betas=(0.9, 0.999), eps: float = 1e-8, max_norm: float = 1.0, num_warmup_steps: int = 0,
                  num_training_steps: int = 1, dropout: bool = True, seed: int = 0, clip_model=None,
-                 grad_accum_steps: int = 1, process_group=None):
+                 grad_accum_steps: int = 1, process_group=None, compact_head: bool = True):
         self.model = model
         self.dtype = model.compute_dtype
         self.B, self.Lc = batch_size, caption_len
@@ -52,7 +52,7 @@ class CaptionTrainer:
         P = model.total_prefix_length
         self.P = P
         self.mws = self.mcore.alloc(B, train=True)
-        self.gws = self.gcore.alloc_train(B, P, Lc)
+        self.gws = self.gcore.alloc_train(B, P, Lc, compact_head=compact_head)
         D = self.gcore.D
         M2 = self.mws.M
         E = self.mcore.E

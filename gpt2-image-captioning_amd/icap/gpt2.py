@@ -269,13 +269,21 @@ class GPT2Core:
         self.eps = self.cfg.layer_norm_epsilon
 
     # -- workspaces --------------------------------------------------------------------------------------
-    def alloc_train(self, B: int, P: int, Lc: int, keep_for_dw: bool = False) -> SimpleNamespace:
+    def alloc_train(self, B: int, P: int, Lc: int, keep_for_dw: bool = False,
+                    compact_head: bool = False) -> SimpleNamespace:
+        """compact_head: the LM head and CE run on the rows whose shifted label is not -100 only (at most B*Lc;
+        the count lives on the device). The loss ignores every other row (HF/loss/loss_utils.py:32-46,
+        ignore_index=-100), so their logits feed nothing and their dlogits are exactly 0: loss and gradients are
+        those of the full-width head. Needs labels; not with a trainable (tied) wte."""
         S = P + Lc
         M = B * S
         D, H, dt, dev = self.D, self.H, self.dtype, self.dev
         nl = self.cfg.n_layer
         e = lambda *shape, dtype=dt: torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
         ws = SimpleNamespace(B=B, P=P, Lc=Lc, S=S, M=M)
+        ws.compact = bool(compact_head and Lc > 0 and not keep_for_dw)
+        ws.Mh = B * Lc if ws.compact else M  # rows of the LM head / CE buffers
+        ws.head_rows_hint = None  # host-known number of target rows (roofline bookkeeping only)
         ws.x = [e(M, D) for _ in range(nl + 1)]
         ws.h1 = [e(M, D) for _ in range(nl)]
         ws.qkv = [e(M, 3 * D) for _ in range(nl)]
@@ -294,19 +302,22 @@ class GPT2Core:
         else:
             a, o, a2, f = e(M, D), e(M, D), e(M, D), e(M, 4 * D)
             ws.a1, ws.o, ws.a2, ws.f = [a] * nl, [o] * nl, [a2] * nl, [f] * nl
-        ws.hf = e(M, D)
-        ws.logits = e(M, self.Vp)
+        Mh = ws.Mh
+        ws.hf = e(Mh, D)
+        ws.logits = e(Mh, self.Vp)
         ws.key_mask = e(M, dtype=torch.int32)
         ws.labels_shift = e(M, dtype=torch.int32)
+        ws.row_slot = e(M, dtype=torch.int32) if ws.compact else None
+        ws.labels_c = e(Mh, dtype=torch.int32) if ws.compact else None
         ws.n_valid = e(1, dtype=torch.int32)
         ws.loss = e(1, dtype=torch.float32)
-        ws.ce_ws = e(ops.cross_entropy_workspace(M), dtype=torch.uint8)
+        ws.ce_ws = e(ops.cross_entropy_workspace(Mh), dtype=torch.uint8)
         # backward scratch
         ws.dx, ws.dx2, ws.dxd = e(M, D), e(M, D), e(M, D)
         ws.dff = e(M, 4 * D)
         ws.dqkv = e(M, 3 * D)
         ws.do, ws.da = e(M, D), e(M, D)
-        ws.dhf = e(M, D)
+        ws.dhf = e(Mh, D)
         return ws
 
     # -- dropout sites (distinct offsets so masks never coincide) -------------------------------------------
@@ -336,14 +347,22 @@ class GPT2Core:
         With fuse_dlogits the CE kernel also writes dlogits (in place over the logits, or into `dlogits`)."""
         B, P, Lc, S, M = ws.B, ws.P, ws.Lc, ws.S, ws.M
         D, H, hd = self.D, self.H, self.hd
-        ops.caption_prep(B, P, Lc, mask, labels, ws.key_mask, ws.labels_shift, ws.n_valid)
+        cp = ws.compact
+        if cp and labels is None:
+            raise L.IcapError("compact LM head needs labels")
+        ops.caption_prep(B, P, Lc, mask, labels, ws.key_mask, ws.labels_shift, ws.n_valid,
+                         ws.row_slot if cp else None, ws.labels_c if cp else None)
         ops.gpt2_embed(prefix, prefix_bstride, self.wte, self.wpe, ids, ws.x[0], B=B, P=P, L_=Lc, D=D, drop=dr.embd)
         self._blocks_fwd(ws, dr, B, S, M, causal_mask=ws.key_mask if mask is not None else None)
-        ops.layernorm_fwd(ws.x[-1], self.lnf_g, self.lnf_b, self.eps, ws.hf, ws.meanf, ws.rstdf)
-        ops.gemm(ws.hf, self.wte, ws.logits, alg_flops=2.0 * ws.M * self.V * self.D)
+        ops.layernorm_fwd(ws.x[-1], self.lnf_g, self.lnf_b, self.eps, ws.hf, ws.meanf, ws.rstdf,
+                          y_rowmap=ws.row_slot if cp else None)
+        rows = ws.head_rows_hint if (cp and ws.head_rows_hint is not None) else ws.Mh
+        ops.gemm(ws.hf, self.wte, ws.logits, M=ws.Mh, m_dev=ws.n_valid if cp else None,
+                 alg_flops=2.0 * rows * self.V * self.D)
         if labels is not None:
             dl = (dlogits if dlogits is not None else ws.logits) if fuse_dlogits else None
-            ops.cross_entropy(ws.logits, self.V, ws.labels_shift, ws.n_valid, ws.loss, dl, ws.ce_ws, grad_scale)
+            ops.cross_entropy(ws.logits, self.V, ws.labels_c if cp else ws.labels_shift, ws.n_valid, ws.loss, dl,
+                              ws.ce_ws, grad_scale, rows=ws.Mh, rows_dev=ws.n_valid if cp else None)
 
     def _blocks_fwd(self, ws, dr, B, S, M, causal_mask):
         D, H, hd = self.D, self.H, self.hd
@@ -367,12 +386,23 @@ class GPT2Core:
         D, H, hd = self.D, self.H, self.hd
         scale = 1.0 / math.sqrt(hd)
         nl = len(self.layers)
-        ops.gemm(dlogits, self.wte_t, ws.dhf, alg_flops=2.0 * M * D * self.V)  # dh_f = dlogits . wte (K padded)
+        cp = ws.compact
+        if cp and grads is not None:
+            raise L.IcapError("compact LM head: the tied wte gradient needs every row (alloc_train(keep_for_dw))")
+        rows = ws.head_rows_hint if (cp and ws.head_rows_hint is not None) else ws.Mh
+        # dh_f = dlogits . wte (K padded); compact: target rows only, scattered back by the ln_f backward
+        split = 0
+        if cp and rows > 128:  # long K (50304), few output tiles: split K so ~2 blocks/CU work on the live rows
+            tiles = -(-rows // 128) * -(-D // 128)
+            split = max(1, min(16, round(512 / max(tiles, 1))))
+        ops.gemm(dlogits, self.wte_t, ws.dhf, M=ws.Mh, m_dev=ws.n_valid if cp else None,
+                 alg_flops=2.0 * rows * D * self.V, split_k=split)
         if grads is not None:  # d(wte) from the tied LM head: dW[V,D] += dlogits^T . hf
             dw.dW(dlogits, ws.hf, grads.wte, M=M, N=self.V)
         ops.layernorm_bwd(ws.x[-1], self.lnf_g, ws.meanf, ws.rstdf, ws.dhf, ws.dx, dx_drop=ws.dxd,
                           drop=dr.rm(nl - 1), dgamma=grads.lnf_g if grads else None,
-                          dbeta=grads.lnf_b if grads else None, workspace=dw.ln_ws if dw else None)
+                          dbeta=grads.lnf_b if grads else None, workspace=dw.ln_ws if dw else None,
+                          dy_rowmap=ws.row_slot if cp else None)
         dres, dnew = ws.dx, ws.dx2
         for l in reversed(range(nl)):
             lw = self.layers[l]

@@ -69,10 +69,11 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          aux: Optional[Tensor] = None, dact: int = L.ACT_NONE, dact_src: Optional[Tensor] = None,
          resid: Optional[Tensor] = None, alpha: float = 1.0, beta: float = 0.0, drop: Dropout = NO_DROP,
          M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None,
-         alg_flops: Optional[float] = None, split_k: int = 0) -> Tensor:
+         alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
     alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).
-    split_k: 0 = automatic split-K for launches of <= 64 output tiles, 1 = never, > 1 = forced."""
+    split_k: 0 = automatic split-K for launches of <= 64 output tiles, 1 = never, > 1 = forced.
+    m_dev: device int32 row count <= M (rows past it are neither computed nor stored)."""
     M = A.shape[0] if M is None else M
     K = A.shape[1] if K is None else K
     N = B.shape[0] if N is None else N
@@ -98,18 +99,20 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     a.drop_p, a.seed, a.offset, a.seed_ptr = drop.p, drop.seed, drop.offset, drop.ptr
     ws = gemm_workspace(A.device)
     a.workspace, a.workspace_bytes, a.split_k = ws.data_ptr(), ws.numel() * 4, split_k
+    a.m_dev = _p(m_dev)
     if GEMM_TIMER is None:
         call("icap_gemm", C.byref(a), _stream())
     else:  # per-launch HIP-event timing (bench.py kernel roofline pass; never inside a captured graph)
-        key = ("bf16" if a.in_dtype == L.BF16 else "f32") + "->" + ("bf16" if a.c_dtype == L.BF16 else "f32")
-        key = (key, f"{M}x{N}x{K} act{act} dact{dact} drop{int(drop.p > 0)} res{int(resid is not None)} "
-                    f"aux{int(aux is not None)} beta{beta:g}")
+        name = L.load().icap_gemm_kernel_name(C.byref(a))  # the instantiation rocprofv3 will name
+        key = (name.decode() if name else "?",
+               f"{M}x{N}x{K} act{act} dact{dact} drop{int(drop.p > 0)} res{int(resid is not None)} "
+               f"aux{int(aux is not None)} beta{beta:g}{' m_dev' if m_dev is not None else ''}")
         GEMM_TIMER.launch(key, 2.0 * M * N * K if alg_flops is None else alg_flops,
                           lambda: call("icap_gemm", C.byref(a), _stream()))
     return out
 
 
-GEMM_WORKSPACE_BYTES = 64 << 20
+GEMM_WORKSPACE_BYTES = 192 << 20  # split-K slabs up to splits*M*N fp32 (LM-head dX: 6 x 6400 x 768)
 _gemm_ws = {}
 
 
@@ -128,11 +131,12 @@ GEMM_TIMER = None  # set to an object with .launch(key, flops, fn) to time every
 
 
 def layernorm_fwd(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, y: Tensor, mean: Optional[Tensor],
-                  rstd: Optional[Tensor], rows: Optional[int] = None) -> Tensor:
+                  rstd: Optional[Tensor], rows: Optional[int] = None, y_rowmap: Optional[Tensor] = None) -> Tensor:
+    """y_rowmap: int32 [rows]; row r goes to y row y_rowmap[r] (skipped when < 0)."""
     rows = _rows(x) if rows is None else rows
     D = gamma.shape[0]
     call("icap_layernorm_fwd", dtype_code(x.dtype), rows, D, x.data_ptr(), _ld(x), gamma.data_ptr(),
-         beta.data_ptr(), eps, y.data_ptr(), _ld(y), _p(mean), _p(rstd), _stream())
+         beta.data_ptr(), eps, y.data_ptr(), _ld(y), _p(mean), _p(rstd), _p(y_rowmap), _stream())
     return y
 
 
@@ -143,13 +147,15 @@ def layernorm_bwd_workspace(rows: int, D: int) -> int:
 def layernorm_bwd(x: Tensor, gamma: Tensor, mean: Tensor, rstd: Tensor, dy: Tensor, dx: Tensor, *,
                   dres: Optional[Tensor] = None, dx_drop: Optional[Tensor] = None, drop: Dropout = NO_DROP,
                   dgamma: Optional[Tensor] = None, dbeta: Optional[Tensor] = None,
-                  workspace: Optional[Tensor] = None, rows: Optional[int] = None) -> Tensor:
+                  workspace: Optional[Tensor] = None, rows: Optional[int] = None,
+                  dy_rowmap: Optional[Tensor] = None) -> Tensor:
+    """dy_rowmap: int32 [rows]; dy of row r is dy row dy_rowmap[r] (zero when < 0)."""
     rows = _rows(x) if rows is None else rows
     D = gamma.shape[0]
     call("icap_layernorm_bwd", dtype_code(x.dtype), rows, D, x.data_ptr(), _ld(x), gamma.data_ptr(),
          mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), _ld(dy), _p(dres), _ld(dres) if dres is not None else 0,
          dx.data_ptr(), _ld(dx), _p(dx_drop), drop.p, drop.seed, drop.offset, drop.ptr, _p(dgamma), _p(dbeta),
-         _p(workspace), _stream())
+         _p(workspace), _p(dy_rowmap), _stream())
     return dx
 
 
@@ -204,12 +210,14 @@ def gpt2_embed(prefix: Optional[Tensor], prefix_bstride: int, wte: Tensor, wpe: 
 
 
 def caption_prep(B: int, P: int, L_: int, mask: Optional[Tensor], labels: Optional[Tensor],
-                 key_mask: Optional[Tensor], labels_shift: Optional[Tensor], n_valid: Optional[Tensor]) -> None:
+                 key_mask: Optional[Tensor], labels_shift: Optional[Tensor], n_valid: Optional[Tensor],
+                 row_slot: Optional[Tensor] = None, labels_compact: Optional[Tensor] = None) -> None:
+    """row_slot/labels_compact: the target-row compaction (include/icap.h icap_caption_prep)."""
     for t in (mask, labels):
         if t is not None and t.dtype != torch.int64:
             raise L.IcapError("caption_prep: mask/labels must be int64")
     call("icap_caption_prep", B, P, L_, _p(mask), _p(labels), _p(key_mask), _p(labels_shift), _p(n_valid),
-         _stream())
+         _p(row_slot), _p(labels_compact), _stream())
 
 
 def cross_entropy_workspace(rows: int) -> int:
@@ -218,11 +226,12 @@ def cross_entropy_workspace(rows: int) -> int:
 
 def cross_entropy(logits: Tensor, V: int, labels: Tensor, n_valid: Tensor, loss: Tensor,
                   dlogits: Optional[Tensor], workspace: Tensor, grad_scale: float = 1.0,
-                  rows: Optional[int] = None) -> Tensor:
+                  rows: Optional[int] = None, rows_dev: Optional[Tensor] = None) -> Tensor:
+    """rows_dev: device int32 row count (compacted targets); rows past it are untouched."""
     rows = logits.shape[0] if rows is None else rows
     call("icap_cross_entropy", dtype_code(logits.dtype), rows, V, logits.data_ptr(), _ld(logits),
          labels.data_ptr(), n_valid.data_ptr(), loss.data_ptr(), _p(dlogits), grad_scale, workspace.data_ptr(),
-         _stream())
+         _p(rows_dev), _stream())
     return loss
 
 

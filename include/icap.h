@@ -89,7 +89,14 @@ typedef struct {
   /* and only when the workspace is given), 1 = never, > 1 = forced.            */
   /* The partial sums are reduced in a fixed order (deterministic).             */
   void* workspace; int64_t workspace_bytes; int32_t split_k;
+  /* optional device-side row count (int32, <= M): only rows < *m_dev are     */
+  /* computed and stored; the launch geometry stays sized for M, so a graph   */
+  /* captured once serves every count (LM head over the compacted targets).   */
+  const int32_t* m_dev;
 } icap_gemm_args;
+/* name of the kernel instantiation icap_gemm launches for these arguments    */
+/* (as rocprofv3 prints it, minus the parameter list); NULL on invalid args.   */
+const char* icap_gemm_kernel_name(const icap_gemm_args* a);
 int icap_gemm(const icap_gemm_args* a, void* stream);
 
 /* ------------------------------------------------------------------------- */
@@ -99,20 +106,24 @@ int icap_gemm(const icap_gemm_args* a, void* stream);
 /* y = (x-mean)*rstd*gamma + beta; mean/rstd (fp32 [rows]) saved for backward. */
 /* D % 4 == 0, D <= 1024.                                                      */
 /* ------------------------------------------------------------------------- */
+/* y_rowmap (optional int32 [rows]): row r is stored to y row y_rowmap[r], or  */
+/* not at all when it is < 0 (gathers the LM-head target rows).                */
 int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
                        const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
-                       float* mean, float* rstd, void* stream);
+                       float* mean, float* rstd, const int32_t* y_rowmap, void* stream);
 /* dx = LN'(x)^T dy [+ dres];  optional dx_drop = dx * dropmask(p,seed,offset)  */
 /* (the residual-dropout backward of the producing layer, fused);             */
 /* optional dgamma/dbeta (+= into fp32 [D]) via a caller workspace of          */
 /* icap_layernorm_bwd_workspace_bytes(rows, D) bytes.                           */
+/* dy_rowmap (optional int32 [rows]): dy of row r is dy row dy_rowmap[r], or 0 */
+/* when it is < 0 (scatters the LM-head target-row gradient back).             */
 size_t icap_layernorm_bwd_workspace_bytes(int64_t rows, int64_t D);
 int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
                        const float* gamma, const float* mean, const float* rstd,
                        const void* dy, int64_t lddy, const void* dres, int64_t lddres,
                        void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
                        uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
-                       void* workspace, void* stream);
+                       void* workspace, const int32_t* dy_rowmap, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Multi-head softmax attention over a fused QKV activation.                  */
@@ -168,9 +179,14 @@ int icap_gpt2_embed(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D,
 /* dwte[ids[b,t]] += dx[b*(P+L) + P + t]  (fp32 atomics)                                    */
 int icap_embedding_scatter_add(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D,
                                const void* dx, const int64_t* ids, float* dwte, void* stream);
+/* Target compaction (optional, both or neither): row_slot[b*S+t] = index of  */
+/* row (b,t) among the rows whose shifted label != -100 (row order), else -1;  */
+/* labels_compact[row_slot[i]] = labels_shift[i]. Only those n_valid rows       */
+/* reach the loss (loss_utils.py:32-46 ignore_index=-100), so the LM head and  */
+/* CE run on them alone; everything they feed back is identical.              */
 int icap_caption_prep(int32_t B, int32_t P, int32_t L, const int64_t* mask,
                       const int64_t* labels, int32_t* key_mask, int32_t* labels_shift,
-                      int32_t* n_valid, void* stream);
+                      int32_t* n_valid, int32_t* row_slot, int32_t* labels_compact, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Causal-LM cross entropy fused with its backward (HF/loss/loss_utils.py     */
@@ -179,11 +195,14 @@ int icap_caption_prep(int32_t B, int32_t P, int32_t L, const int64_t* mask,
 /*   dlogits_r = grad_scale*(softmax(x_r) - onehot(y))/n_valid (0 for ignored  */
 /*   rows and for padding columns V..ld). dlogits may alias logits. n_valid is */
 /*   read from device memory (written by icap_caption_prep).                   */
+/*   rows_dev (optional): only rows r < *rows_dev exist (compacted targets);    */
+/*   the others are neither read nor written.                                  */
 /* ------------------------------------------------------------------------- */
 size_t icap_cross_entropy_workspace_bytes(int64_t rows);
 int icap_cross_entropy(int32_t dtype, int64_t rows, int64_t V, const void* logits, int64_t ld,
                        const int32_t* labels, const int32_t* n_valid, float* loss,
-                       void* dlogits, float grad_scale, void* workspace, void* stream);
+                       void* dlogits, float grad_scale, void* workspace, const int32_t* rows_dev,
+                       void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Global grad-norm clip + AdamW + linear LR schedule over ONE flat fp32       */

@@ -37,7 +37,7 @@ def accesses(name, args):
                 ("C", g.C, _rows(g.M, g.ldc, g.N, ec)), ("bias", g.bias, g.N * 4),
                 ("aux", g.aux, _rows(g.M, g.ldaux, g.N, ec)), ("dact_src", g.dact_src, _rows(g.M, g.ld_dact, g.N, ec)),
                 ("resid", g.resid, _rows(g.M, g.ldr, g.N, ec)), ("seed_ptr", g.seed_ptr, 8),
-                ("workspace", g.workspace, g.workspace_bytes)]
+                ("workspace", g.workspace, g.workspace_bytes), ("m_dev", g.m_dev, 4)]
     elif name in ("icap_attention_fwd", "icap_attention_bwd"):
         t = a[0]._obj
         es = ES[t.dtype]
@@ -57,19 +57,24 @@ def accesses(name, args):
                 ("v", t.exp_avg_sq, n * 4), ("bf16_out", t.bf16_out, n * 2), ("state", t.state, 64),
                 ("ws", a[1], ops.adamw_workspace(n))]
     elif name == "icap_layernorm_fwd":
-        dt, rows, D, x, ldx, gm, bt, _, y, ldy, mean, rstd, _s = a
+        dt, rows, D, x, ldx, gm, bt, _, y, ldy, mean, rstd, ymap, _s = a
         es = ES[dt]
+        # with a row map the stored rows are the compacted slots (< n_valid <= B*L, set on the device by
+        # icap_caption_prep): only the first row is checkable here
+        yrows = 1 if ymap else rows
         out += [("x", x, _rows(rows, ldx, D, es)), ("gamma", gm, D * 4), ("beta", bt, D * 4),
-                ("y", y, _rows(rows, ldy, D, es)), ("mean", mean, rows * 4), ("rstd", rstd, rows * 4)]
+                ("y", y, _rows(yrows, ldy, D, es)), ("mean", mean, rows * 4), ("rstd", rstd, rows * 4),
+                ("y_rowmap", ymap, rows * 4)]
     elif name == "icap_layernorm_bwd":
         (dt, rows, D, x, ldx, gm, mean, rstd, dy, lddy, dres, lddres, dx, lddx, dxd, _p, _sd, _o, sp, dg, db, ws,
-         _s) = a
+         dymap, _s) = a
         es = ES[dt]
+        dyrows = 1 if dymap else rows  # row map: compacted slots (see layernorm_fwd)
         out += [("x", x, _rows(rows, ldx, D, es)), ("gamma", gm, D * 4), ("mean", mean, rows * 4),
-                ("rstd", rstd, rows * 4), ("dy", dy, _rows(rows, lddy, D, es)),
+                ("rstd", rstd, rows * 4), ("dy", dy, _rows(dyrows, lddy, D, es)),
                 ("dres", dres, _rows(rows, lddres, D, es)), ("dx", dx, _rows(rows, lddx, D, es)),
                 ("dx_drop", dxd, _rows(rows, lddx, D, es)), ("seed_ptr", sp, 8), ("dgamma", dg, D * 4),
-                ("dbeta", db, D * 4)]
+                ("dbeta", db, D * 4), ("dy_rowmap", dymap, rows * 4)]
         if dg or db:
             out.append(("ws", ws, ops.layernorm_bwd_workspace(rows, D)))
     elif name == "icap_gpt2_embed":
@@ -79,14 +84,16 @@ def accesses(name, args):
                 ("wpe", wpe, (P + L) * D * es), ("ids", ids, B * L * 8), ("x", x, B * (P + L) * D * es),
                 ("seed_ptr", sp, 8)]
     elif name == "icap_caption_prep":
-        B, P, L, mask, labels, km, ls, nv, _s = a
+        B, P, L, mask, labels, km, ls, nv, slot, labc, _s = a
         out += [("mask", mask, B * L * 8), ("labels", labels, B * L * 8), ("key_mask", km, B * (P + L) * 4),
-                ("labels_shift", ls, B * (P + L) * 4), ("n_valid", nv, 4)]
+                ("labels_shift", ls, B * (P + L) * 4), ("n_valid", nv, 4), ("row_slot", slot, B * (P + L) * 4),
+                ("labels_compact", labc, B * L * 4)]
     elif name == "icap_cross_entropy":
-        dt, rows, V, lg, ld, lab, nv, loss, dl, _g, ws, _s = a
+        dt, rows, V, lg, ld, lab, nv, loss, dl, _g, ws, rdev, _s = a
         es = ES[dt]
         out += [("logits", lg, _rows(rows, ld, V, es)), ("labels", lab, rows * 4), ("n_valid", nv, 4),
-                ("loss", loss, 4), ("dlogits", dl, _rows(rows, ld, ld, es)), ("ws", ws, rows * 4)]
+                ("loss", loss, 4), ("dlogits", dl, _rows(rows, ld, ld, es)), ("ws", ws, rows * 4),
+                ("rows_dev", rdev, 4)]
     elif name == "icap_transpose":
         dt, rows, cols, src, lds, dst, ldd, rp, _s = a
         es = ES[dt]

@@ -67,3 +67,28 @@ def test_error_reporting_without_gpu():
     a.lda = a.ldb = a.ldc = 4
     with pytest.raises(_lib.IcapError, match="K must be a multiple"):
         _lib.call("icap_gemm", C.byref(a), None)
+
+
+def _gemm_args(M, N, K, **kw):
+    a = _lib.GemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.in_dtype = a.c_dtype = _lib.BF16
+    a.A = a.B = a.C = 1 << 20  # never dereferenced: the plan is host-only
+    a.lda, a.ldb, a.ldc = K, K, N
+    a.alpha = 1.0
+    for k, v in kw.items():
+        setattr(a, k, v)
+    return a
+
+
+def test_gemm_kernel_name_query_without_gpu():
+    """icap_gemm_kernel_name names the instantiation icap_gemm would launch (bench.py keys its roofline by it,
+    matching rocprofv3's kernel names)."""
+    lib = _lib.load()
+    big = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 50304, 768))).decode()
+    assert big.startswith("icap::gemm") and "unsigned short, unsigned short" in big
+    skinny = lib.icap_gemm_kernel_name(C.byref(_gemm_args(128, 2304, 768))).decode()
+    assert skinny.startswith("icap::gemm_skinny_kernel<unsigned short, unsigned short, 2")
+    f32 = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 768, 768, c_dtype=_lib.F32))).decode()
+    assert "unsigned short, float" in f32
+    assert lib.icap_gemm_kernel_name(C.byref(_gemm_args(8, 8, 3))) is None  # invalid K

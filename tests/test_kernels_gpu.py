@@ -359,3 +359,60 @@ def test_transpose_colsum_bf16_vector_paths(dev, rows, cols, rows_pad):
     ws = torch.empty(ops.colsum_workspace(rows, cols), dtype=torch.uint8, device=dev)
     ops.colsum(x, cs, ws, accumulate=False)
     assert rel_err(cs, x.double().sum(0)) < 1e-5
+
+
+def test_caption_prep_target_compaction(dev):
+    """row_slot / labels_compact / n_valid vs a host restatement of the shifted-label rule
+    (HF/loss/loss_utils.py:49-71 shift, src/models.py:296-317 prefix labels -100)."""
+    B, P, L_ = 37, 15, 50
+    g = torch.Generator().manual_seed(40)
+    labels = torch.randint(0, 50257, (B, L_), generator=g)
+    lens = torch.randint(0, L_ + 1, (B,), generator=g)
+    for b in range(B):
+        labels[b, lens[b]:] = -100
+    mask = (labels != -100).long()
+    S = P + L_
+    km, ls = torch.empty(B * S, dtype=torch.int32, device=dev), torch.empty(B * S, dtype=torch.int32, device=dev)
+    nv = torch.empty(1, dtype=torch.int32, device=dev)
+    slot = torch.empty(B * S, dtype=torch.int32, device=dev)
+    labc = torch.full((B * L_,), -7, dtype=torch.int32, device=dev)
+    ops.caption_prep(B, P, L_, mask.to(dev), labels.to(dev), km, ls, nv, slot, labc)
+    full = torch.cat([torch.full((B, P), -100, dtype=torch.long), labels], 1)
+    shifted = torch.cat([full[:, 1:], torch.full((B, 1), -100, dtype=torch.long)], 1).reshape(-1)
+    valid = shifted != -100
+    exp_slot = torch.where(valid, torch.cumsum(valid.int(), 0) - 1, torch.full_like(shifted, -1))
+    n = int(valid.sum())
+    assert int(nv.item()) == n
+    assert torch.equal(ls.cpu().long(), shifted)
+    assert torch.equal(slot.cpu().long(), exp_slot)
+    assert torch.equal(labc[:n].cpu().long(), shifted[valid])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_device_row_count(dev, dtype):
+    """m_dev: rows >= *m_dev are neither computed nor stored; rows below equal the full product."""
+    for M, N, K, mv in [(700, 1000, 768, 333), (100, 50304, 768, 41), (6400, 768, 512, 1), (256, 256, 64, 0)]:
+        A, Bw = rnd((M, K), dev, dtype, seed=41), rnd((N, K), dev, dtype, seed=42)
+        ref = torch.empty((M, N), device=dev, dtype=dtype)
+        ops.gemm(A, Bw, ref)
+        out = torch.full((M, N), 7.0, device=dev, dtype=dtype)
+        ops.gemm(A, Bw, out, m_dev=torch.tensor([mv], dtype=torch.int32, device=dev))
+        assert torch.equal(out[:mv], ref[:mv]), (M, N, K)
+        assert torch.all(out[mv:] == 7.0), (M, N, K)
+
+
+def test_cross_entropy_rows_dev(dev):
+    rows, V, ld, nr = 64, 1000, 1024, 23
+    logits = rnd((rows, ld), dev, torch.float32, 2.0, seed=43)
+    labels = torch.randint(0, V, (rows,), generator=torch.Generator().manual_seed(44), dtype=torch.int32).to(dev)
+    nv = torch.tensor([nr], dtype=torch.int32, device=dev)
+    loss = torch.empty(1, device=dev)
+    dl = torch.full_like(logits, 5.0)
+    ws = torch.empty(ops.cross_entropy_workspace(rows), dtype=torch.uint8, device=dev)
+    ops.cross_entropy(logits, V, labels, nv, loss, dl, ws, rows_dev=nv)
+    x = logits[:nr, :V].double().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(x, labels[:nr].long())
+    (gx,) = torch.autograd.grad(ref, x)
+    assert abs(loss.item() - ref.item()) < 1e-5 * max(1, abs(ref.item()))
+    assert rel_err(dl[:nr, :V], gx) < 1e-4
+    assert torch.all(dl[nr:] == 5.0)

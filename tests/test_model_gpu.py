@@ -259,3 +259,26 @@ def test_bf16_train_with_clip_dropout_decreases(dev):
         losses.append(t.last_loss.item())
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0] - 0.5, losses
+
+
+@pytest.mark.parametrize("dropout", [False, True])
+def test_compact_head_equals_full_head(dev, dropout):
+    """The trainer's LM head over the target rows only (compact_head, the default) gives the loss and parameter
+    updates of the full 65-row head: the skipped rows have label -100 and contribute exactly nothing."""
+    g = load("tiny")
+    batch = inputs(g, dev)
+    ids, mask, labels, emb = batch
+    res = []
+    for compact in (True, False):
+        model = build(TINY_G, TINY_M, torch.float32, dev)
+        t = CaptionTrainer(model, ids.shape[0], ids.shape[1], lr=1e-3, num_training_steps=4, dropout=dropout,
+                           compact_head=compact, seed=5)
+        t.load_batch(ids, mask, labels, emb)
+        losses = []
+        for _ in range(3):
+            t.micro_step()
+            losses.append(t.last_loss.item())
+        res.append((losses, {k: v.detach().clone() for k, v in model.mapping_network.state_dict().items()}))
+    assert np.allclose(res[0][0], res[1][0], rtol=1e-6, atol=0), (res[0][0], res[1][0])
+    for k in res[0][1]:
+        assert torch.allclose(res[0][1][k], res[1][1][k], rtol=1e-6, atol=1e-9), k

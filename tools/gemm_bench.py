@@ -33,6 +33,13 @@ SHAPES = [
     (768, 768, 3200, "beta", torch.float32),
     (128, 2304, 768, "plain", torch.bfloat16),
     (128, 768, 3072, "resid", torch.bfloat16),
+    (8320, 768, 768, "plain", torch.bfloat16),
+    (6400, 768, 768, "resid", torch.bfloat16),
+    (6400, 2304, 768, "plain", torch.bfloat16),
+    (3200, 768, 768, "resid_drop", torch.bfloat16),
+    (3200, 2304, 768, "plain", torch.bfloat16),
+    (3200, 768, 3072, "plain", torch.bfloat16),
+    (3072, 768, 3200, "beta", torch.float32),
 ]
 
 
