@@ -30,6 +30,8 @@
 // C/D map (both): col = lane&15, row = 4*(lane>>4) + reg.
 #include "common.h"
 
+#include <type_traits>
+
 namespace icap {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -64,10 +66,27 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
 }
 
+// same, with the inputs forced into SGPRs (readfirstlane) so hipcc can prove the descriptor wave-uniform and
+// emits no waterfall loop around the buffer ops (cdna_hip_programming.md T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_u(const void* base, uint64_t bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes > 0x7fffffffull ? 0x7fffffffu : (uint32_t)bytes);
+  void* pb = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, (int)n, 0x00020000);
+}
+
 // 16-byte LDS-DMA of one wave: lane l's 16 bytes land at lds + 16 l
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(lds), 16, off, 0, 0, 0);
+}
+
+// same with a wave-uniform soffset (row / k offsets in SGPRs, one per-lane VGPR offset)
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(lds), 16, voff, soff, 0, 0);
 }
 
 __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
@@ -658,6 +677,229 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm3b_kernel(icap_gemm_ar
   }
 }
 
+// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14) for the
+// builtin form, which hipcc's wait-count tracking sees (inline asm is opaque to it, so it adds its own vmcnt(0)
+// before the next read of a stage it believes still has DMA pending)
+constexpr int wait_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+
+// Phase-interleaved 8-wave GEMM (bf16 in, fp32 accumulate) for the large products of the step: 256-row tiles,
+// BN = 256 or 128 columns, 8 waves as 2 (M) x 4 (N), each wave a (128) x (BN/4) accumulator block (two waves per
+// SIMD, so one wave's LDS reads and waits overlap the other's MFMAs). Per-wave LDS reads per MFMA are 25-40 %
+// below the 128x128/4-wave kernels (the operand fragments of a 128-row wave block are reused over BN/4 columns).
+//
+// K advances 64 at a time through two LDS stages E (even k-tiles) and O (odd), each one compile-time
+// __shared__ object so hipcc's LDS-DMA alias tracking never drains the DMA queue before a fragment read. One
+// k-tile is four phases, one quadrant (64 rows x BN/8 columns, 16 MFMAs at BN=256) each:
+//   ph1: read A rows 0-63 + B cols 0..   -> Q00      ph2: read B cols BN/8.. -> Q01
+//   ph3: read A rows 64-127; DMA the B halves of k-tile t+2 into this stage (last read in ph2) -> Q11
+//   ph4: DMA the A halves of k-tile t+2 (last read in ph3); counted vmcnt: k-tile t+1 has landed -> Q10
+// Every phase: reads, [DMA], s_barrier, lgkmcnt(0), setprio(1) MFMAs setprio(0), s_barrier. The counted vmcnt
+// leaves k-tile t+2's DMA in flight across four phases (cdna_hip_programming.md §5 "The 256² 8-phase
+// template", "Pipelining across barriers"; raw s_barrier so no vmcnt(0) is emitted). Reads of a stage follow
+// the wait + barrier that retire its DMA; a stage is re-filled one phase after its last read retired (lgkmcnt(0)
+// before the MFMAs, barrier after them).
+template <typename TC, int BN>
+__global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int tiles_n, int splits, int nk_split,
+                                                      uint32_t drop_thresh, float inv_keep) {
+  constexpr int BM = 256, WN = 4;
+  constexpr int TM = BM / 32, TN = BN / (16 * WN);  // per-wave 16x16 tiles: 8 x (4 | 2)
+  constexpr int QM = TM / 2, QN = TN / 2;           // per-phase quadrant tiles
+  constexpr int STA = BM * GROWB;                   // A bytes per stage
+  constexpr int ST = (BM + BN) * GROWB;             // bytes per stage
+  constexpr int GA = BM / 128, GB = BN / 128;       // DMA instructions per thread per A / B half
+  constexpr int GT = 2 * (GA + GB);                 // per k-tile (the vmcnt unit)
+  constexpr int EPR = 16, ELD = 16 * TN + 4;
+  static_assert(8 * EPR * ELD * 4 <= ST, "epilogue staging must fit one stage");
+  __shared__ __attribute__((aligned(16))) char smE[ST];
+  __shared__ __attribute__((aligned(16))) char smO[ST];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles = (int)(gridDim.x / splits);
+  const int split = wgid / tiles, tile = wgid - split * tiles;
+  const int tiles_m = tiles / tiles_n;
+  const int tm = p.m_dev ? tile % tiles_m : tile / tiles_n;
+  const int tn = p.m_dev ? tile / tiles_m : tile - tm * tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t M = p.M, N = p.N, K = p.K;
+  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;
+  if (m0 >= Mv) return;
+  const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * 2;
+  const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * 2;
+  const int64_t mrows = Mv - m0 < BM ? Mv - m0 : BM;
+  const int64_t nrows = N - n0 < BN ? N - n0 : BN;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc_u(Ab, (uint64_t)((mrows - 1) * p.lda + K) * 2);
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc_u(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * 2);
+  // lane l of a DMA wave-instruction fills row l>>3, physical 16-byte chunk l&7 of an 8-row piece; the source
+  // chunk is XOR-swizzled by the row (the fragment reads apply the same involution: lds_off)
+  const int lrow = lane >> 3;
+  const int lchunk = ((lane & 7) ^ lrow) * 8;
+  // per-lane part of the source offset in one VGPR per operand; the row piece and k offsets are wave-uniform
+  const uint32_t va = (uint32_t)((lrow * p.lda + lchunk) * 2), vb = (uint32_t)((lrow * p.ldb + lchunk) * 2);
+  const uint32_t lda8 = (uint32_t)(p.lda * 16), ldb8 = (uint32_t)(p.ldb * 16);  // bytes per 8 rows
+  const int nk_all = (int)((K + 63) / 64);
+  const int kt0 = split * nk_split;
+  const int nk = (nk_all - kt0 < nk_split ? nk_all - kt0 : nk_split);
+  const int64_t kbase = (int64_t)kt0 * 64;
+  auto dmaA = [&](char* st, int t, int h) {
+    const int64_t k0 = kbase + (int64_t)t * 64;
+    const uint32_t v = k0 + lchunk < K ? va : OOB;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int pc = h * (BM / 16) + i * 8 + wave;  // 8-row piece of the stage's A image
+      dma16s(ra, st + pc * 8 * GROWB, v, __builtin_amdgcn_readfirstlane((uint32_t)pc * lda8 + (uint32_t)(k0 * 2)));
+    }
+  };
+  auto dmaB = [&](char* st, int t, int h) {
+    const int64_t k0 = kbase + (int64_t)t * 64;
+    const uint32_t v = k0 + lchunk < K ? vb : OOB;
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int pc = h * (BN / 16) + i * 8 + wave;
+      dma16s(rb, st + STA + pc * 8 * GROWB, v, __builtin_amdgcn_readfirstlane((uint32_t)pc * ldb8 + (uint32_t)(k0 * 2)));
+    }
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  // Fragment reads are inline-asm ds_read_b128: hipcc then sees no LDS read it could order against the LDS-DMA
+  // (it otherwise drains the DMA queue with vmcnt(0) at the loop head), and the waits are ours: lgkmcnt(0) +
+  // sched_barrier before the MFMAs that consume a phase's reads (cdna_hip_programming.md §5.4 rule 18).
+  const uint32_t baseE = (uint32_t)reinterpret_cast<uintptr_t>(smE);
+  const uint32_t baseO = (uint32_t)reinterpret_cast<uintptr_t>(smO);
+  uint32_t la[2], lb[2];  // per-lane byte offsets of the k-half ks fragment within a stage
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const uint32_t sw = (uint32_t)(((ks * 4 + fg) ^ (fr & 7)) << 4);
+    la[ks] = (uint32_t)((wm * (BM / 2) + fr) * GROWB) + sw;
+    lb[ks] = (uint32_t)(STA + (wn * (BN / 4) + fr) * GROWB) + sw;
+  }
+  // fragment registers: A rows 0-63 (fa0) / 64-127 (fa1) of the wave block; B column halves in fb[0], fb[1]
+  // (which half each holds alternates per k-tile: B-sub0 of k-tile t sits in fb[t & 1])
+  uint4 fa0[2][QM], fa1[2][QM], fb[2][2][QN];
+  auto rdA = [&](uint32_t st, auto qi_c, uint4 (&f)[2][QM]) {
+    constexpr int qi = decltype(qi_c)::value;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint32_t a = st + la[ks];
+#pragma unroll
+      for (int i = 0; i < QM; ++i)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][i]) : "v"(a), "i"((qi * (BM / 4) + i * 16) * GROWB));
+    }
+  };
+  auto rdB = [&](uint32_t st, auto qj_c, uint4 (&f)[2][QN]) {
+    constexpr int qj = decltype(qj_c)::value;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint32_t a = st + lb[ks];
+#pragma unroll
+      for (int j = 0; j < QN; ++j)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][j]) : "v"(a), "i"((qj * (BN / 8) + j * 16) * GROWB));
+    }
+  };
+  using C0 = std::integral_constant<int, 0>;
+  using C1 = std::integral_constant<int, 1>;
+  auto reads_done = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mm = [&](int qi, int qj, const uint4 (&a)[2][QM], const uint4 (&b)[2][QN]) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < QM; ++i)
+#pragma unroll
+        for (int j = 0; j < QN; ++j) mfma_chunk<bf16_t>(acc[qi * QM + i][qj * QN + j], a[ks][i], b[ks][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // k-tile t from stage X (parity P = t & 1), stage Y holds k-tile t+1. Fragment reads run one phase ahead of the
+  // MFMAs that consume them, so LDS latency hides under the previous quadrant; one barrier per k-tile.
+  auto ktile = [&](char* X, uint32_t bx, uint32_t by, int t, uint4 (&bs0)[2][QN], uint4 (&bs1)[2][QN]) {
+    const bool next = t + 1 < nk;
+    reads_done();              // fa0 / bs0 (read during the previous k-tile) are in registers
+    rdB(bx, C1{}, bs1);        // B cols BN/8.. of k-tile t
+    mm(0, 0, fa0, bs0);
+    reads_done();
+    rdA(bx, C1{}, fa1);        // A rows 64-127 of k-tile t
+    mm(0, 1, fa0, bs1);
+    // every read of X for k-tile t has retired and k-tile t+1 has landed in Y, on every wave
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (next) rdA(by, C0{}, fa0);  // A rows 0-63 of k-tile t+1
+    if (t + 2 < nk) { dmaB(X, t + 2, 0); dmaB(X, t + 2, 1); dmaA(X, t + 2, 0); dmaA(X, t + 2, 1); }
+    mm(1, 1, fa1, bs1);
+    reads_done();
+    if (next) rdB(by, C0{}, bs1);  // B cols 0.. of k-tile t+1 (bs1 is free after Q11)
+    mm(1, 0, fa1, bs0);
+  };
+
+  dmaA(smE, 0, 0); dmaA(smE, 0, 1); dmaB(smE, 0, 0); dmaB(smE, 0, 1);
+  if (nk > 1) {
+    dmaA(smO, 1, 0); dmaA(smO, 1, 1); dmaB(smO, 1, 0); dmaB(smO, 1, 1);
+    __builtin_amdgcn_s_waitcnt(wait_vm(GT));
+  } else {
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
+  }
+  __builtin_amdgcn_s_barrier();
+  rdA(baseE, C0{}, fa0);
+  rdB(baseE, C0{}, fb[0]);
+  for (int t = 0; t < nk; t += 2) {
+    ktile(smE, baseE, baseO, t, fb[0], fb[1]);
+    if (t + 1 < nk) ktile(smO, baseO, baseE, t + 1, fb[1], fb[0]);
+  }
+  reads_done();
+  __syncthreads();  // the epilogue stages through smE
+
+  uint64_t seed = 0;
+  if (splits == 1 && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
+  float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
+  float* cs = reinterpret_cast<float*>(smE) + wave * (EPR * ELD);
+  constexpr int LPR = 4 * TN;
+  constexpr int RPI = 64 / LPR;
+  const int er = lane / LPR;
+  const int ec = (lane - er * LPR) * 4;
+  const int64_t col = n0 + wn * 16 * TN + ec;
+  const bool full4 = col + 4 <= N;
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < TM; ++h) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) cs[(fg * 4 + v) * ELD + j * 16 + fr] = acc[h][j][v];
+    __syncthreads();
+#pragma unroll 2
+    for (int t = 0; t < EPR / RPI; ++t) {
+      const int lr = t * RPI + er;
+      const int64_t row = m0 + wm * (BM / 2) + h * EPR + lr;
+      float x[4];
+      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
+      if (row < Mv && col < N) {
+        if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
+        else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Skinny-M GEMM (M <= 128: greedy-decode steps over the batch, CLIP projection, mapper input Linear).
 // A weight-streaming, latency-bound problem: block = 8 waves over a 16*NT-column slab of B (= W rows) and a
 // 16*MT-row slab of A (grid.y walks M, so no block streams all of A through its CU: per-CU L2 bandwidth, not
@@ -904,6 +1146,16 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
     const int64_t tm2 = (p.M + 255) / 256;
     pl.grid = dim3((unsigned)(tm2 * tiles_n * splits));
     pl.block = dim3(512);
+  } else if (pl.variant == 10 || pl.variant == 11) {  // phase-interleaved 8-wave: 256x256 / 256x128 (bf16 only)
+    if (p.in_dtype != ICAP_BF16) {
+      pl.variant = 0;
+    } else {
+      const int bn = pl.variant == 10 ? 256 : 128;
+      const int64_t tm2 = (p.M + 255) / 256, tn2 = (p.N + bn - 1) / bn;
+      pl.grid = dim3((unsigned)(tm2 * tn2 * splits));
+      pl.tiles_n = (int)tn2;
+      pl.block = dim3(512);
+    }
   }
   return ICAP_OK;
 }
@@ -918,6 +1170,8 @@ static const char* variant_kernel(int v) {
     case 7: return "gemm2b_kernel<%s, %s, 2, 2, 2, 4, 4>";
     case 8: return "gemm2b_kernel<%s, %s, 1, 2, 4, 8, 4>";
     case 9: return "gemm3b_kernel<%s, %s, 1, 4, 2, 4, 4>";
+    case 10: return "gemm8p_kernel<%s, 256>";
+    case 11: return "gemm8p_kernel<%s, 128>";
     default: return "gemm3b_kernel<%s, %s, 1, 2, 2, 4, 4>";
   }
 }
@@ -933,7 +1187,8 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
   if (pl.skinny) snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2>", pl.nt);
   else snprintf(fmt, sizeof fmt, "%s", variant_kernel(pl.variant));
   char inner[128];
-  snprintf(inner, sizeof inner, fmt, ti, tc);
+  if (!pl.skinny && (pl.variant == 10 || pl.variant == 11)) snprintf(inner, sizeof inner, fmt, tc);
+  else snprintf(inner, sizeof inner, fmt, ti, tc);
   snprintf(buf, sizeof buf, "icap::%s", inner);
   return buf;
 }
@@ -975,7 +1230,15 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     case 9: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 4, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
     default: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
   }
-  if (p.in_dtype == ICAP_BF16) {
+  if (pl.variant == 10 || pl.variant == 11) {  // bf16 inputs (the plan falls back to variant 0 otherwise)
+    if (pl.variant == 10) {
+      if (p.c_dtype == ICAP_BF16) hipLaunchKernelGGL((gemm8p_kernel<bf16_t, 256>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm8p_kernel<float, 256>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    } else {
+      if (p.c_dtype == ICAP_BF16) hipLaunchKernelGGL((gemm8p_kernel<bf16_t, 128>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm8p_kernel<float, 128>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    }
+  } else if (p.in_dtype == ICAP_BF16) {
     if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(bf16_t, bf16_t) } else { ICAP_GEMM_LAUNCH(bf16_t, float) }
   } else {
     if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(float, bf16_t) } else { ICAP_GEMM_LAUNCH(float, float) }
