@@ -121,6 +121,47 @@ def cpu_baseline(seconds_budget: float = 20.0):
                       f"fwd/bwd + AdamW, dropout 0.1, fp32, torch CPU {cores} threads) in {el:.1f}s"}
 
 
+def greedy_rate(model, Bd, dev, world):
+    """50-token KV-cached greedy captions/s over a batch of Bd image embeddings (all 50 steps decoded)."""
+    g = torch.Generator().manual_seed(5)
+    emb = torch.randn((Bd, 512), generator=g)
+    emb = (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
+    # one caption = 50 greedy tokens after the 15-token prefix (SURVEY.md §8d): decode all 50 steps (the trained
+    # synthetic model emits EOS early; the reference loop would stop there), output identical either way
+    model.generate(emb, max_length=50, temperature=0.0, early_exit=False)  # warm-up
+    torch.cuda.synchronize()
+    td0 = time.perf_counter()
+    nd = 3
+    lens = []
+    for _ in range(nd):
+        out = model.generate(emb, max_length=50, temperature=0.0, early_exit=False)
+        lens.append(out.shape[1])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - td0
+    caps_per_s = world * Bd * nd / dt
+
+    return caps_per_s, dt, nd, lens
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (tools/pmc_traffic.sh writes
+    profiles/*pmc_traffic.json from separate FETCH_SIZE / WRITE_SIZE passes over this bench's train step).
+    FETCH_SIZE is doubled (gfx950 tallies 128-B wide reads at 64 B: MI355X_MICROARCH.md, HBM)."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k:
+            best = (k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best if best else (None, None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,6 +171,7 @@ def main():
     ap.add_argument("--decode-batch", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-decode", action="store_true", help="skip the greedy-decode measurement (PMC passes)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -192,22 +234,10 @@ def main():
 
     # -- greedy decode throughput ------------------------------------------------------------------------------
     Bd = args.decode_batch
-    g = torch.Generator().manual_seed(5)
-    emb = torch.randn((Bd, 512), generator=g)
-    emb = (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
-    # one caption = 50 greedy tokens after the 15-token prefix: decode all 50 steps (the trained
-    # synthetic model emits EOS early; the reference loop would stop there), output identical either way
-    model.generate(emb, max_length=50, temperature=0.0, early_exit=False)  # warm-up
-    torch.cuda.synchronize()
-    td0 = time.perf_counter()
-    nd = 3
-    lens = []
-    for _ in range(nd):
-        out = model.generate(emb, max_length=50, temperature=0.0, early_exit=False)
-        lens.append(out.shape[1])
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - td0
-    caps_per_s = world * Bd * nd / dt
+    caps_per_s, dt, nd, lens = None, None, 1, [None]
+    if not args.no_decode:
+        caps_per_s, dt, nd, lens = greedy_rate(model, Bd, dev, world)
+    traffic, traffic_src = pmc_traffic(dom)
 
     if rank == 0:
         res = {
@@ -223,12 +253,13 @@ def main():
                        "per_gpu_batch": B, "global_batch": B * world, "seq_len": 65, "caption_len": 50,
                        "parallelism": f"dp{world}", "graph": use_graph},
             "final_loss": round(loss, 4),
-            "greedy_captions_per_s": round(caps_per_s, 1),
+            "greedy_captions_per_s": round(caps_per_s, 1) if caps_per_s else None,
             "greedy": {"batch_per_gpu": Bd, "decode_steps": 50, "returned_len": lens[-1], "kv_cache": True,
-                       "ms_per_batch": round(dt / nd * 1e3, 3)},
+                       "ms_per_batch": round(dt / nd * 1e3, 3) if dt else None},
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1),
                          "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
-                         "traffic": None, "launches_per_step": n_l,
+                         "traffic": traffic, "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
+                         "traffic_source": traffic_src, "launches_per_step": n_l,
                          "avg_launch_us": round(ms / n_l * 1e3, 2),
                          "alg_gflop_per_launch": round(fl / n_l / 1e9, 3),
                          "all_gemm_ms_per_step": round(gemm_ms, 3), "all_gemm_tflop_per_step": round(all_fl / 1e12, 4),
