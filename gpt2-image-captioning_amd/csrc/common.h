@@ -78,15 +78,24 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// ---- counter-based dropout RNG (splitmix64 finaliser) ------------------------
+// ---- counter-based dropout RNG -----------------------------------------------
 // keep(idx) is a pure function of (seed, idx): forward and backward regenerate
-// the same mask without storing it.
+// the same mask without storing it. 32-bit arithmetic only: (lo ^ s0) * golden
+// + hi, xor s1, then the lowbias32 finaliser (Wellons) — three v_mul_lo_u32
+// (quarter rate) per element instead of the twelve a 64-bit splitmix64 chain
+// costs; dropout runs on every GPT-2 / mapper activation and attention prob of
+// a train step (~0.7 G draws), where the 64-bit chain was ~1 ms of VALU a step.
+// For a fixed seed the map idx -> hash is a bijection on idx < 2^32 (odd
+// multiply, xor and the finaliser are all invertible), so no two elements of
+// one tensor share a draw. tests/test_dropout_hash.py restates it in numpy.
 __device__ __forceinline__ uint32_t hash32(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+  uint32_t x = (((uint32_t)idx ^ (uint32_t)seed) * 0x9E3779B9u + (uint32_t)(idx >> 32)) ^ (uint32_t)(seed >> 32);
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
 }
 __device__ __forceinline__ uint64_t eff_seed(uint64_t seed, const uint64_t* ptr) {
   return ptr ? seed + (*ptr) * 0x9E3779B97F4A7C15ull : seed;

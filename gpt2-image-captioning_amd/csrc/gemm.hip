@@ -93,6 +93,15 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
 template <typename T> struct vec4io;
 template <> struct vec4io<float> {
   static __device__ __forceinline__ void ld(const float* p, float v[4]) { io<float>::ld4(p, v); }
@@ -106,10 +115,19 @@ template <> struct vec4io<bf16_t> {
 // Epilogue of 4 consecutive columns [col, col+4) of row `row` (the order is the one include/icap.h documents).
 // x: alpha-unscaled fp32 accumulators; bias4: bias[col..col+3] (0 past N); full4: all 4 columns in range and
 // C/aux/resid/dact_src leading dimensions allow 4-wide vector access (checked per operand).
+// pre: optional prefetched bf16 quad of the epilogue's input operand at (row, col..col+3) — dact_src in the
+// backward form, resid in the forward form — loaded by the caller ahead of the LDS staging (full4 rows only).
+__device__ __forceinline__ void unpack_bf16x4(const uint2 w, float v[4]) {
+  v[0] = __uint_as_float(w.x << 16);
+  v[1] = __uint_as_float(w.x & 0xffff0000u);
+  v[2] = __uint_as_float(w.y << 16);
+  v[3] = __uint_as_float(w.y & 0xffff0000u);
+}
+
 template <typename TC>
 __device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64_t col, float x[4],
                                      const float bias4[4], bool full4, uint64_t seed, uint32_t drop_thresh,
-                                     float inv_keep) {
+                                     float inv_keep, const uint2* pre = nullptr) {
   const int64_t N = p.N;
   TC* C = reinterpret_cast<TC*>(p.C);
   TC* aux = reinterpret_cast<TC*>(p.aux);
@@ -122,7 +140,8 @@ __device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64
   constexpr uintptr_t VA = 4 * sizeof(TC) - 1;
   full4 = full4 && (p.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(C) & VA) == 0;
   if (p.dact != ICAP_ACT_NONE) {
-    if (full4 && (p.ld_dact & 3) == 0 && (reinterpret_cast<uintptr_t>(dsrc) & VA) == 0) vec4io<TC>::ld(dsrc + row * p.ld_dact + col, a4);
+    if (pre) unpack_bf16x4(*pre, a4);
+    else if (full4 && (p.ld_dact & 3) == 0 && (reinterpret_cast<uintptr_t>(dsrc) & VA) == 0) vec4io<TC>::ld(dsrc + row * p.ld_dact + col, a4);
     else for (int e = 0; e < 4; ++e) a4[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -150,7 +169,8 @@ __device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64
       for (int e = 0; e < 4; ++e) x[e] *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
     }
     if (resid) {
-      if (full4 && (p.ldr & 3) == 0 && (reinterpret_cast<uintptr_t>(resid) & VA) == 0) vec4io<TC>::ld(resid + row * p.ldr + col, r4);
+      if (pre) unpack_bf16x4(*pre, r4);
+      else if (full4 && (p.ldr & 3) == 0 && (reinterpret_cast<uintptr_t>(resid) & VA) == 0) vec4io<TC>::ld(resid + row * p.ldr + col, r4);
       else for (int e = 0; e < 4; ++e) r4[e] = (col + e < N) ? io<TC>::ld(resid + row * p.ldr + col + e) : 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) x[e] += r4[e];
@@ -326,10 +346,50 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
   }
-  if (NST == 1) __syncthreads();  // the single stage buffer is still being read by other waves
+  // Prefetch of the epilogue's input operand (bf16 C: dact_src in the backward form, resid in the forward form):
+  // the rows this lane stores, issued before the LDS staging (all of them, or in two halves at 4 blocks/CU) so one
+  // memory latency is exposed per group instead of one dependent round trip per staged row pair (on the N = 768
+  // launches a CU holds 1-2 tiles, so nothing else hides it). Out-of-range rows read row Mv-1 (no branch per
+  // load: cdna_hip_programming.md §5 trap (c)) and are never stored.
+  constexpr int NH = 16 * TM / EPR;              // staging passes
+  constexpr int NPG = MINB >= 4 && NH >= 2 ? 2 : 1;  // prefetch groups: half the rows at a time at 128 VGPRs
+  constexpr int HPG = NH / NPG;                  // passes per prefetch group
+  constexpr int NEP = HPG * (EPR / RPI);         // prefetched rows held at once
+  uint2 pre[NEP];
+  bool want_pre = false;  // block-uniform: this launch has a bf16 dact_src / resid operand
+  const bf16_t* esrc = nullptr;
+  int64_t eld = 0;
+  const int64_t rb = m0 + wm * 16 * TM + er;  // row of (pass h, row t) = rb + h EPR + t RPI
+  auto prefetch = [&](auto gc) __attribute__((always_inline)) {  // rows of passes [g HPG, g HPG + HPG)
+    constexpr int g = decltype(gc)::value;
+    if (want_pre && full4) {
 #pragma unroll
-  for (int h = 0; h < 16 * TM / EPR; ++h) {
-    // stage rows [EPR h, EPR h + EPR) of this wave's accumulator tile
+      for (int i = 0; i < NEP; ++i) {
+        const int64_t r0 = rb + (int64_t)(g * NEP + i) * RPI;
+        const int64_t row = r0 < Mv ? r0 : Mv - 1;
+        pre[i] = *reinterpret_cast<const uint2*>(esrc + row * eld + col);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads here: hipcc would sink each to its use
+  };
+  if constexpr (std::is_same<TC, bf16_t>::value) {
+    if (splits == 1) {
+      if (p.dact != ICAP_ACT_NONE) {
+        esrc = reinterpret_cast<const bf16_t*>(p.dact_src);
+        eld = p.ld_dact;
+      } else if (p.resid) {
+        esrc = reinterpret_cast<const bf16_t*>(p.resid);
+        eld = p.ldr;
+      }
+    }
+    want_pre = esrc != nullptr && (eld & 3) == 0 && (reinterpret_cast<uintptr_t>(esrc) & 7) == 0 &&
+               (p.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(p.C) & 7) == 0;
+    prefetch(std::integral_constant<int, 0>{});
+  }
+  if (NST == 1) __syncthreads();  // the single stage buffer is still being read by other waves
+  // rows [EPR h, EPR h + EPR) of this wave's accumulator tile -> LDS (h compile-time: it indexes acc[])
+  auto stage_rows = [&](auto hc) __attribute__((always_inline)) {
+    constexpr int h = decltype(hc)::value;
 #pragma unroll
     for (int ii = 0; ii < EPR / 16; ++ii)
 #pragma unroll
@@ -337,19 +397,41 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
 #pragma unroll
         for (int v = 0; v < 4; ++v)
           cs[(ii * 16 + fg * 4 + v) * ELD + j * 16 + fr] = acc[(EPR / 16) * h + ii][j][v];
-    __syncthreads();
-#pragma unroll 2
-    for (int t = 0; t < EPR / RPI; ++t) {
-      const int lr = t * RPI + er;  // 0..EPR-1
-      const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
-      float x[4];
-      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
-      if (row < Mv && col < N) {
-        if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
-        else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
-      }
+  };
+  auto store_row = [&](int h, int t, const uint2* pq) __attribute__((always_inline)) {
+    const int lr = t * RPI + er;  // 0..EPR-1
+    const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
+    float x[4];
+    *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
+    if (row < Mv && col < N) {
+      if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
+      else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep, pq);
     }
-    __syncthreads();
+  };
+  if (want_pre || MINB >= 4) {  // (at 4 blocks/CU one path: a second one made the 128-VGPR build spill)
+    // passes h / rows t as compile-time indices (static_for) so pre[] stays in registers (the unroller refuses
+    // a full unroll of this body by size); a separate path, so launches without the operand keep the compact
+    // loop below (the fully unrolled copy cost the plain launches 5-15 % in instruction fetch)
+    static_for<0, NH>([&](auto hc) {
+      constexpr int h = decltype(hc)::value;
+      if constexpr (h > 0 && h % HPG == 0) prefetch(std::integral_constant<int, h / HPG>{});
+      stage_rows(hc);
+      __syncthreads();
+      static_for<0, EPR / RPI>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        store_row(h, t, full4 ? &pre[(h % HPG) * (EPR / RPI) + t] : nullptr);
+      });
+      __syncthreads();
+    });
+  } else {
+    static_for<0, NH>([&](auto hc) {  // h compile-time: acc[] is indexed by it
+      constexpr int h = decltype(hc)::value;
+      stage_rows(hc);
+      __syncthreads();
+#pragma unroll 2
+      for (int t = 0; t < EPR / RPI; ++t) store_row(h, t, nullptr);
+      __syncthreads();
+    });
   }
 }
 
@@ -1058,7 +1140,9 @@ static int gemm_variant(const icap_gemm_args& p, int64_t nk_per_block) {
   const int o = gemm_variant_override();
   if (o >= 0) return o;
   if (nk_per_block > 16) return 0;
-  const bool heavy = p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE || p.aux || p.drop_p > 0.f;
+  // 4 blocks/CU only for the epilogues that move a second M x N tensor (dact_src read / aux store); with the
+  // epilogue-operand prefetch, activation / dropout / residual epilogues run faster at 3 (profiles/r01_gemm_ab3.txt)
+  const bool heavy = p.dact != ICAP_ACT_NONE || p.aux;
   return heavy ? 5 : 4;
 }
 

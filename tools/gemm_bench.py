@@ -1,6 +1,7 @@
 """GEMM microbenchmark over the shapes/epilogues of one training step (random bf16 operands; HIP-event timing).
 
-Usage: ICAP_GEMM_VARIANT=<n> python tools/gemm_bench.py   (variant: see gemm_kernel in csrc/gemm.hip)
+Usage: ICAP_GEMM_VARIANT=<n> [ICAP_LIB=path/to/other/libicap_hip.so] python tools/gemm_bench.py
+       (variant: see gemm_kernel in csrc/gemm.hip)
 """
 
 import os
@@ -44,6 +45,8 @@ SHAPES = [
 
 
 def main():
+    if os.environ.get("ICAP_LIB"):  # A/B against another build of the library
+        L.load(os.environ["ICAP_LIB"])
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     reps = int(os.environ.get("REPS", "20"))
