@@ -102,32 +102,60 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-template <typename T> struct vec4io;
-template <> struct vec4io<float> {
-  static __device__ __forceinline__ void ld(const float* p, float v[4]) { io<float>::ld4(p, v); }
-  static __device__ __forceinline__ void st(float* p, const float v[4]) { io<float>::st4(p, v); }
+// W consecutive elements (W = 4 or 8) as fp32, through one 8- or 16-byte access (bf16) or one / two float4 (f32)
+template <typename T, int W> struct vecio;
+template <int W> struct vecio<float, W> {
+  static __device__ __forceinline__ void ld(const float* p, float v[W]) {
+#pragma unroll
+    for (int q = 0; q < W / 4; ++q) io<float>::ld4(p + 4 * q, v + 4 * q);
+  }
+  static __device__ __forceinline__ void st(float* p, const float v[W]) {
+#pragma unroll
+    for (int q = 0; q < W / 4; ++q) io<float>::st4(p + 4 * q, v + 4 * q);
+  }
 };
-template <> struct vec4io<bf16_t> {
+template <> struct vecio<bf16_t, 4> {
   static __device__ __forceinline__ void ld(const bf16_t* p, float v[4]) { io<bf16_t>::ld4(p, v); }
   static __device__ __forceinline__ void st(bf16_t* p, const float v[4]) { io<bf16_t>::st4(p, v); }
 };
-
-// Epilogue of 4 consecutive columns [col, col+4) of row `row` (the order is the one include/icap.h documents).
-// x: alpha-unscaled fp32 accumulators; bias4: bias[col..col+3] (0 past N); full4: all 4 columns in range and
-// C/aux/resid/dact_src leading dimensions allow 4-wide vector access (checked per operand).
-// pre: optional prefetched bf16 quad of the epilogue's input operand at (row, col..col+3) — dact_src in the
-// backward form, resid in the forward form — loaded by the caller ahead of the LDS staging (full4 rows only).
-__device__ __forceinline__ void unpack_bf16x4(const uint2 w, float v[4]) {
+template <> struct vecio<bf16_t, 8> {
+  static __device__ __forceinline__ void ld(const bf16_t* p, float v[8]) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[2 * q] = __uint_as_float(w[q] << 16);
+      v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void st(bf16_t* p, const float v[8]) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7]));
+  }
+};
+// raw bf16 vector of W elements (prefetched epilogue operands)
+template <int W> struct rawbf;
+template <> struct rawbf<4> { typedef uint2 T; };
+template <> struct rawbf<8> { typedef uint4 T; };
+__device__ __forceinline__ void unpack_bf16(const uint2 w, float v[4]) {
   v[0] = __uint_as_float(w.x << 16);
   v[1] = __uint_as_float(w.x & 0xffff0000u);
   v[2] = __uint_as_float(w.y << 16);
   v[3] = __uint_as_float(w.y & 0xffff0000u);
 }
+__device__ __forceinline__ void unpack_bf16(const uint4 w, float v[8]) {
+  unpack_bf16(make_uint2(w.x, w.y), v);
+  unpack_bf16(make_uint2(w.z, w.w), v + 4);
+}
 
-template <typename TC>
-__device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64_t col, float x[4],
-                                     const float bias4[4], bool full4, uint64_t seed, uint32_t drop_thresh,
-                                     float inv_keep, const uint2* pre = nullptr) {
+// Epilogue of W consecutive columns [col, col+W) of row `row` (the order is the one include/icap.h documents).
+// x: alpha-unscaled fp32 accumulators; biasw: bias[col..col+W-1] (0 past N); fullw: all W columns in range;
+// W-wide vector access is used per operand where its leading dimension and base pointer are W-aligned.
+// pre: optional prefetched raw bf16 vector of the epilogue's input operand at (row, col..) — dact_src in the
+// backward form, resid in the forward form — loaded by the caller ahead of the LDS staging (fullw rows only).
+template <typename TC, int W>
+__device__ __forceinline__ void epiw(const icap_gemm_args& p, int64_t row, int64_t col, float x[W],
+                                     const float biasw[W], bool fullw, uint64_t seed, uint32_t drop_thresh,
+                                     float inv_keep, const typename rawbf<W>::T* pre = nullptr) {
   const int64_t N = p.N;
   TC* C = reinterpret_cast<TC*>(p.C);
   TC* aux = reinterpret_cast<TC*>(p.aux);
@@ -135,59 +163,68 @@ __device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64
   const TC* dsrc = reinterpret_cast<const TC*>(p.dact_src);
   const bool use_drop = drop_thresh != 0u;
   const uint64_t didx = p.offset + (uint64_t)(row * N + col);
-  float a4[4], r4[4], c4[4];
-  // 4-wide vector access needs the leading dimension AND the base pointer aligned to 4 elements
-  constexpr uintptr_t VA = 4 * sizeof(TC) - 1;
-  full4 = full4 && (p.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(C) & VA) == 0;
+  float a[W], r[W], c[W];
+  // W-wide vector access needs the leading dimension AND the base pointer aligned to W elements (16 B suffices
+  // for 8 f32: two float4)
+  constexpr uintptr_t VA = (W * sizeof(TC) > 16 ? 16 : W * sizeof(TC)) - 1;
+  auto vok = [&](int64_t ld, const void* ptr) { return (ld % W) == 0 && (reinterpret_cast<uintptr_t>(ptr) & VA) == 0; };
+  fullw = fullw && vok(p.ldc, C);
   if (p.dact != ICAP_ACT_NONE) {
-    if (pre) unpack_bf16x4(*pre, a4);
-    else if (full4 && (p.ld_dact & 3) == 0 && (reinterpret_cast<uintptr_t>(dsrc) & VA) == 0) vec4io<TC>::ld(dsrc + row * p.ld_dact + col, a4);
-    else for (int e = 0; e < 4; ++e) a4[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
+    if (pre) unpack_bf16(*pre, a);
+    else if (fullw && vok(p.ld_dact, dsrc)) vecio<TC, W>::ld(dsrc + row * p.ld_dact + col, a);
+    else for (int e = 0; e < W; ++e) a[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < W; ++e) {
       float y = p.alpha * x[e];
       if (use_drop) y *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
-      x[e] = y * act_bwd(p.dact, a4[e]);
+      x[e] = y * act_bwd(p.dact, a[e]);
     }
   } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) x[e] = p.alpha * x[e] + bias4[e];
+    for (int e = 0; e < W; ++e) x[e] = p.alpha * x[e] + biasw[e];
     if (p.act != ICAP_ACT_NONE || aux) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < W; ++e) {
         const float y = act_fwd(p.act, x[e]);
-        a4[e] = (p.act == ICAP_ACT_TANH) ? y : x[e];
+        a[e] = (p.act == ICAP_ACT_TANH) ? y : x[e];
         x[e] = y;
       }
       if (aux) {
-        if (full4 && (p.ldaux & 3) == 0 && (reinterpret_cast<uintptr_t>(aux) & VA) == 0) vec4io<TC>::st(aux + row * p.ldaux + col, a4);
-        else for (int e = 0; e < 4; ++e) if (col + e < N) io<TC>::st(aux + row * p.ldaux + col + e, a4[e]);
+        if (fullw && vok(p.ldaux, aux)) vecio<TC, W>::st(aux + row * p.ldaux + col, a);
+        else for (int e = 0; e < W; ++e) if (col + e < N) io<TC>::st(aux + row * p.ldaux + col + e, a[e]);
       }
     }
     if (use_drop) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
+      for (int e = 0; e < W; ++e) x[e] *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
     }
     if (resid) {
-      if (pre) unpack_bf16x4(*pre, r4);
-      else if (full4 && (p.ldr & 3) == 0 && (reinterpret_cast<uintptr_t>(resid) & VA) == 0) vec4io<TC>::ld(resid + row * p.ldr + col, r4);
-      else for (int e = 0; e < 4; ++e) r4[e] = (col + e < N) ? io<TC>::ld(resid + row * p.ldr + col + e) : 0.f;
+      if (pre) unpack_bf16(*pre, r);
+      else if (fullw && vok(p.ldr, resid)) vecio<TC, W>::ld(resid + row * p.ldr + col, r);
+      else for (int e = 0; e < W; ++e) r[e] = (col + e < N) ? io<TC>::ld(resid + row * p.ldr + col + e) : 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] += r4[e];
+      for (int e = 0; e < W; ++e) x[e] += r[e];
     }
   }
   TC* cp = C + row * p.ldc + col;
-  if (full4) {
+  if (fullw) {
     if (p.beta != 0.f) {
-      vec4io<TC>::ld(cp, c4);
+      vecio<TC, W>::ld(cp, c);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] += p.beta * c4[e];
+      for (int e = 0; e < W; ++e) x[e] += p.beta * c[e];
     }
-    vec4io<TC>::st(cp, x);
+    vecio<TC, W>::st(cp, x);
   } else {
-    for (int e = 0; e < 4; ++e)
+    for (int e = 0; e < W; ++e)
       if (col + e < N) io<TC>::st(cp + e, p.beta != 0.f ? x[e] + p.beta * io<TC>::ld(cp + e) : x[e]);
   }
+}
+
+template <typename TC>
+__device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64_t col, float x[4],
+                                     const float bias4[4], bool full4, uint64_t seed, uint32_t drop_thresh,
+                                     float inv_keep) {
+  epiw<TC, 4>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
 }
 
 // Block geometry: WM x WN waves, each owning a (16 TM) x (16 TN) sub-tile of MFMA 16x16 accumulators, so the
@@ -333,18 +370,22 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   // split-K partial slab of this split: raw fp32 [M, N] (N % 4 == 0 is guaranteed by the host)
   float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
 
-  // ---- LDS-staged epilogue: each wave re-reads its accumulators 4 consecutive columns per lane ----
+  // ---- LDS-staged epilogue: each wave re-reads its accumulators EW = 8 consecutive columns per lane, so every
+  // global access of the epilogue is 16 bytes (bf16) — the store tail is issue-bound (cdna_hip_programming.md T21)
   float* cs = reinterpret_cast<float*>(smem) + wave * (EPR * ELD);
-  constexpr int LPR = 4 * TN;       // lanes per staged row (4 columns each)
+  constexpr int EW = 8;
+  constexpr int LPR = 16 * TN / EW;  // lanes per staged row (EW columns each)
   constexpr int RPI = 64 / LPR;     // rows per wave instruction
   const int er = lane / LPR;
-  const int ec = (lane - er * LPR) * 4;
+  const int ec = (lane - er * LPR) * EW;
   const int64_t col = n0 + wn * 16 * TN + ec;
-  const bool full4 = col + 4 <= N;
-  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool fullw = col + EW <= N;
+  float biasw[EW];
+#pragma unroll
+  for (int e = 0; e < EW; ++e) biasw[e] = 0.f;
   if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
+    for (int e = 0; e < EW; ++e) biasw[e] = (col + e < N) ? p.bias[col + e] : 0.f;
   }
   // Prefetch of the epilogue's input operand (bf16 C: dact_src in the backward form, resid in the forward form):
   // the rows this lane stores, issued before the LDS staging (all of them, or in two halves at 4 blocks/CU) so one
@@ -355,19 +396,20 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   constexpr int NPG = MINB >= 4 && NH >= 2 ? 2 : 1;  // prefetch groups: half the rows at a time at 128 VGPRs
   constexpr int HPG = NH / NPG;                  // passes per prefetch group
   constexpr int NEP = HPG * (EPR / RPI);         // prefetched rows held at once
-  uint2 pre[NEP];
+  typedef typename rawbf<EW>::T pre_t;
+  pre_t pre[NEP];
   bool want_pre = false;  // block-uniform: this launch has a bf16 dact_src / resid operand
   const bf16_t* esrc = nullptr;
   int64_t eld = 0;
   const int64_t rb = m0 + wm * 16 * TM + er;  // row of (pass h, row t) = rb + h EPR + t RPI
   auto prefetch = [&](auto gc) __attribute__((always_inline)) {  // rows of passes [g HPG, g HPG + HPG)
     constexpr int g = decltype(gc)::value;
-    if (want_pre && full4) {
+    if (want_pre && fullw) {
 #pragma unroll
       for (int i = 0; i < NEP; ++i) {
         const int64_t r0 = rb + (int64_t)(g * NEP + i) * RPI;
         const int64_t row = r0 < Mv ? r0 : Mv - 1;
-        pre[i] = *reinterpret_cast<const uint2*>(esrc + row * eld + col);
+        pre[i] = *reinterpret_cast<const pre_t*>(esrc + row * eld + col);
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the loads here: hipcc would sink each to its use
@@ -382,8 +424,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
         eld = p.ldr;
       }
     }
-    want_pre = esrc != nullptr && (eld & 3) == 0 && (reinterpret_cast<uintptr_t>(esrc) & 7) == 0 &&
-               (p.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(p.C) & 7) == 0;
+    want_pre = esrc != nullptr && (eld % EW) == 0 && (reinterpret_cast<uintptr_t>(esrc) & 15) == 0 &&
+               (p.ldc % EW) == 0 && (reinterpret_cast<uintptr_t>(p.C) & 15) == 0;
     prefetch(std::integral_constant<int, 0>{});
   }
   if (NST == 1) __syncthreads();  // the single stage buffer is still being read by other waves
@@ -398,14 +440,22 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
         for (int v = 0; v < 4; ++v)
           cs[(ii * 16 + fg * 4 + v) * ELD + j * 16 + fr] = acc[(EPR / 16) * h + ii][j][v];
   };
-  auto store_row = [&](int h, int t, const uint2* pq) __attribute__((always_inline)) {
+  auto store_row = [&](int h, int t, const pre_t* pq) __attribute__((always_inline)) {
     const int lr = t * RPI + er;  // 0..EPR-1
     const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
-    float x[4];
-    *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
+    float x[EW];
+#pragma unroll
+    for (int q = 0; q < EW / 4; ++q)
+      *reinterpret_cast<float4*>(x + 4 * q) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec + 4 * q);
     if (row < Mv && col < N) {
-      if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
-      else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep, pq);
+      if (slab) {  // N % 4 == 0 (host check): whole float4 pieces
+#pragma unroll
+        for (int q = 0; q < EW / 4; ++q)
+          if (col + 4 * q < N)
+            *reinterpret_cast<float4*>(slab + row * N + col + 4 * q) = *reinterpret_cast<const float4*>(x + 4 * q);
+      } else {
+        epiw<TC, EW>(p, row, col, x, biasw, fullw, seed, drop_thresh, inv_keep, pq);
+      }
     }
   };
   if (want_pre || MINB >= 4) {  // (at 4 blocks/CU one path: a second one made the 128-VGPR build spill)
@@ -419,7 +469,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       __syncthreads();
       static_for<0, EPR / RPI>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        store_row(h, t, full4 ? &pre[(h % HPG) * (EPR / RPI) + t] : nullptr);
+        store_row(h, t, fullw ? &pre[(h % HPG) * (EPR / RPI) + t] : nullptr);
       });
       __syncthreads();
     });
