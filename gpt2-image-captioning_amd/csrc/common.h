@@ -52,6 +52,9 @@ template <> struct io<float> {
   static __device__ __forceinline__ void st4(float* p, const float v[4]) {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
+  // 8 consecutive elements (16-byte aligned)
+  static __device__ __forceinline__ void ld8(const float* p, float v[8]) { ld4(p, v); ld4(p + 4, v + 4); }
+  static __device__ __forceinline__ void st8(float* p, const float v[8]) { st4(p, v); st4(p + 4, v + 4); }
 };
 template <> struct io<bf16_t> {
   static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
@@ -63,6 +66,19 @@ template <> struct io<bf16_t> {
   }
   static __device__ __forceinline__ void st4(bf16_t* p, const float v[4]) {
     *reinterpret_cast<uint2*>(p) = make_uint2(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]));
+  }
+  // 8 consecutive elements in one 16-byte access (16-byte aligned)
+  static __device__ __forceinline__ void ld8(const bf16_t* p, float v[8]) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[2 * q] = __uint_as_float(w[q] << 16);
+      v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void st8(bf16_t* p, const float v[8]) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7]));
   }
 };
 

@@ -197,9 +197,208 @@ __global__ __launch_bounds__(1024) void ln_param_reduce(int nblk, int D, const f
   }
 }
 
+// ---- 16-byte variants (D % 8 == 0, 8-aligned strides, 16-byte aligned bases: every GPT-2 / mapper / CLIP LN) --
+// Half a wave per row: 32 lanes x LN8_MAXC chunks of 8 elements, each one 16-byte access (the 4-wide form moves
+// 8 bytes per lane and access; these kernels are access-issue bound, like the GEMM store tail). 8 rows per
+// 256-thread block; the row reductions stay inside the half-wave (xor shuffles 16..1).
+// LN8_MAXC (template): chunks per lane, 3 for D <= 768, 4 for D <= 1024
+
+__device__ __forceinline__ float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T, int LN8_MAXC>
+__global__ __launch_bounds__(256) void ln_fwd8_kernel(int64_t rows, int D, const T* __restrict__ x, int64_t ldx,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     T* __restrict__ y, int64_t ldy, float* mean_out,
+                                                     float* rstd_out, const int32_t* __restrict__ y_rowmap) {
+  const int hl = threadIdx.x & 31;
+  const int64_t nr = (int64_t)gridDim.x * 8;
+  const int D8 = D >> 3;
+  const float invD = 1.f / (float)D;
+  for (int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); r < rows; r += nr) {
+    float v[LN8_MAXC][8];
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < LN8_MAXC; ++t) {
+      const int g = hl + 32 * t;
+      if (g < D8) {
+        io<T>::ld8(x + r * ldx + 8 * g, v[t]);
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) s += v[t][e] + v[t][e + 1];
+      }
+    }
+    const float mean = half_sum(s) * invD;
+    float s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < LN8_MAXC; ++t) {
+      const int g = hl + 32 * t;
+      if (g < D8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = v[t][e] - mean;
+          s2 += d * d;
+        }
+      }
+    }
+    const float rs = 1.f / sqrtf(half_sum(s2) * invD + eps);
+    const int64_t yr = y_rowmap ? (int64_t)y_rowmap[r] : r;
+#pragma unroll
+    for (int t = 0; t < LN8_MAXC; ++t) {
+      const int g = hl + 32 * t;
+      if (g < D8 && yr >= 0) {
+        float gm[8], bt[8], o[8];
+        io<float>::ld8(gamma + 8 * g, gm);
+        io<float>::ld8(beta + 8 * g, bt);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (v[t][e] - mean) * rs * gm[e] + bt[e];
+        io<T>::st8(y + yr * ldy + 8 * g, o);
+      }
+    }
+    if (hl == 0) {
+      if (mean_out) mean_out[r] = mean;
+      if (rstd_out) rstd_out[r] = rs;
+    }
+  }
+}
+
+// PARAMS: accumulate dgamma / dbeta partials (per block, combined by ln_param_reduce); GPT-2's LNs are frozen
+template <typename T, bool PARAMS, int LN8_MAXC>
+__global__ __launch_bounds__(256) void ln_bwd8_kernel(int64_t rows, int D, const T* __restrict__ x, int64_t ldx,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in,
+                                                     const T* __restrict__ dy, int64_t lddy,
+                                                     const T* __restrict__ dres, int64_t lddres,
+                                                     T* __restrict__ dx, int64_t lddx, T* __restrict__ dx_drop,
+                                                     uint32_t thr, float inv_keep, uint64_t seed0,
+                                                     const uint64_t* seed_ptr, uint64_t offset,
+                                                     float* __restrict__ partial,
+                                                     const int32_t* __restrict__ dy_rowmap) {
+  __shared__ float red[PARAMS ? 4 : 1][2][PARAMS ? LN8_MAXC * 256 : 1];  // [wave][dgamma|dbeta][column]
+  const int hl = threadIdx.x & 31;
+  const int wv = threadIdx.x >> 6;
+  const int64_t nr = (int64_t)gridDim.x * 8;
+  const int D8 = D >> 3;
+  const float invD = 1.f / (float)D;
+  const uint64_t seed = thr ? eff_seed(seed0, seed_ptr) : 0ull;
+  float gm[LN8_MAXC][8];
+#pragma unroll
+  for (int t = 0; t < LN8_MAXC; ++t)
+    if (hl + 32 * t < D8) io<float>::ld8(gamma + 8 * (hl + 32 * t), gm[t]);
+  float dg[PARAMS ? LN8_MAXC : 1][8], db[PARAMS ? LN8_MAXC : 1][8];
+  if constexpr (PARAMS) {
+#pragma unroll
+    for (int t = 0; t < LN8_MAXC; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dg[t][e] = db[t][e] = 0.f;
+  }
+  for (int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); r < rows; r += nr) {
+    const float mean = mean_in[r], rs = rstd_in[r];
+    const int64_t dyr = dy_rowmap ? (int64_t)dy_rowmap[r] : r;
+    float xv[LN8_MAXC][8], dv[LN8_MAXC][8], rv[LN8_MAXC][8];
+#pragma unroll
+    for (int t = 0; t < LN8_MAXC; ++t) {
+      const int g = hl + 32 * t;
+      if (g < D8) {
+        io<T>::ld8(x + r * ldx + 8 * g, xv[t]);
+        if (dyr >= 0) io<T>::ld8(dy + dyr * lddy + 8 * g, dv[t]);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dv[t][e] = 0.f;
+        if (dres) io<T>::ld8(dres + r * lddres + 8 * g, rv[t]);
+        else
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rv[t][e] = 0.f;
+      }
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int t = 0; t < LN8_MAXC; ++t) {
+      if (hl + 32 * t < D8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xh = (xv[t][e] - mean) * rs;
+          if constexpr (PARAMS) {
+            dg[t][e] += dv[t][e] * xh;
+            db[t][e] += dv[t][e];
+          }
+          const float gy = dv[t][e] * gm[t][e];
+          s1 += gy;
+          s2 += gy * xh;
+          xv[t][e] = xh;
+          dv[t][e] = gy;
+        }
+      }
+    }
+    const float m1 = half_sum(s1) * invD;
+    const float m2 = half_sum(s2) * invD;
+#pragma unroll
+    for (int t = 0; t < LN8_MAXC; ++t) {
+      const int g = hl + 32 * t;
+      if (g < D8) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = rs * (dv[t][e] - m1 - xv[t][e] * m2) + rv[t][e];
+        io<T>::st8(dx + r * lddx + 8 * g, o);
+        if (dx_drop) {
+          const uint64_t base = offset + (uint64_t)(r * D + 8 * g);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] *= drop_scale(seed, base + e, thr, inv_keep);
+          io<T>::st8(dx_drop + r * lddx + 8 * g, o);
+        }
+      }
+    }
+  }
+  if constexpr (PARAMS) {
+    // the two half-waves of a wave hold the same columns: fold them, then one wave's partial per LDS slot
+#pragma unroll
+    for (int t = 0; t < LN8_MAXC; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dg[t][e] += __shfl_xor(dg[t][e], 32, 64);
+        db[t][e] += __shfl_xor(db[t][e], 32, 64);
+      }
+    if ((threadIdx.x & 63) < 32) {
+#pragma unroll
+      for (int t = 0; t < LN8_MAXC; ++t) {
+        const int g = hl + 32 * t;
+        if (g < D8) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            red[wv][0][8 * g + e] = dg[t][e];
+            red[wv][1][8 * g + e] = db[t][e];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256) {
+      partial[(int64_t)blockIdx.x * 2 * D + c] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+      partial[(int64_t)blockIdx.x * 2 * D + D + c] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    }
+  }
+}
+
 }  // namespace icap
 
 using namespace icap;
+
+// the 16-byte kernels need D % 8 == 0, an 8-element stride and a 16-byte aligned base
+static bool ln8_ok(int32_t dtype, int64_t D, const void* p, int64_t ld) {
+  const int es = dtype == ICAP_BF16 ? 2 : 4;
+  return D % 8 == 0 && ld % 8 == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0 && (D * es) % 16 == 0;
+}
+
+static int ln_blocks8(int64_t rows, int cap) {
+  int64_t b = (rows + 7) / 8;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
 
 static int ln_blocks(int64_t rows, int cap) {
   int64_t b = (rows + 3) / 4;
@@ -216,6 +415,19 @@ extern "C" int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const 
   ICAP_REQUIRE(ldx % 4 == 0 && ldy % 4 == 0, "icap_layernorm_fwd: strides must be multiples of 4");
   if (rows == 0) return ICAP_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (ln8_ok(dtype, D, x, ldx) && ln8_ok(dtype, D, y, ldy)) {
+    const int nb8 = ln_blocks8(rows, 4096);
+#define ICAP_LN_FWD8(T, NC)                                                                                    \
+  hipLaunchKernelGGL((ln_fwd8_kernel<T, NC>), dim3(nb8), dim3(256), 0, s, rows, (int)D, (const T*)x, ldx, gamma, \
+                     beta, eps, (T*)y, ldy, mean, rstd, y_rowmap)
+    if (dtype == ICAP_BF16) {
+      if (D <= 768) ICAP_LN_FWD8(bf16_t, 3); else ICAP_LN_FWD8(bf16_t, 4);
+    } else {
+      if (D <= 768) ICAP_LN_FWD8(float, 3); else ICAP_LN_FWD8(float, 4);
+    }
+#undef ICAP_LN_FWD8
+    return check_launch("icap_layernorm_fwd");
+  }
   const int nb = ln_blocks(rows, 4096);
   if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, rows, (int)D,
@@ -248,7 +460,24 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
   const uint32_t thr = drop_p > 0.f ? drop_threshold(drop_p) : 0u;
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   float* partial = want_params ? reinterpret_cast<float*>(workspace) : nullptr;
-  if (dtype == ICAP_BF16)
+  if (ln8_ok(dtype, D, x, ldx) && ln8_ok(dtype, D, dy, lddy) && ln8_ok(dtype, D, dx, lddx) &&
+      (dres == nullptr || ln8_ok(dtype, D, dres, lddres)) && (dx_drop == nullptr || ln8_ok(dtype, D, dx_drop, lddx))) {
+    // same block count as the partial workspace is sized for (8 rows per block here, 4 in the 4-wide form)
+    const int nb8 = want_params ? nb : ln_blocks8(rows, 4096);
+#define ICAP_LN_BWD8(T, P)                                                                                      \
+  if (D <= 768) ICAP_LN_BWD8N(T, P, 3); else ICAP_LN_BWD8N(T, P, 4)
+#define ICAP_LN_BWD8N(T, P, NC)                                                                                 \
+  hipLaunchKernelGGL((ln_bwd8_kernel<T, P, NC>), dim3(nb8), dim3(256), 0, s, rows, (int)D, (const T*)x, ldx, gamma, \
+                     mean, rstd, (const T*)dy, lddy, (const T*)dres, lddres, (T*)dx, lddx, (T*)dx_drop, thr,     \
+                     inv_keep, seed, seed_ptr, offset, partial, dy_rowmap)
+    if (dtype == ICAP_BF16) {
+      if (want_params) ICAP_LN_BWD8(bf16_t, true); else ICAP_LN_BWD8(bf16_t, false);
+    } else {
+      if (want_params) ICAP_LN_BWD8(float, true); else ICAP_LN_BWD8(float, false);
+    }
+#undef ICAP_LN_BWD8
+#undef ICAP_LN_BWD8N
+  } else if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const bf16_t*)x, ldx,
                        gamma, mean, rstd, (const bf16_t*)dy, lddy, (const bf16_t*)dres, lddres, (bf16_t*)dx,
                        lddx, (bf16_t*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial, dy_rowmap);
