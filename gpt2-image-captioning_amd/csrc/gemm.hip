@@ -1183,6 +1183,16 @@ static int gemm_variant_override() {
   return v;
 }
 
+// 128 x 64 tiles for under-filled bf16 launches: ICAP_GEMM_NARROW=0 disables them, 12 / 13 forces that variant on
+// every bf16 launch with M > 128 (A/B measurements only); unset = automatic (gemm_plan)
+static int gemm_narrow_override() {
+  static const int v = [] {
+    const char* e = getenv("ICAP_GEMM_NARROW");
+    return e ? atoi(e) : -1;
+  }();
+  return v;
+}
+
 // Measured on MI355X (tools/gemm_bench.py, profiles/r01_gemm_variants.txt): short K (<= 16 stages) is bound by the
 // per-block prologue/epilogue, which co-resident blocks hide -> single LDS buffer, 3-4 blocks/CU (4 when the
 // epilogue is heavy); long K favours the double-buffered main loop at 2 blocks/CU.
@@ -1226,8 +1236,21 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.beta == 0.f || p.c_dtype == ICAP_F32, "icap_gemm: beta != 0 requires f32 C");
   ICAP_REQUIRE(p.dact == ICAP_ACT_NONE || p.dact_src != nullptr, "icap_gemm: dact requires dact_src");
   ICAP_REQUIRE(p.drop_p >= 0.f && p.drop_p < 1.f, "icap_gemm: drop_p out of range");
-  const int64_t tiles_m = (p.M + GBM - 1) / GBM, tiles_n = (p.N + GBN - 1) / GBN;
-  const int64_t tiles = tiles_m * tiles_n;
+  const int64_t tiles_m = (p.M + GBM - 1) / GBM;
+  int64_t tiles_n = (p.N + GBN - 1) / GBN;
+  int64_t tiles = tiles_m * tiles_n;
+  // Short-K launches (<= 16 stages) of fewer than 4 tiles of 128 x 128 per CU (the N = 768 products, the mapper's
+  // M = 3200 and CLIP's M = 6400 ones) run faster on 128 x 64 tiles: twice the blocks, so a CU holds more of them
+  // to hide each one's prologue / epilogue; longer K keeps 128 x 128 (profiles/r01_gemm_narrow.txt).
+  const int narrow_env = gemm_narrow_override();
+  const int64_t nk_all = (p.K + 128 / (p.in_dtype == ICAP_BF16 ? 2 : 4) - 1) / (128 / (p.in_dtype == ICAP_BF16 ? 2 : 4));
+  const bool narrow = p.in_dtype == ICAP_BF16 && p.M > 128 && narrow_env != 0 &&
+                      (narrow_env > 0 || (tiles < 1024 && nk_all <= 16 && gemm_variant_override() < 0));
+  const int narrow_variant = narrow_env > 1 ? narrow_env : (tiles < 256 ? 12 : 13);
+  if (narrow) {
+    tiles_n = (p.N + 63) / 64;
+    tiles = tiles_m * tiles_n;
+  }
   ICAP_REQUIRE(tiles < (1ll << 26), "icap_gemm: too many tiles");
   ICAP_REQUIRE(p.split_k >= 0, "icap_gemm: split_k must be >= 0");
   pl.thr = p.drop_p > 0.f ? drop_threshold(p.drop_p) : 0u;
@@ -1268,6 +1291,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   pl.splits = (int)splits;
   pl.nk_split = (int)nk_split;
   pl.variant = gemm_variant(p, nk_split);
+  if (narrow) pl.variant = narrow_variant;
   pl.tiles_n = (int)tiles_n;
   pl.block = dim3(GNT);
   pl.grid = dim3((unsigned)(tiles * splits));
@@ -1300,6 +1324,8 @@ static const char* variant_kernel(int v) {
     case 0: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4>";
     case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4>";
     case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4>";
+    case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2>";
+    case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2>";
     case 6: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 8, 4>";
     case 7: return "gemm2b_kernel<%s, %s, 2, 2, 2, 4, 4>";
     case 8: return "gemm2b_kernel<%s, %s, 1, 2, 4, 8, 4>";
@@ -1364,7 +1390,15 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     case 9: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 4, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
     default: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
   }
-  if (pl.variant == 10 || pl.variant == 11) {  // bf16 inputs (the plan falls back to variant 0 otherwise)
+  if (pl.variant == 12 || pl.variant == 13) {  // 128 x 64 (bf16 inputs only)
+    if (p.c_dtype == ICAP_BF16) {
+      if (pl.variant == 12) hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 3, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 1, 4, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    } else {
+      if (pl.variant == 12) hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 3, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 1, 4, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    }
+  } else if (pl.variant == 10 || pl.variant == 11) {  // bf16 inputs (the plan falls back to variant 0 otherwise)
     if (pl.variant == 10) {
       if (p.c_dtype == ICAP_BF16) hipLaunchKernelGGL((gemm8p_kernel<bf16_t, 256>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
       else hipLaunchKernelGGL((gemm8p_kernel<float, 256>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
