@@ -227,6 +227,31 @@ __device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64
   epiw<TC, 4>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
 }
 
+// ---- K-outer operand images (trans_ab): [64 k-rows][128 columns] bf16, 256-byte rows, 16-byte chunk ch of row r
+// stored at chunk ch ^ kout_swz(r) (cdna_hip_programming.md T10 layout (b)) so the transposed reads below are
+// at most 2-way bank conflicted.
+__device__ __forceinline__ int kout_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int kout_off(int r, int ch) { return r * 256 + ((ch ^ kout_swz(r)) << 4); }
+typedef short kv4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) kv4s_t* kout_lds_ptr;
+// MFMA 16x16x32 operand (lane: column c0 + (lane & 15)) over k-rows r0..r0+31 of a K-outer image, as two
+// ds_read_b64_tr_b16: lane 4q+p of 16-lane group g addresses row r0 + 4g + q (then + 16), columns 4p..4p+3 of
+// the 16-column block; element j of the result = k-row r0 + 4g + j (j < 4), r0 + 16 + 4g + j - 4 (j >= 4)
+__device__ __forceinline__ uint4 kout_frag(const char* img, int r0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int ch = (c0 >> 3) + (pp >> 1), half = (pp & 1) * 8;
+  const char* a0 = img + kout_off(r0 + 4 * g + q, ch) + half;
+  const char* a1 = img + kout_off(r0 + 16 + 4 * g + q, ch) + half;
+  const kv4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((kout_lds_ptr)(a0));
+  const kv4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((kout_lds_ptr)(a1));
+  uint4 r;
+  r.x = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
+  r.y = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
+  r.z = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
+  r.w = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
+  return r;
+}
+
 // Block geometry: WM x WN waves, each owning a (16 TM) x (16 TN) sub-tile of MFMA 16x16 accumulators, so the
 // block tile is BM = 16 WM TM by BN = 16 WN TN. One pipeline stage holds 128 bytes of K per row (bf16: 64 K,
 // f32: 32 K) for the BM rows of A and the BN rows of B in LDS.
@@ -234,9 +259,16 @@ __device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64
 // buffer, two barriers per K step, latency hidden by MINB co-resident blocks per CU).
 // Configurations in use: 128x128 / 4 waves (NST 1 or 2) and 256x256 / 8 waves (NST 2, 128 KiB, 1 block per CU:
 // 4x the MFMA work per staged byte and per exposed load latency).
-template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN>
+// KOUT: both operands K-outer (icap_gemm_args.trans_ab): A stored [K][lda] (m contiguous), B [K][ldb] — the dW
+// products dY^T X over token rows, read without transposing either. A stage is then 64 k-rows x 128 m (n)
+// columns, 256-byte LDS rows in the T10 (b) XOR image (cdna_hip_programming.md T10), written by LDS-DMA with the
+// swizzle on the source address; fragments come from ds_read_b64_tr_b16 pairs (k order {4g..4g+3, 16+4g..},
+// the same on both operands, so the contraction is unchanged). bf16 inputs, 128 x 128 tiles only.
+template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
                                                                   int nk_split, uint32_t drop_thresh, float inv_keep) {
+  static_assert(!KOUT || (sizeof(TI) == 2 && 16 * WM * TM == 128 && 16 * WN * TN == 128),
+                "K-outer operands: bf16, 128 x 128 tiles");
   constexpr int NW = WM * WN;
   constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
   constexpr int STB = (BM + BN) * GROWB;    // bytes per stage
@@ -273,23 +305,54 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;  // device row count
   if (m0 >= Mv) return;
   // tile-relative buffer descriptors: rows past M / N fall beyond num_records and load zeros
-  const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
-  const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
+  // (K-outer: k-rows past K do; columns past M / N read neighbouring data that only reaches unstored outputs)
+  const char* Ab = reinterpret_cast<const char*>(p.A) + (KOUT ? m0 : m0 * p.lda) * ES;
+  const char* Bb = reinterpret_cast<const char*>(p.B) + (KOUT ? n0 : n0 * p.ldb) * ES;
   const int64_t mrows = Mv - m0 < BM ? Mv - m0 : BM;
   const int64_t nrows = N - n0 < BN ? N - n0 : BN;
-  const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
-  const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
+  // (K-outer: the last row's range ends on a whole 16-byte chunk — the hardware zeroes a dword that crosses
+  // num_records — which lda % 8 == 0, lda >= M keeps inside the allocation)
+  const __amdgpu_buffer_rsrc_t ra_rsrc =
+      make_rsrc(Ab, (uint64_t)(KOUT ? (K - 1) * p.lda + ((mrows + 7) & ~7ll) : (mrows - 1) * p.lda + K) * ES);
+  const __amdgpu_buffer_rsrc_t rb_rsrc =
+      make_rsrc(Bb, (uint64_t)(KOUT ? (K - 1) * p.ldb + ((nrows + 7) & ~7ll) : (nrows - 1) * p.ldb + K) * ES);
   // LDS-DMA staging (buffer_load_dwordx4 ... lds): one wave-instruction writes 1 KiB = 8 LDS rows of
   // 128 B linearly (lane l -> row l>>3, physical chunk l&7). The XOR swizzle therefore goes on the SOURCE:
   // physical chunk pc of row r holds logical K-chunk pc ^ (r & 7) (cdna_hip_programming.md §5.4 rule 21).
   const int lrow = lane >> 3;
   const int lchunk = ((lane & 7) ^ lrow) * EPC;  // logical K offset (elements) of this lane's 16 B
   uint32_t a_off[APW], b_off[BPW];
+  if constexpr (KOUT) {
+    // one wave-instruction = 4 k-rows of 256 B: lane l -> row 4 i' + (l >> 4), physical chunk l & 15 holding
+    // logical chunk (l & 15) ^ kout_swz(row)
+    const int krow = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < APW; ++i) a_off[i] = (uint32_t)(((wave * APW + i) * 8 + lrow) * p.lda + lchunk) * ES;
+    for (int i = 0; i < APW; ++i) {
+      const int row = (wave * APW + i) * 4 + krow;
+      a_off[i] = (uint32_t)(row * p.lda + (((lane & 15) ^ kout_swz(row)) << 3)) * ES;
+    }
 #pragma unroll
-  for (int i = 0; i < BPW; ++i) b_off[i] = (uint32_t)(((wave * BPW + i) * 8 + lrow) * p.ldb + lchunk) * ES;
+    for (int i = 0; i < BPW; ++i) {
+      const int row = (wave * BPW + i) * 4 + krow;
+      b_off[i] = (uint32_t)(row * p.ldb + (((lane & 15) ^ kout_swz(row)) << 3)) * ES;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < APW; ++i) a_off[i] = (uint32_t)(((wave * APW + i) * 8 + lrow) * p.lda + lchunk) * ES;
+#pragma unroll
+    for (int i = 0; i < BPW; ++i) b_off[i] = (uint32_t)(((wave * BPW + i) * 8 + lrow) * p.ldb + lchunk) * ES;
+  }
   auto load_stage = [&](int64_t k0, int s) {
+    if constexpr (KOUT) {  // k-rows past K lie beyond num_records (zeros)
+      char* As = smem + s * STB;
+      char* Bs = As + BM * GROWB;
+      const uint32_t ka = (uint32_t)(k0 * p.lda * ES), kb2 = (uint32_t)(k0 * p.ldb * ES);
+#pragma unroll
+      for (int i = 0; i < APW; ++i) dma16(ra_rsrc, As + (wave * APW + i) * 8 * GROWB, a_off[i] + ka);
+#pragma unroll
+      for (int i = 0; i < BPW; ++i) dma16(rb_rsrc, Bs + (wave * BPW + i) * 8 * GROWB, b_off[i] + kb2);
+      return;
+    }
     const uint32_t kb = (uint32_t)(k0 * ES);
     const bool kin = k0 + lchunk < K;
     char* As = smem + s * STB;
@@ -314,6 +377,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
 
   auto read_frags = [&](const char* As, uint4 (&af)[2][TM], uint4 (&bfr)[2][TN]) {
     const char* Bs = As + BM * GROWB;
+    if constexpr (KOUT) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[ks][i] = kout_frag(As, ks * 32, wm * 16 * TM + i * 16, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[ks][j] = kout_frag(Bs, ks * 32, wn * 16 * TN + j * 16, lane);
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + fg;
@@ -1225,9 +1298,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16, "icap_gemm: bad in_dtype");
   ICAP_REQUIRE(p.c_dtype == ICAP_F32 || p.c_dtype == ICAP_BF16, "icap_gemm: bad c_dtype");
   const int epc = p.in_dtype == ICAP_BF16 ? 8 : 4;
-  ICAP_REQUIRE(p.K % epc == 0, "icap_gemm: K must be a multiple of 8 (bf16) / 4 (f32)");
+  ICAP_REQUIRE(p.trans_ab || p.K % epc == 0, "icap_gemm: K must be a multiple of 8 (bf16) / 4 (f32)");
   ICAP_REQUIRE(p.lda % epc == 0 && p.ldb % epc == 0, "icap_gemm: lda/ldb must be multiples of 8 (bf16) / 4 (f32)");
-  ICAP_REQUIRE(p.lda >= p.K && p.ldb >= p.K && p.ldc >= p.N, "icap_gemm: leading dimension too small");
+  ICAP_REQUIRE((p.trans_ab || (p.lda >= p.K && p.ldb >= p.K)) && p.ldc >= p.N, "icap_gemm: leading dimension too small");
   ICAP_REQUIRE((reinterpret_cast<uintptr_t>(p.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.B) & 15) == 0,
                "icap_gemm: A and B must be 16-byte aligned");
   const int es = p.in_dtype == ICAP_BF16 ? 2 : 4;
@@ -1236,6 +1309,13 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.beta == 0.f || p.c_dtype == ICAP_F32, "icap_gemm: beta != 0 requires f32 C");
   ICAP_REQUIRE(p.dact == ICAP_ACT_NONE || p.dact_src != nullptr, "icap_gemm: dact requires dact_src");
   ICAP_REQUIRE(p.drop_p >= 0.f && p.drop_p < 1.f, "icap_gemm: drop_p out of range");
+  if (p.trans_ab) {
+    ICAP_REQUIRE(p.in_dtype == ICAP_BF16, "icap_gemm: trans_ab needs bf16 inputs");
+    ICAP_REQUIRE(p.lda >= p.M && p.ldb >= p.N, "icap_gemm: trans_ab needs lda >= M, ldb >= N");
+    ICAP_REQUIRE(p.m_dev == nullptr, "icap_gemm: trans_ab does not take m_dev");
+    ICAP_REQUIRE((int64_t)(p.K + 64) * p.lda * 2 < 0x7fffffffll && (int64_t)(p.K + 64) * p.ldb * 2 < 0x7fffffffll,
+                 "icap_gemm: trans_ab operands must stay below 2 GiB");
+  }
   const int64_t tiles_m = (p.M + GBM - 1) / GBM;
   int64_t tiles_n = (p.N + GBN - 1) / GBN;
   int64_t tiles = tiles_m * tiles_n;
@@ -1244,7 +1324,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // to hide each one's prologue / epilogue; longer K keeps 128 x 128 (profiles/r01_gemm_narrow.txt).
   const int narrow_env = gemm_narrow_override();
   const int64_t nk_all = (p.K + 128 / (p.in_dtype == ICAP_BF16 ? 2 : 4) - 1) / (128 / (p.in_dtype == ICAP_BF16 ? 2 : 4));
-  const bool narrow = p.in_dtype == ICAP_BF16 && p.M > 128 && narrow_env != 0 &&
+  const bool narrow = p.in_dtype == ICAP_BF16 && p.M > 128 && narrow_env != 0 && !p.trans_ab &&
                       (narrow_env > 0 || (tiles < 1024 && nk_all <= 16 && gemm_variant_override() < 0));
   const int narrow_variant = narrow_env > 1 ? narrow_env : (tiles < 256 ? 12 : 13);
   if (narrow) {
@@ -1255,7 +1335,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.split_k >= 0, "icap_gemm: split_k must be >= 0");
   pl.thr = p.drop_p > 0.f ? drop_threshold(p.drop_p) : 0u;
   pl.inv_keep = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
-  if (p.M <= 128 && p.split_k == 0 && tiles <= 128 && gemm_variant_override() < 0) {
+  if (p.M <= 128 && p.split_k == 0 && tiles <= 128 && gemm_variant_override() < 0 && !p.trans_ab) {
     pl.skinny = true;
     pl.nt = p.N > 1536 ? 2 : 1;  // 32-column slabs once there are enough of them
     pl.grid = dim3((unsigned)((p.N + 16 * pl.nt - 1) / (16 * pl.nt)), (unsigned)((p.M + 31) / 32));
@@ -1292,6 +1372,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   pl.nk_split = (int)nk_split;
   pl.variant = gemm_variant(p, nk_split);
   if (narrow) pl.variant = narrow_variant;
+  if (p.trans_ab) pl.variant = nk_split > 16 ? 14 : 15;  // K-outer forms of variants 0 / 4
   pl.tiles_n = (int)tiles_n;
   pl.block = dim3(GNT);
   pl.grid = dim3((unsigned)(tiles * splits));
@@ -1325,6 +1406,8 @@ static const char* variant_kernel(int v) {
     case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4>";
     case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4>";
     case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2>";
+    case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true>";
+    case 15: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true>";
     case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2>";
     case 6: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 8, 4>";
     case 7: return "gemm2b_kernel<%s, %s, 2, 2, 2, 4, 4>";
@@ -1390,7 +1473,15 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     case 9: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 4, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
     default: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
   }
-  if (pl.variant == 12 || pl.variant == 13) {  // 128 x 64 (bf16 inputs only)
+  if (pl.variant == 14 || pl.variant == 15) {  // K-outer operands (bf16 inputs only)
+    if (p.c_dtype == ICAP_BF16) {
+      if (pl.variant == 14) hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 2, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 1, 3, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    } else {
+      if (pl.variant == 14) hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 2, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 1, 3, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    }
+  } else if (pl.variant == 12 || pl.variant == 13) {  // 128 x 64 (bf16 inputs only)
     if (p.c_dtype == ICAP_BF16) {
       if (pl.variant == 12) hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 3, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
       else hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 1, 4, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);

@@ -42,6 +42,7 @@ class GemmArgs(C.Structure):
         ("seed_ptr", vp),
         ("workspace", vp), ("workspace_bytes", i64), ("split_k", i32),
         ("m_dev", vp),
+        ("trans_ab", i32),
     ]
 
 

@@ -30,9 +30,15 @@ def _rup(x: int, m: int) -> int:
 # --------------------------------------------------------------------------- dW helper
 
 
+def _kout_ok(t: Tensor) -> bool:
+    """K-outer GEMM operand requirements: 16-byte aligned base, row stride a multiple of 8 elements."""
+    return t.data_ptr() % 16 == 0 and t.stride(0) % 8 == 0 and t.stride(-1) == 1
+
+
 class DWHelper:
-    """dW[N,K] += dY[M,N]^T . X[M,K] on the MFMA GEMM: both operands are transposed into K(=M)-contiguous
-    scratch (M padded to 64 with zeros) first, then one C = A.B^T product accumulates into the fp32 grad."""
+    """dW[N,K] += dY[M,N]^T . X[M,K] on the MFMA GEMM. bf16: one K-outer product (trans_ab) straight from dY
+    and X; fp32 (parity mode): both operands are transposed into K(=M)-contiguous scratch (M padded to 64 with
+    zeros) first, then one C = A.B^T product accumulates into the fp32 grad."""
 
     def __init__(self, dtype: torch.dtype, device, max_rows: int, max_cols: int, ln_rows: int, ln_D: int,
                  colsum_cols: int = 0):
@@ -54,6 +60,13 @@ class DWHelper:
            transpose_out: bool = False) -> None:
         N = dY.shape[1] if N is None else N
         K = X.shape[1] if K is None else K
+        if self.dtype == torch.bfloat16 and _kout_ok(dY) and _kout_ok(X):
+            # bf16: one K-outer GEMM reads dY and X in place (icap_gemm_args.trans_ab), no transposes
+            if transpose_out:
+                ops.gemm(X, dY, out, beta=1.0, M=K, N=N, K=M, trans_ab=True)
+            else:
+                ops.gemm(dY, X, out, beta=1.0, M=N, N=K, K=M, trans_ab=True)
+            return
         Mp = _rup(M, 64)
         a = self._t(self.tA, dY, M, N, Mp)  # [N][Mp]
         b = self._t(self.tB, X, M, K, Mp)   # [K][Mp]

@@ -69,15 +69,23 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          aux: Optional[Tensor] = None, dact: int = L.ACT_NONE, dact_src: Optional[Tensor] = None,
          resid: Optional[Tensor] = None, alpha: float = 1.0, beta: float = 0.0, drop: Dropout = NO_DROP,
          M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None,
-         alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None) -> Tensor:
+         alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None,
+         trans_ab: bool = False) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
+    trans_ab: A and B are K-outer ([K, M] / [K, N] row-major: out = epi(alpha * A^T @ B)), bf16 only.
     alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).
     split_k: 0 = automatic split-K for launches of <= 64 output tiles, 1 = never, > 1 = forced.
     m_dev: device int32 row count <= M (rows past it are neither computed nor stored)."""
-    M = A.shape[0] if M is None else M
-    K = A.shape[1] if K is None else K
-    N = B.shape[0] if N is None else N
+    if trans_ab:
+        M = A.shape[1] if M is None else M
+        K = A.shape[0] if K is None else K
+        N = B.shape[1] if N is None else N
+    else:
+        M = A.shape[0] if M is None else M
+        K = A.shape[1] if K is None else K
+        N = B.shape[0] if N is None else N
     a = GemmArgs()
+    a.trans_ab = 1 if trans_ab else 0
     a.M, a.N, a.K = M, N, K
     a.in_dtype = dtype_code(A.dtype)
     a.c_dtype = dtype_code(out.dtype)
@@ -106,7 +114,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
         name = L.load().icap_gemm_kernel_name(C.byref(a))  # the instantiation rocprofv3 will name
         key = (name.decode() if name else "?",
                f"{M}x{N}x{K} act{act} dact{dact} drop{int(drop.p > 0)} res{int(resid is not None)} "
-               f"aux{int(aux is not None)} beta{beta:g}{' m_dev' if m_dev is not None else ''}")
+               f"aux{int(aux is not None)} beta{beta:g}{' m_dev' if m_dev is not None else ''}"
+               f"{' kout' if trans_ab else ''}")
         GEMM_TIMER.launch(key, 2.0 * M * N * K if alg_flops is None else alg_flops,
                           lambda: call("icap_gemm", C.byref(a), _stream()))
     return out

@@ -93,6 +93,10 @@ typedef struct {
   /* computed and stored; the launch geometry stays sized for M, so a graph   */
   /* captured once serves every count (LM head over the compacted targets).   */
   const int32_t* m_dev;
+  /* trans_ab != 0: both operands K-outer — A stored [K][lda] (element (m,k) at A[k*lda+m]), B stored      */
+  /* [K][ldb] — the weight-gradient products dW = dY^T X over token rows (src/train.py:145 backward of   */
+  /* every nn.Linear / Conv1D) without transposing either operand. bf16 inputs, lda >= M, ldb >= N.    */
+  int32_t trans_ab;
 } icap_gemm_args;
 /* name of the kernel instantiation icap_gemm launches for these arguments    */
 /* (as rocprofv3 prints it, minus the parameter list); NULL on invalid args.   */

@@ -33,7 +33,11 @@ def accesses(name, args):
     if name == "icap_gemm":
         g = a[0]._obj
         ei, ec = ES[g.in_dtype], ES[g.c_dtype]
-        out += [("A", g.A, _rows(g.M, g.lda, g.K, ei)), ("B", g.B, _rows(g.N, g.ldb, g.K, ei)),
+        if g.trans_ab:  # K-outer operands: [K][lda] / [K][ldb]
+            out += [("A", g.A, _rows(g.K, g.lda, g.M, ei)), ("B", g.B, _rows(g.K, g.ldb, g.N, ei))]
+        else:
+            out += [("A", g.A, _rows(g.M, g.lda, g.K, ei)), ("B", g.B, _rows(g.N, g.ldb, g.K, ei))]
+        out += [
                 ("C", g.C, _rows(g.M, g.ldc, g.N, ec)), ("bias", g.bias, g.N * 4),
                 ("aux", g.aux, _rows(g.M, g.ldaux, g.N, ec)), ("dact_src", g.dact_src, _rows(g.M, g.ld_dact, g.N, ec)),
                 ("resid", g.resid, _rows(g.M, g.ldr, g.N, ec)), ("seed_ptr", g.seed_ptr, 8),

@@ -128,6 +128,24 @@ def test_gemm_split_k_matches_single_pass(dev, dtype):
     assert rel_err(outs[3][1], z + bias.double()) < tol
 
 
+@pytest.mark.parametrize("M,N,K", [(768, 3072, 3200), (200, 72, 100), (130, 200, 64), (768, 768, 128), (3, 5, 7)])
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+def test_gemm_trans_ab(dev, M, N, K, cdt):
+    """K-outer operands (dW = dY^T X over token rows): out = beta*out + alpha * A[K,M]^T B[K,N], strided A."""
+    lda = (M + 7) // 8 * 8 + 8
+    A = rnd((K, lda), dev, torch.bfloat16, seed=41)[:, :M]
+    B = rnd((K, N + (8 - N % 8) % 8), dev, torch.bfloat16, seed=42)[:, :N]
+    C0 = rnd((M, N), dev, cdt, seed=43)
+    beta = 1.0 if cdt == torch.float32 else 0.0
+    ref = beta * C0.double() + 0.5 * (A.double().t() @ B.double())
+    scale = (A.double().abs().t() @ B.double().abs()) * 0.5 + beta * C0.double().abs() + 1e-30
+    for sk in ((0, 3) if cdt == torch.float32 else (0,)):
+        C = C0.clone()
+        ops.gemm(A, B, C, alpha=0.5, beta=beta, trans_ab=True, split_k=sk)
+        err = ((C.double() - ref).abs() / scale).max().item()
+        assert err < (1e-5 if cdt == torch.float32 else 8e-3), (sk, err)
+
+
 def test_gemm_dropout_statistics(dev):
     M, N, K = 512, 512, 64
     A = torch.ones((M, K), device=dev)
