@@ -1385,6 +1385,16 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
     const int64_t tm2 = (p.M + 255) / 256;
     pl.grid = dim3((unsigned)(tm2 * tiles_n * splits));
     pl.block = dim3(512);
+  } else if (pl.variant == 16 || pl.variant == 17) {  // 8 waves of 64 x 64: 256 x 128 / 128 x 256 (bf16 only)
+    if (p.in_dtype != ICAP_BF16) {
+      pl.variant = 0;
+    } else {
+      const int bm = pl.variant == 16 ? 256 : 128, bn = pl.variant == 16 ? 128 : 256;
+      const int64_t tm2 = (p.M + bm - 1) / bm, tn2 = (p.N + bn - 1) / bn;
+      pl.grid = dim3((unsigned)(tm2 * tn2 * splits));
+      pl.tiles_n = (int)tn2;
+      pl.block = dim3(512);
+    }
   } else if (pl.variant == 10 || pl.variant == 11) {  // phase-interleaved 8-wave: 256x256 / 256x128 (bf16 only)
     if (p.in_dtype != ICAP_BF16) {
       pl.variant = 0;
@@ -1402,14 +1412,16 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
 // "TI, TC, template ints" of each variant (keep in sync with ICAP_GEMM_LAUNCH)
 static const char* variant_kernel(int v) {
   switch (v) {
-    case 0: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4>";
-    case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4>";
-    case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4>";
-    case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2>";
+    case 0: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, false>";
+    case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, false>";
+    case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4, false>";
+    case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2, false>";
     case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true>";
+    case 16: return "gemm_kernel<%s, %s, 2, 1, 4, 2, 4, 4, false>";
+    case 17: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 4, 4, false>";
     case 15: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true>";
-    case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2>";
-    case 6: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 8, 4>";
+    case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2, false>";
+    case 6: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 8, 4, false>";
     case 7: return "gemm2b_kernel<%s, %s, 2, 2, 2, 4, 4>";
     case 8: return "gemm2b_kernel<%s, %s, 1, 2, 4, 8, 4>";
     case 9: return "gemm3b_kernel<%s, %s, 1, 4, 2, 4, 4>";
@@ -1480,6 +1492,14 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     } else {
       if (pl.variant == 14) hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 2, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
       else hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 1, 3, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    }
+  } else if (pl.variant == 16 || pl.variant == 17) {  // 256 x 128 / 128 x 256, 8 waves (bf16 inputs only)
+    if (p.c_dtype == ICAP_BF16) {
+      if (pl.variant == 16) hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 1, 4, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 1, 2, 4, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    } else {
+      if (pl.variant == 16) hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 1, 4, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 1, 2, 4, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
     }
   } else if (pl.variant == 12 || pl.variant == 13) {  // 128 x 64 (bf16 inputs only)
     if (p.c_dtype == ICAP_BF16) {
