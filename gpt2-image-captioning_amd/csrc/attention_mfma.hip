@@ -340,8 +340,7 @@ __device__ __forceinline__ uint4 trfrag(const bf16_t* base, int r0, int c0, int 
 }
 
 template <int HD>
-__global__ __launch_bounds__(HD == 64 ? 1024 : 512) void bwd2_kernel(icap_attn_args p, Geo g, uint32_t thr,
-                                                                     float inv_keep) {
+__global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint32_t thr, float inv_keep) {
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
   constexpr int LDR = HD + 8;
   constexpr int NKS = HD / 32;  // 32-deep k steps over the head dim
@@ -356,7 +355,7 @@ __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void bwd2_kernel(icap_attn_a
   bf16_t* Qs = sm;
   bf16_t* Ks = Qs + Sp * LDR;
   bf16_t* Vs = Ks + Sp * LDR;
-  bf16_t* dOs = Vs + Sp * LDR;
+  bf16_t* dOs = Vs + g.Sp16 * LDR;  // V is only read by 16-row tiles below Sp16 (skipped past it in the dQ loop)
   float* lse_s = reinterpret_cast<float*>(dOs + Sp * LDR);
   float* delta_s = lse_s + Sp;
   const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
@@ -380,7 +379,7 @@ __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void bwd2_kernel(icap_attn_a
     }
     *reinterpret_cast<uint4*>(Qs + r * LDR + 8 * c) = q;
     *reinterpret_cast<uint4*>(Ks + r * LDR + 8 * c) = k;
-    *reinterpret_cast<uint4*>(Vs + r * LDR + 8 * c) = v;
+    if (r < g.Sp16) *reinterpret_cast<uint4*>(Vs + r * LDR + 8 * c) = v;
     *reinterpret_cast<uint4*>(dOs + r * LDR + 8 * c) = d;
   }
   // delta[q] = sum_d dO[q][d] O[q][d], one thread per query in a fixed order (deterministic)
@@ -463,9 +462,12 @@ __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void bwd2_kernel(icap_attn_a
             make_uint2(f2bf2(dv[dt][0], dv[dt][1]), f2bf2(dv[dt][2], dv[dt][3]));
       }
     }
-  } else if (wave < 2 * nt) {
+  }
+  // one wave per 16-row tile runs both roles in turn (nt waves per block: 120 VGPRs and a 54 KB LDS image fit
+  // three blocks per CU, where a wave per role held one 2 nt-wave block per CU)
+  if (wave < nt) {
     // ---- dQ for queries [16 qt, 16 qt + 16): accumulators C[key][q] (lane = query, rows = 4 keys)
-    const int qt = wave - nt;
+    const int qt = wave;
     const int q = qt * 16 + fr;
     uint4 qf[NKS], of[NKS];
 #pragma unroll
@@ -484,10 +486,12 @@ __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void bwd2_kernel(icap_attn_a
       for (int sub = 0; sub < 2; ++sub) {
         const int kt = 2 * kp + sub;
         f32x4_t st = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dpt = st;
+        if (kt < nt) {  // key tiles past Sp16 are all padding (and V holds no rows for them)
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          st = mfma(rowfrag<LDR>(Ks, kt * 16, ks * 32, lane), qf[ks], st);
-          dpt = mfma(rowfrag<LDR>(Vs, kt * 16, ks * 32, lane), of[ks], dpt);
+          for (int ks = 0; ks < NKS; ++ks) {
+            st = mfma(rowfrag<LDR>(Ks, kt * 16, ks * 32, lane), qf[ks], st);
+            dpt = mfma(rowfrag<LDR>(Vs, kt * 16, ks * 32, lane), of[ks], dpt);
+          }
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
@@ -651,7 +655,7 @@ static bool mfma_fwd2_ok(const icap_attn_args* a) {
 }
 
 size_t mfma_bwd2_lds(const amfma::Geo& g) {
-  return 2 * 4 * (size_t)g.Sp32 * (g.hd + 8) + 2 * sizeof(float) * (size_t)g.Sp32;
+  return 2 * (3 * (size_t)g.Sp32 + (size_t)g.Sp16) * (g.hd + 8) + 2 * sizeof(float) * (size_t)g.Sp32;
 }
 
 // v2 backward: needs O (delta), 16-byte aligned row segments, and 2 * Sp16/16 waves within the launch bound
@@ -661,8 +665,8 @@ static bool mfma_bwd2_ok(const icap_attn_args* a) {
        reinterpret_cast<uintptr_t>(a->dout) | reinterpret_cast<uintptr_t>(a->dqkv)) & 15)
     return false;
   const amfma::Geo g = mfma_geo(a);
-  const int waves = 2 * (g.Sp16 / 16);
-  return waves * 64 <= (a->hd == 64 ? 1024 : 512) && mfma_bwd2_lds(g) <= 160 * 1024;
+  const int waves = g.Sp16 / 16;
+  return waves * 64 <= 512 && mfma_bwd2_lds(g) <= 160 * 1024;
 }
 
 bool mfma_attention_ok(const icap_attn_args* a, bool bwd) {
@@ -705,7 +709,7 @@ int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float
   } else {
     if (mfma_bwd2_ok(a)) {
       const size_t lds2 = mfma_bwd2_lds(g);
-      const dim3 block2((unsigned)(64 * 2 * (g.Sp16 / 16)));
+      const dim3 block2((unsigned)(64 * (g.Sp16 / 16)));
       if (a->hd == 64) {
         static bool once = (lds_limit(amfma::bwd2_kernel<64>), true); (void)once;
         hipLaunchKernelGGL(amfma::bwd2_kernel<64>, grid, block2, lds2, s, *a, g, thr, inv_keep);
