@@ -146,6 +146,36 @@ def test_gemm_trans_ab(dev, M, N, K, cdt):
         assert err < (1e-5 if cdt == torch.float32 else 8e-3), (sk, err)
 
 
+@pytest.mark.parametrize("transpose_out", [False, True])
+def test_dw_helper_kout_matches_transpose_path(dev, transpose_out):
+    """mapper DWHelper.dW (src/train.py:145 weight grads): the bf16 K-outer product equals dY^T X (fp64) and
+    the transpose-then-NT path it replaced, accumulating into the existing fp32 grad."""
+    from icap.mapper import DWHelper, _kout_ok
+
+    M, N, K = 3200, 768, 3072
+    dY = rnd((M, N), dev, torch.bfloat16, seed=51)
+    X = rnd((M, K), dev, torch.bfloat16, seed=52)
+    shape = (K, N) if transpose_out else (N, K)
+    g0 = rnd(shape, dev, seed=53)
+    ref = g0.double() + (X.double().t() @ dY.double() if transpose_out else dY.double().t() @ X.double())
+    h = DWHelper(torch.bfloat16, dev, max_rows=M, max_cols=K, ln_rows=M, ln_D=N)
+    assert _kout_ok(dY) and _kout_ok(X)
+    g1 = g0.clone()
+    h.dW(dY, X, g1, M=M, transpose_out=transpose_out)
+    scale = (X.double().abs().t() @ dY.double().abs() if transpose_out else dY.double().abs().t() @ X.double().abs())
+    assert ((g1.double() - ref).abs() / (scale + g0.double().abs())).max().item() < 1e-5
+    # the transpose path (fp32 parity mode's route) on the same bf16 operands
+    g2 = g0.clone()
+    Mp = (M + 63) // 64 * 64
+    a = h._t(h.tA, dY, M, N, Mp)
+    b = h._t(h.tB, X, M, K, Mp)
+    if transpose_out:
+        ops.gemm(b, a, g2, beta=1.0, M=K, N=N, K=Mp)
+    else:
+        ops.gemm(a, b, g2, beta=1.0, M=N, N=K, K=Mp)
+    assert ((g1.double() - g2.double()).abs() / (scale + g0.double().abs())).max().item() < 1e-5
+
+
 def test_gemm_dropout_statistics(dev):
     M, N, K = 512, 512, 64
     A = torch.ones((M, K), device=dev)
