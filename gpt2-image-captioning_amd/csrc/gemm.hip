@@ -1116,6 +1116,29 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int ti
 // fragments in flight each (range-checked buffer loads straight from HBM/L2). The fp32 partial tiles are reduced
 // through LDS in two rounds before the shared epilogue. One launch, no slabs.
 // Accumulators use the C layout (lane = column, 4 consecutive rows per lane).
+// one 16-byte A chunk -> LayerNorm-ed chunk in the input dtype
+template <typename TI>
+__device__ __forceinline__ uint4 ln_chunk(const uint4 a, float mean, float rs, const float* g, const float* bt);
+template <>
+__device__ __forceinline__ uint4 ln_chunk<bf16_t>(const uint4 a, float mean, float rs, const float* g, const float* bt) {
+  const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float v0 = (__uint_as_float(w[q] << 16) - mean) * rs * g[2 * q] + bt[2 * q];
+    const float v1 = (__uint_as_float(w[q] & 0xffff0000u) - mean) * rs * g[2 * q + 1] + bt[2 * q + 1];
+    o[q] = f2bf2(v0, v1);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+template <>
+__device__ __forceinline__ uint4 ln_chunk<float>(const uint4 a, float mean, float rs, const float* g, const float* bt) {
+  return make_uint4(__float_as_uint((__uint_as_float(a.x) - mean) * rs * g[0] + bt[0]),
+                    __float_as_uint((__uint_as_float(a.y) - mean) * rs * g[1] + bt[1]),
+                    __float_as_uint((__uint_as_float(a.z) - mean) * rs * g[2] + bt[2]),
+                    __float_as_uint((__uint_as_float(a.w) - mean) * rs * g[3] + bt[3]));
+}
+
 constexpr int SK_WAVES = 8;
 template <typename TI, typename TC, int NT, int MT>
 __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_args p, uint32_t drop_thresh,
@@ -1146,6 +1169,42 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  // LayerNorm-fused A (icap_gemm_args.ln_gamma): mean / rstd of the block's rows over all K, 16 threads per row,
+  // two passes (the formula and rounding of ln_fwd8_kernel: (x - mean) * rstd * gamma + beta -> input dtype)
+  // (computed after the first k-steps' operand loads are issued, so their latency overlaps it)
+  __shared__ float ln_mr[BM][2];
+  const bool fuse_ln = p.ln_gamma != nullptr;
+  auto ln_stats = [&]() {
+    const int t = threadIdx.x & 15;
+    for (int rr = threadIdx.x >> 4; rr < BM; rr += 64 * SK_WAVES / 16) {
+      const int64_t row = m0 + rr < M ? m0 + rr : M - 1;
+      const TI* xr = reinterpret_cast<const TI*>(p.A) + row * p.lda;
+      float s = 0.f;
+      for (int64_t k = (int64_t)t * EPC; k < K; k += 16 * EPC) {
+        float v[EPC];
+        if constexpr (EPC == 8) io<TI>::ld8(xr + k, v); else io<TI>::ld4(xr + k, v);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) s += v[e];
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      const float mean = s / (float)K;
+      float s2 = 0.f;
+      for (int64_t k = (int64_t)t * EPC; k < K; k += 16 * EPC) {
+        float v[EPC];
+        if constexpr (EPC == 8) io<TI>::ld8(xr + k, v); else io<TI>::ld4(xr + k, v);
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) s2 += (v[e] - mean) * (v[e] - mean);
+      }
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+      if (t == 0) {
+        ln_mr[rr][0] = mean;
+        ln_mr[rr][1] = 1.f / sqrtf(s2 / (float)K + p.ln_eps);
+      }
+    }
+    __syncthreads();
+  };
   // rows past M / N lie beyond the descriptor range (zero-filled); K-tail chunks and steps past the end are
   // redirected out of range (zero fragments: the MFMAs on them add nothing)
   uint32_t aoff[MT], boff[NT];
@@ -1154,8 +1213,8 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
 #pragma unroll
   for (int j = 0; j < NT; ++j) boff[j] = (uint32_t)(((j * 16 + fr) * p.ldb + fg * EPC) * ES);
   const int64_t nks = (K + KSTEP - 1) / KSTEP;
-  for (int64_t base = wave; base < nks; base += SK_WAVES * SK_U) {
-    uint4 af[SK_U][MT], bfr[SK_U][NT];
+  uint4 af[SK_U][MT], bfr[SK_U][NT];
+  auto load_steps = [&](int64_t base) {  // steps past the end load zero fragments (the MFMAs add nothing)
 #pragma unroll
     for (int u = 0; u < SK_U; ++u) {
       const int64_t k0 = (base + (int64_t)u * SK_WAVES) * KSTEP;
@@ -1166,15 +1225,39 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
 #pragma unroll
       for (int i = 0; i < MT; ++i) af[u][i] = bload(ra, kin ? aoff[i] + kb : OOB);
     }
+  };
+  // every wave runs at least one (possibly all-zero) pass, so the LN-stats barrier below is block-uniform
+  load_steps(wave);
+  if (fuse_ln) ln_stats();
+  for (int64_t base = wave;;) {
     // all SK_U steps' loads are issued before the first MFMA waits (without this fence hipcc sinks each load
     // to its use and every MFMA waits out a full memory latency)
     __builtin_amdgcn_sched_barrier(0);
+    if (fuse_ln) {
+#pragma unroll
+      for (int u = 0; u < SK_U; ++u) {
+        const int64_t k0 = (base + (int64_t)u * SK_WAVES) * KSTEP + fg * EPC;
+        if (k0 < K) {  // K-tail / past-the-end chunks stay zero
+          float g[EPC], bt[EPC];
+          if constexpr (EPC == 8) { io<float>::ld8(p.ln_gamma + k0, g); io<float>::ld8(p.ln_beta + k0, bt); }
+          else { io<float>::ld4(p.ln_gamma + k0, g); io<float>::ld4(p.ln_beta + k0, bt); }
+#pragma unroll
+          for (int i = 0; i < MT; ++i) {
+            const float mean = ln_mr[i * 16 + fr][0], rs = ln_mr[i * 16 + fr][1];
+            af[u][i] = ln_chunk<TI>(af[u][i], mean, rs, g, bt);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int u = 0; u < SK_U; ++u)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) mfma_chunk<TI>(acc[i][j], af[u][i], bfr[u][j]);
+    base += SK_WAVES * SK_U;
+    if (base >= nks) break;
+    load_steps(base);
   }
   // round 1: waves [HALF, 2 HALF) park their partials, waves [0, HALF) add them; round 2: the HALF sums -> LDS
   auto park = [&](float* dst) {
@@ -1339,7 +1422,11 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.split_k >= 0, "icap_gemm: split_k must be >= 0");
   pl.thr = p.drop_p > 0.f ? drop_threshold(p.drop_p) : 0u;
   pl.inv_keep = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
-  if (p.M <= 128 && p.split_k == 0 && tiles <= 128 && gemm_variant_override() < 0 && !p.trans_ab) {
+  const bool fuse_ln = p.ln_gamma != nullptr;
+  ICAP_REQUIRE(!fuse_ln || (p.ln_beta && p.M <= 128 && p.split_k == 0 && !p.trans_ab && p.K <= 4096),
+               "icap_gemm: ln_gamma needs ln_beta, M <= 128, K <= 4096, no split_k / trans_ab");
+  if (p.M <= 128 && p.split_k == 0 && (tiles <= 128 || fuse_ln) && (gemm_variant_override() < 0 || fuse_ln) &&
+      !p.trans_ab) {
     pl.skinny = true;
     pl.nt = p.N > 1536 ? 2 : 1;  // 32-column slabs once there are enough of them
     pl.grid = dim3((unsigned)((p.N + 16 * pl.nt - 1) / (16 * pl.nt)), (unsigned)((p.M + 31) / 32));

@@ -43,6 +43,7 @@ class GemmArgs(C.Structure):
         ("workspace", vp), ("workspace_bytes", i64), ("split_k", i32),
         ("m_dev", vp),
         ("trans_ab", i32),
+        ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
     ]
 
 

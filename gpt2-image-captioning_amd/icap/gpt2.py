@@ -490,17 +490,26 @@ class GPT2Core:
         B = ds.B
         scale = 1.0 / math.sqrt(hd)
         a, o, h1, f = ds.a[:rows], ds.o[:rows], ds.h1[:rows], ds.f[:rows]
+        # per-token steps (rows = B <= 128): ln_1 / ln_2 run inside the QKV / c_fc GEMMs (one launch each
+        # instead of two; the decode step is bound by its ~90 launches, not by bytes)
+        fuse_ln = rows <= 128
         for l, lw in enumerate(self.layers):
-            ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, a, None, None, rows=rows)
             qkv = ds.cache[l][pos0 * B: (pos0 + npos) * B]
-            ops.gemm(a, lw.w_attn_t, qkv, bias=lw.b_attn, M=rows)
+            if fuse_ln:
+                ops.gemm(x, lw.w_attn_t, qkv, bias=lw.b_attn, M=rows, ln=(lw.ln1_g, lw.ln1_b, self.eps))
+            else:
+                ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, a, None, None, rows=rows)
+                ops.gemm(a, lw.w_attn_t, qkv, bias=lw.b_attn, M=rows)
             if prefill:
                 ops.attention_fwd(ds.cache[l], o, B=B, S=npos, H=H, hd=hd, scale=scale, causal=True, rsb=1, rss=B)
             else:
                 ops.attention_decode(ds.cache[l], o, B=B, H=H, hd=hd, pos=pos0, scale=scale)
             ops.gemm(o, lw.w_proj_t, h1, bias=lw.b_proj, resid=x, M=rows)
-            ops.layernorm_fwd(h1, lw.ln2_g, lw.ln2_b, self.eps, a, None, None, rows=rows)
-            ops.gemm(a, lw.w_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows)
+            if fuse_ln:
+                ops.gemm(h1, lw.w_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows, ln=(lw.ln2_g, lw.ln2_b, self.eps))
+            else:
+                ops.layernorm_fwd(h1, lw.ln2_g, lw.ln2_b, self.eps, a, None, None, rows=rows)
+                ops.gemm(a, lw.w_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows)
             ops.gemm(f, lw.w_mp_t, x, bias=lw.b_mp, resid=h1, M=rows)
 
     def _decode_head(self, ds, x_last: Tensor, step: int, pos_next: int):

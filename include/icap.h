@@ -97,6 +97,10 @@ typedef struct {
   /* [K][ldb] — the weight-gradient products dW = dY^T X over token rows (src/train.py:145 backward of   */
   /* every nn.Linear / Conv1D) without transposing either operand. bf16 inputs, lda >= M, ldb >= N.    */
   int32_t trans_ab;
+  /* ln_gamma != NULL: A is replaced by LayerNorm(A) over its K columns first (row mean / variance, eps,    */
+  /* then * ln_gamma[k] + ln_beta[k], rounded to the input dtype) — the decode step's ln_1 / ln_2 fused    */
+  /* into the QKV / c_fc GEMMs (HF/models/gpt2/modeling_gpt2.py:281,301). Only for M <= 128 launches.     */
+  const float* ln_gamma; const float* ln_beta; float ln_eps;
 } icap_gemm_args;
 /* name of the kernel instantiation icap_gemm launches for these arguments    */
 /* (as rocprofv3 prints it, minus the parameter list); NULL on invalid args.   */

@@ -41,7 +41,8 @@ def accesses(name, args):
                 ("C", g.C, _rows(g.M, g.ldc, g.N, ec)), ("bias", g.bias, g.N * 4),
                 ("aux", g.aux, _rows(g.M, g.ldaux, g.N, ec)), ("dact_src", g.dact_src, _rows(g.M, g.ld_dact, g.N, ec)),
                 ("resid", g.resid, _rows(g.M, g.ldr, g.N, ec)), ("seed_ptr", g.seed_ptr, 8),
-                ("workspace", g.workspace, g.workspace_bytes), ("m_dev", g.m_dev, 4)]
+                ("workspace", g.workspace, g.workspace_bytes), ("m_dev", g.m_dev, 4),
+                ("ln_gamma", g.ln_gamma, g.K * 4), ("ln_beta", g.ln_beta, g.K * 4)]
     elif name in ("icap_attention_fwd", "icap_attention_bwd"):
         t = a[0]._obj
         es = ES[t.dtype]

@@ -176,6 +176,28 @@ def test_dw_helper_kout_matches_transpose_path(dev, transpose_out):
     assert ((g1.double() - g2.double()).abs() / (scale + g0.double().abs())).max().item() < 1e-5
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N", [(128, 2304), (7, 3072), (128, 40)])
+def test_gemm_fused_layernorm(dev, dtype, M, N):
+    """decode-step ln_1 / ln_2 fused into the skinny GEMM == layernorm_fwd then GEMM (modeling_gpt2.py:281,301)."""
+    K = 768
+    x = rnd((M, K), dev, dtype, 2.0, seed=61) + 0.3
+    g = rnd((K,), dev, seed=62) * 0.2 + 1
+    b = rnd((K,), dev, seed=63) * 0.1
+    W = rnd((N, K), dev, dtype, 0.05, seed=64)
+    bias = rnd((N,), dev, scale=0.1, seed=65)
+    y = torch.empty((M, K), device=dev, dtype=dtype)
+    ops.layernorm_fwd(x, g, b, 1e-5, y, None, None)
+    ref = torch.empty((M, N), device=dev, dtype=dtype)
+    ops.gemm(y, W, ref, bias=bias, act=L.ACT_GELU_NEW)
+    out = torch.empty_like(ref)
+    ops.gemm(x, W, out, bias=bias, act=L.ACT_GELU_NEW, ln=(g, b, 1e-5))
+    # fp32: the same arithmetic up to the stats' summation order; bf16: plus an occasional 1-ulp rounding flip
+    # of a normalised input
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel_err(out, ref) < tol
+
+
 def test_gemm_dropout_statistics(dev):
     M, N, K = 512, 512, 64
     A = torch.ones((M, K), device=dev)
