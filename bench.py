@@ -143,6 +143,37 @@ def greedy_rate(model, Bd, dev, world):
     return caps_per_s, dt, nd, lens
 
 
+def preprocess_rate(dev):
+    """CLIP image preprocessing: device (icap_clip_preprocess, Pillow-exact) vs the host
+    PIL processor on the same decoded 480x640 RGB images; images/s (JPEG decode excluded on both sides)."""
+    import numpy as np
+
+    from icap import ops
+    from icap.clip import CLIPProcessor
+
+    rng = np.random.default_rng(3)
+    ims = [rng.integers(0, 256, (480, 640, 3), dtype=np.uint8) for _ in range(32)]
+    nd = 256
+    batch = [ims[i % len(ims)] for i in range(nd)]
+    ops.clip_preprocess(batch[:8], dev)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        ops.clip_preprocess(batch, dev)
+    torch.cuda.synchronize()
+    dev_rate = 3 * nd / (time.perf_counter() - t0)
+    from PIL import Image
+
+    pil = [Image.fromarray(a) for a in ims[:16]]
+    proc = CLIPProcessor()
+    t0 = time.perf_counter()
+    proc(pil)
+    host_rate = len(pil) / (time.perf_counter() - t0)
+    return {"device_images_per_s": round(dev_rate, 1), "host_pil_images_per_s": round(host_rate, 1),
+            "image": "480x640 RGB uint8 -> 3x224x224 fp32 (shortest-edge bicubic, centre crop, normalise)",
+            "device_includes": "host packing + H2D copy of the uint8 pixels + 2 kernels"}
+
+
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (tools/pmc_traffic.sh writes
     profiles/*pmc_traffic.json from separate FETCH_SIZE / WRITE_SIZE passes over this bench's train step).
@@ -238,6 +269,7 @@ def main():
     if not args.no_decode:
         caps_per_s, dt, nd, lens = greedy_rate(model, Bd, dev, world)
     traffic, traffic_src = pmc_traffic(dom)
+    prep = None if args.no_decode else preprocess_rate(dev)
 
     if rank == 0:
         res = {
@@ -256,6 +288,7 @@ def main():
             "greedy_captions_per_s": round(caps_per_s, 1) if caps_per_s else None,
             "greedy": {"batch_per_gpu": Bd, "decode_steps": 50, "returned_len": lens[-1], "kv_cache": True,
                        "ms_per_batch": round(dt / nd * 1e3, 3) if dt else None},
+            "clip_preprocess": prep,
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1),
                          "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
                          "traffic": traffic, "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE)",

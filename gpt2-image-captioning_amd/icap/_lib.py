@@ -111,6 +111,7 @@ SIGNATURES = {
     "icap_l2norm_rows": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, vp]),
     "icap_greedy_next": (C.c_int, [i32, i32, i64, vp, i64, i64, vp, vp, vp, i64, i32, vp, vp, i32, i32, vp, vp]),
     "icap_add_position": (C.c_int, [i32, i32, i32, i32, vp, i64, i64, vp, i32, vp, vp]),
+    "icap_clip_preprocess": (C.c_int, [i32, vp, vp, i32, i32, vp, vp, vp, vp, vp]),
 }
 
 _lib = None

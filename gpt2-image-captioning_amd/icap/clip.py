@@ -287,6 +287,15 @@ def _load_state(path: str):
     return {k: v for k, v in sd.items() if k.startswith("vision_model.") or k == "visual_projection.weight"}
 
 
+def resize_shortest_edge(wh, size: int):
+    """(width, height) after CLIPImageProcessor's shortest-edge resize: short side -> size, long side ->
+    int(size * long / short) (HF image_transforms.get_resize_output_image_size, default_to_square=False)."""
+    w, h = wh
+    short, long = (w, h) if w <= h else (h, w)
+    new_long = int(size * long / short)
+    return (size, new_long) if w <= h else (new_long, size)
+
+
 class CLIPProcessor:
     """Host-side CLIPImageProcessor equivalent: shortest-edge resize (bicubic) to 224, centre crop, /255,
     mean/std normalise -> fp32 [B,3,224,224]. (Device-side preprocessing is SURVEY.md §8f rank 1: later.)"""
@@ -303,9 +312,7 @@ class CLIPProcessor:
         out = []
         for im in images:
             im = im.convert("RGB")
-            w, h = im.size
-            s = self.size / min(w, h)
-            im = im.resize((max(self.size, round(w * s)), max(self.size, round(h * s))), Image.BICUBIC)
+            im = im.resize(resize_shortest_edge(im.size, self.size), Image.BICUBIC)
             w, h = im.size
             left, top = (w - self.size) // 2, (h - self.size) // 2
             im = im.crop((left, top, left + self.size, top + self.size))
@@ -313,6 +320,25 @@ class CLIPProcessor:
             a = (a - np.array(CLIP_MEAN, np.float32)) / np.array(CLIP_STD, np.float32)
             out.append(torch.from_numpy(a.transpose(2, 0, 1).copy()))
         return SimpleNamespace(pixel_values=torch.stack(out))
+
+
+class DeviceCLIPProcessor(CLIPProcessor):
+    """CLIPProcessor with the resize / crop / normalise on the GPU (icap_clip_preprocess; Pillow-exact):
+    the host only decodes to RGB uint8. pixel_values come back on `device`."""
+
+    def __init__(self, size: int = 224, device=None):
+        super().__init__(size)
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+
+    def __call__(self, images, return_tensors: str = "pt"):
+        import numpy as np
+
+        from . import ops
+
+        if not isinstance(images, (list, tuple)):
+            images = [images]
+        arrs = [np.asarray(im.convert("RGB")) if hasattr(im, "convert") else np.asarray(im) for im in images]
+        return SimpleNamespace(pixel_values=ops.clip_preprocess(arrs, self.device, self.size, self.size))
 
 
 @torch.no_grad()

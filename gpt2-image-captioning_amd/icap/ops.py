@@ -364,3 +364,64 @@ def embedding_scatter_add(dx: Tensor, ids: Tensor, dwte: Tensor, *, B: int, P: i
     call("icap_embedding_scatter_add", dtype_code(dx.dtype), B, P, L_, D, dx.data_ptr(), ids.data_ptr(),
          dwte.data_ptr(), _stream())
     return dwte
+
+
+# ---------------------------------------------------------------------------------------------- CLIP input
+def _pillow_window(in_size: int, out_size: int, xx: int):
+    """Pillow Resample.c precompute_coeffs window of output index xx: (xmin, taps) (same double math)."""
+    scale = in_size / out_size
+    filterscale = max(scale, 1.0)
+    support = 2.0 * filterscale
+    center = (xx + 0.5) * scale
+    xmin = max(int(center - support + 0.5), 0)
+    xmax = min(int(center + support + 0.5), in_size)
+    return xmin, xmax - xmin
+
+
+def clip_preprocess_geometry(sizes, size: int = 224, crop: int = 224):
+    """Per image (h, w): the int64 geo row icap_clip_preprocess takes, and the tmp rows it needs."""
+    from .clip import resize_shortest_edge
+
+    geo, src_off, tmp_off = [], 0, 0
+    for h, w in sizes:
+        new_w, new_h = resize_shortest_edge((w, h), size)
+        if new_w < crop or new_h < crop:
+            raise L.IcapError(f"clip_preprocess: resized {new_w}x{new_h} is smaller than the {crop} crop")
+        top, left = (new_h - crop) // 2, (new_w - crop) // 2
+        if new_h == h:
+            y_first, rows = top, crop
+        else:
+            y_first = _pillow_window(h, new_h, top)[0]
+            lo, n = _pillow_window(h, new_h, top + crop - 1)
+            rows = lo + n - y_first
+        geo.append([src_off, h, w, new_h, new_w, top, left, tmp_off, y_first, rows])
+        src_off += h * w * 3
+        tmp_off += rows * crop * 3
+    return geo, tmp_off
+
+
+def clip_preprocess(images, device, size: int = 224, crop: int = 224, mean=None, std=None) -> Tensor:
+    """Decoded RGB uint8 images ([H, W, 3] numpy / torch, any sizes) -> fp32 [n, 3, crop, crop] on `device`,
+    equal to CLIPImageProcessor(images).pixel_values (src/embeddings/clip.py:129; PIL-backed HF processor)."""
+    import numpy as np
+
+    from .clip import CLIP_MEAN, CLIP_STD
+
+    arrs = [np.ascontiguousarray(np.asarray(im, dtype=np.uint8)) for im in images]
+    for a in arrs:
+        if a.ndim != 3 or a.shape[2] != 3:
+            raise L.IcapError("clip_preprocess: images must be RGB uint8 [H, W, 3]")
+    n = len(arrs)
+    out = torch.empty((n, 3, crop, crop), dtype=torch.float32, device=device)
+    if n == 0:
+        return out
+    geo, tmp_bytes = clip_preprocess_geometry([a.shape[:2] for a in arrs], size, crop)
+    max_rows = max(g[9] for g in geo)
+    px = torch.from_numpy(np.concatenate([a.reshape(-1) for a in arrs])).to(device, non_blocking=True)
+    geo_t = torch.tensor(geo, dtype=torch.int64).to(device, non_blocking=True)
+    tmp = torch.empty(tmp_bytes, dtype=torch.uint8, device=device)
+    m = torch.tensor(CLIP_MEAN if mean is None else mean, dtype=torch.float32).to(device)
+    s = torch.tensor(CLIP_STD if std is None else std, dtype=torch.float32).to(device)
+    call("icap_clip_preprocess", n, px.data_ptr(), geo_t.data_ptr(), crop, max_rows, tmp.data_ptr(), m.data_ptr(),
+         s.data_ptr(), out.data_ptr(), _stream())
+    return out

@@ -292,6 +292,20 @@ int icap_add_position(int32_t dtype, int32_t B, int32_t npos, int32_t D, const v
                       int64_t src_bstride, int64_t src_tstride, const void* wpe, int32_t pos0,
                       void* x, void* stream);
 
+/* ------------------------------------------------------------------------- */
+/* CLIP image preprocessing: the reference's           */
+/* CLIPImageProcessor (src/embeddings/clip.py:129 -> HF image_processing_clip:*/
+/* shortest-edge PIL-BICUBIC resize, centre crop, x 1/255, (x - mean) / std) */
+/* for n decoded RGB uint8 HWC images packed in `pixels`. geo: device int64  */
+/* [n][10] = {src_off, in_h, in_w, new_h, new_w, top, left, tmp_off, y_first, */
+/* tmp_rows} (icap/ops.py clip_preprocess computes it); tmp: uint8 scratch of */
+/* sum(tmp_rows) * crop * 3 bytes; out: fp32 [n][3][crop][crop]. Pillow's    */
+/* fixed-point two-pass resampler, bit-exact.                                 */
+/* ------------------------------------------------------------------------- */
+int icap_clip_preprocess(int32_t n, const uint8_t* pixels, const int64_t* geo, int32_t crop,
+                         int32_t max_tmp_rows, uint8_t* tmp, const float* mean, const float* stdv,
+                         float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
