@@ -628,6 +628,115 @@ __global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint
   }
 }
 
+// Forward v3 for sequences past the 8 register-resident key tiles of v2 (ViT-L/14: S = 257): the same K/V LDS
+// images and S^T / O^T accumulator layouts, with the keys walked in chunks of 8 tiles under an online softmax
+// (running max / sum per query, O^T rescaled per lane since lane = query), and each wave looping over query
+// tiles. P is exponentiated against the running max, rounded to bf16 unnormalised, and O is divided by the
+// final sum; lse = max + log(sum) as in v2, so the backward recomputes the same probabilities.
+template <int HD>
+__global__ __launch_bounds__(HD == 64 ? 1024 : 512) void fwd3_kernel(icap_attn_args p, Geo g, uint32_t thr, float inv_keep) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
+  constexpr int LDR = HD + 8;
+  constexpr int NKS = HD / 32;
+  constexpr int NDT = HD / 16;
+  constexpr int CPR = HD / 8;
+  const int Sp = g.Sp32, S = g.S;
+  const int bh = blockIdx.x;
+  const int b = bh / g.H, h = bh - b * g.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  bf16_t* Ks = sm;
+  bf16_t* Vs = Ks + Sp * LDR;
+  const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
+  for (int idx = threadIdx.x; idx < Sp * CPR; idx += blockDim.x) {
+    const int r = idx / CPR, c = idx - r * CPR;
+    uint4 k = make_uint4(0, 0, 0, 0), v = k;
+    if (r < S) {
+      const bf16_t* src = qkv + trow(g, b, r) * p.ld_qkv + g.D + h * HD + 8 * c;
+      k = *reinterpret_cast<const uint4*>(src);
+      v = *reinterpret_cast<const uint4*>(src + g.D);
+    }
+    *reinterpret_cast<uint4*>(Ks + r * LDR + 8 * c) = k;
+    *reinterpret_cast<uint4*>(Vs + r * LDR + 8 * c) = v;
+  }
+  __syncthreads();
+  const int nqt = g.Sp16 >> 4;
+  const int nkt = Sp >> 4;  // key tiles incl. the zero rows up to Sp32 (pairs stay whole)
+  const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
+  const uint64_t dbase = p.offset + (uint64_t)bh * S * S;
+  for (int qt = wave; qt < nqt; qt += nw) {
+    const int q = qt * 16 + fr;
+    uint4 qf[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) qf[ks] = gfrag(qkv, p.ld_qkv, h * HD, g, b, qt * 16, ks * 32, lane);
+    const int klim = p.causal ? (qt * 16 + 16 < S ? qt * 16 + 16 : S) : S;  // keys past it are all masked
+    float m = -INFINITY, l = 0.f;
+    f32x4_t o[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) o[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < nkt && c0 * 16 < klim; c0 += MAXKT) {
+      f32x4_t st[MAXKT];
+      float mc = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < MAXKT; ++t) {
+        st[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        if (c0 + t < nkt) {
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks) st[t] = mfma(rowfrag<LDR>(Ks, (c0 + t) * 16, ks * 32, lane), qf[ks], st[t]);
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int key = (c0 + t) * 16 + 4 * fg + v;
+          const float x = (c0 + t < nkt && key_ok(p.causal, p.key_mask, g, b, q, key)) ? st[t][v] * p.scale : -INFINITY;
+          st[t][v] = x;
+          mc = fmaxf(mc, x);
+        }
+      }
+      mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+      mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+      const float mn = fmaxf(m, mc);
+      const float alpha = (m == -INFINITY) ? 0.f : __expf(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) o[dt][v] *= alpha;
+#pragma unroll
+      for (int kp = 0; kp < MAXKT / 2; ++kp) {
+        if (c0 + 2 * kp < nkt) {
+          float pv[8];
+#pragma unroll
+          for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const int key = (c0 + 2 * kp + sub) * 16 + 4 * fg + v;
+              float e = (m == -INFINITY) ? 0.f : __expf(st[2 * kp + sub][v] - m);
+              l += e;
+              if (thr && q < S && key < S) e *= drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
+              pv[sub * 4 + v] = e;
+            }
+          uint4 xp;
+          xp.x = f2bf2(pv[0], pv[1]); xp.y = f2bf2(pv[2], pv[3]); xp.z = f2bf2(pv[4], pv[5]); xp.w = f2bf2(pv[6], pv[7]);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) o[dt] = mfma(trfrag<LDR>(Vs, (c0 / 2 + kp) * 32, dt * 16, lane), xp, o[dt]);
+        }
+      }
+    }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    if (fg == 0 && q < S && p.lse) p.lse[(int64_t)bh * S + q] = l > 0.f ? m + logf(l) : -INFINITY;
+    if (q < S) {
+      bf16_t* rowp = reinterpret_cast<bf16_t*>(p.out) + trow(g, b, q) * p.ld_out + h * HD;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+        *reinterpret_cast<uint2*>(rowp + dt * 16 + 4 * fg) =
+            make_uint2(f2bf2(o[dt][0] * inv, o[dt][1] * inv), f2bf2(o[dt][2] * inv, o[dt][3] * inv));
+    }
+  }
+}
+
 }  // namespace amfma
 
 static inline int rup(int x, int m) { return (x + m - 1) / m * m; }
@@ -669,7 +778,18 @@ static bool mfma_bwd2_ok(const icap_attn_args* a) {
   return waves * 64 <= 512 && mfma_bwd2_lds(g) <= 160 * 1024;
 }
 
+size_t mfma_fwd3_lds(const amfma::Geo& g) { return 2 * 2 * (size_t)g.Sp32 * (g.hd + 8); }
+
+// long-sequence forward (v3): S past 8 key tiles, K/V of the whole sequence in LDS
+static bool mfma_fwd3_ok(const icap_attn_args* a) {
+  if (a->dtype != ICAP_BF16 || (a->hd != 64 && a->hd != 96) || a->S <= 16 * amfma::MAXKT) return false;
+  if ((a->ld_out & 3) || (a->ld_qkv & 7)) return false;
+  if ((reinterpret_cast<uintptr_t>(a->out) & 7) || (reinterpret_cast<uintptr_t>(a->qkv) & 15)) return false;
+  return mfma_fwd3_lds(mfma_geo(a)) <= 160 * 1024;
+}
+
 bool mfma_attention_ok(const icap_attn_args* a, bool bwd) {
+  if (!bwd && mfma_fwd3_ok(a)) return true;
   if (a->dtype != ICAP_BF16 || (a->hd != 64 && a->hd != 96) || a->S > 16 * amfma::MAXKT) return false;
   if ((a->ld_qkv & 7) || (bwd && (a->ld_dout & 7))) return false;
   const amfma::Geo g = mfma_geo(a);
@@ -685,6 +805,21 @@ static void lds_limit(K kernel) {
 int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float inv_keep, hipStream_t s) {
   const amfma::Geo g = mfma_geo(a);
   dim3 grid((unsigned)(a->B * a->H)), block(256);
+  if (!bwd && mfma_fwd3_ok(a)) {
+    // waves: the fewest that cover the query tiles in an equal number of passes (at most 16)
+    const int maxw = a->hd == 64 ? 16 : 8;  // (the hd-96 form is built for 512 threads: register budget)
+    const int nqt = g.Sp16 / 16, passes = (nqt + maxw - 1) / maxw;
+    const dim3 block3((unsigned)(64 * ((nqt + passes - 1) / passes)));
+    const size_t lds3 = mfma_fwd3_lds(g);
+    if (a->hd == 64) {
+      static bool once = (lds_limit(amfma::fwd3_kernel<64>), true); (void)once;
+      hipLaunchKernelGGL(amfma::fwd3_kernel<64>, grid, block3, lds3, s, *a, g, thr, inv_keep);
+    } else {
+      static bool once = (lds_limit(amfma::fwd3_kernel<96>), true); (void)once;
+      hipLaunchKernelGGL(amfma::fwd3_kernel<96>, grid, block3, lds3, s, *a, g, thr, inv_keep);
+    }
+    return check_launch("icap_attention_fwd(mfma v3)");
+  }
   if (!bwd && mfma_fwd2_ok(a)) {
     const size_t lds2 = mfma_fwd2_lds(g);
     const dim3 block2((unsigned)(64 * (g.Sp16 / 16)));

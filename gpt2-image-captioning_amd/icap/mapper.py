@@ -43,6 +43,7 @@ class DWHelper:
     def __init__(self, dtype: torch.dtype, device, max_rows: int, max_cols: int, ln_rows: int, ln_D: int,
                  colsum_cols: int = 0):
         self.dtype = dtype
+        self.split_k = 0  # icap_gemm split_k for the K-outer products (0 = automatic)
         self.Mp_max = _rup(max(max_rows, 1), 64)
         self.tA = torch.zeros(max_cols * self.Mp_max, dtype=dtype, device=device)
         self.tB = torch.zeros(max_cols * self.Mp_max, dtype=dtype, device=device)
@@ -63,9 +64,9 @@ class DWHelper:
         if self.dtype == torch.bfloat16 and _kout_ok(dY) and _kout_ok(X):
             # bf16: one K-outer GEMM reads dY and X in place (icap_gemm_args.trans_ab), no transposes
             if transpose_out:
-                ops.gemm(X, dY, out, beta=1.0, M=K, N=N, K=M, trans_ab=True)
+                ops.gemm(X, dY, out, beta=1.0, M=K, N=N, K=M, trans_ab=True, split_k=self.split_k)
             else:
-                ops.gemm(dY, X, out, beta=1.0, M=N, N=K, K=M, trans_ab=True)
+                ops.gemm(dY, X, out, beta=1.0, M=N, N=K, K=M, trans_ab=True, split_k=self.split_k)
             return
         Mp = _rup(M, 64)
         a = self._t(self.tA, dY, M, N, Mp)  # [N][Mp]

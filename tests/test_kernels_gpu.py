@@ -288,6 +288,34 @@ def test_attention(dev, dtype, B, S, H, hd, causal, masked):
         assert rel_err(dqkv, g) < (1e-5 if dtype == torch.float32 else 2e-2)
 
 
+@pytest.mark.parametrize("B,S,H,hd,causal,masked", [(2, 257, 16, 64, False, False), (2, 200, 4, 64, True, True),
+                                                    (1, 300, 4, 96, False, False)])
+def test_attention_long_sequence_forward(dev, B, S, H, hd, causal, masked):
+    """bf16 forward past 8 key tiles (ViT-L/14 at 224 px: S = 257, BASELINE configs[3]): online-softmax MFMA
+    kernel vs the fp64 definition; lse checked against the reference logsumexp."""
+    D = H * hd
+    qkv = rnd((B * S, 3 * D), dev, torch.bfloat16, seed=22)
+    key_mask = None
+    if masked:
+        km = torch.ones((B, S), dtype=torch.int32)
+        km[0, 150:] = 0
+        key_mask = km.to(dev)
+    out = torch.empty((B * S, D), device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * H * S, device=dev)
+    scale = 1.0 / math.sqrt(hd)
+    ops.attention_fwd(qkv, out, B=B, S=S, H=H, hd=hd, scale=scale, causal=causal, key_mask=key_mask, lse=lse)
+    x = qkv.double().view(B, S, 3, H, hd).permute(2, 0, 3, 1, 4)
+    o = ref_attention(x[0], x[1], x[2], scale, causal, key_mask)
+    assert rel_err(out, o.permute(0, 2, 1, 3).reshape(B * S, D)) < 1e-2
+    s_ = torch.einsum("bhqd,bhkd->bhqk", x[0], x[1]) * scale
+    if causal:
+        s_ = s_.masked_fill(torch.ones(S, S, dtype=torch.bool, device=dev).triu(1), float("-inf"))
+    if key_mask is not None:
+        s_ = s_.masked_fill(key_mask[:, None, None, :] == 0, float("-inf"))
+    ref_lse = torch.logsumexp(s_, dim=-1).reshape(-1)
+    assert (lse.double() - ref_lse).abs().max().item() < 2e-2
+
+
 @pytest.mark.parametrize("B,S,H,hd,causal", [(3, 65, 12, 64, True), (2, 25, 8, 96, False), (2, 128, 4, 64, True)])
 def test_attention_bwd_dropout_paths_agree(dev, B, S, H, hd, causal):
     """bf16 backward with attention dropout: the O-based (v2) and the transposing (v1) backward see the same
