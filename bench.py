@@ -66,17 +66,26 @@ class GemmTimer:
         return agg
 
 
-def build(B, dev, dropout=True):
+def build(B, dev, dropout=True, config="small"):
+    """config "small": BASELINE configs[1] (GPT-2 small + CLIP ViT-B/32); "medium": configs[3] (GPT-2 medium +
+    CLIP ViT-L/14 encoder on the device, mapper at gpt_dim 1024 / CLIP-L embed 768)."""
     from types import SimpleNamespace
 
     from icap import CaptionTrainer, GPT2LMHeadModel, ImageCaptioningModel, TransformerMappingNetwork
-    from icap.clip import CLIPVisionTower
+    from icap.clip import CLIPVisionConfig, CLIPVisionTower
+    from icap.gpt2 import GPT2Config
 
-    gpt = GPT2LMHeadModel.random_init(seed=0)
-    mapper = TransformerMappingNetwork.random_init(seed=0)
+    if config == "medium":
+        gpt = GPT2LMHeadModel.random_init(GPT2Config.medium(), seed=0)
+        mapper = TransformerMappingNetwork.random_init(embed_dim=768, gpt_dim=1024, seed=0)
+        tower_cfg = CLIPVisionConfig.vit_l14()
+    else:
+        gpt = GPT2LMHeadModel.random_init(seed=0)
+        mapper = TransformerMappingNetwork.random_init(seed=0)
+        tower_cfg = None
     model = ImageCaptioningModel(mapper, tokenizer=SimpleNamespace(eos_token_id=50256), gpt=gpt,
                                  compute_dtype=torch.bfloat16).to(dev)
-    tower = CLIPVisionTower.random_init(seed=0).to(dev)
+    tower = CLIPVisionTower.random_init(tower_cfg, seed=0).to(dev)
     trainer = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10 ** 6, clip_model=tower, dropout=dropout,
                              seed=1234)
     return model, tower, trainer
@@ -121,10 +130,10 @@ def cpu_baseline(seconds_budget: float = 20.0):
                       f"fwd/bwd + AdamW, dropout 0.1, fp32, torch CPU {cores} threads) in {el:.1f}s"}
 
 
-def greedy_rate(model, Bd, dev, world):
+def greedy_rate(model, Bd, dev, world, edim=512):
     """50-token KV-cached greedy captions/s over a batch of Bd image embeddings (all 50 steps decoded)."""
     g = torch.Generator().manual_seed(5)
-    emb = torch.randn((Bd, 512), generator=g)
+    emb = torch.randn((Bd, edim), generator=g)
     emb = (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
     # one caption = 50 greedy tokens after the 15-token prefix (SURVEY.md §8d): decode all 50 steps (the trained
     # synthetic model emits EOS early; the reference loop would stop there), output identical either way
@@ -203,6 +212,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the greedy-decode measurement (PMC passes)")
+    ap.add_argument("--config", default="small", choices=["small", "medium"],
+                    help="small = BASELINE configs[1] (default, the headline); medium = configs[3]")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -216,7 +227,7 @@ def main():
     torch.cuda.set_device(dev)
     B = args.batch
 
-    model, tower, trainer = build(B, dev)
+    model, tower, trainer = build(B, dev, config=args.config)
     ids, mask, labels, px = synthetic_batch(B, 1 + rank, dev)  # each rank: its own shard of samples
     trainer.load_batch(ids, mask, labels, pixels=px)
     # LM-head target rows of this batch (the device holds the count; the host copy only prices the roofline)
@@ -267,7 +278,7 @@ def main():
     Bd = args.decode_batch
     caps_per_s, dt, nd, lens = None, None, 1, [None]
     if not args.no_decode:
-        caps_per_s, dt, nd, lens = greedy_rate(model, Bd, dev, world)
+        caps_per_s, dt, nd, lens = greedy_rate(model, Bd, dev, world, 768 if args.config == "medium" else 512)
     traffic, traffic_src = pmc_traffic(dom)
     prep = None if args.no_decode else preprocess_rate(dev)
 
@@ -278,9 +289,13 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (seeded COCO-shaped captions: 13 tokens + EOS, padded to 50; randn 224x224 pixels); "
                     "deterministic random-init weights",
-            "config": {"workload": "train step: CLIP ViT-B/32 fwd (frozen) on 224x224 pixels -> transformer mapper "
-                                   "(8 layers, prefix 15, trained) -> GPT-2 small (frozen) fwd + dX bwd, LM head on "
-                                   "the target rows + CE, dropout 0.1, clip_grad_norm 1.0 + AdamW + linear LR",
+            "config": {"workload": ("train step: CLIP ViT-B/32 fwd (frozen) on 224x224 pixels -> transformer mapper "
+                                    "(8 layers, prefix 15, trained) -> GPT-2 small (frozen) fwd + dX bwd, LM head on "
+                                    "the target rows + CE, dropout 0.1, clip_grad_norm 1.0 + AdamW + linear LR")
+                       if args.config == "small" else
+                       ("BASELINE configs[3] train step: CLIP ViT-L/14 fwd (frozen, 257 tokens) on 224x224 pixels -> "
+                        "transformer mapper (8 layers, gpt_dim 1024, trained) -> GPT-2 medium (24 layers, d 1024, "
+                        "frozen) fwd + dX bwd, LM head on the target rows + CE, dropout 0.1, clip 1.0 + AdamW"),
                        "lm_head_rows_per_step": head_rows,
                        "per_gpu_batch": B, "global_batch": B * world, "seq_len": 65, "caption_len": 50,
                        "parallelism": f"dp{world}", "graph": use_graph},
@@ -300,7 +315,7 @@ def main():
                          "timing": "HIP events around every GEMM launch of one eager step on its launch stream "
                                    "(the timed region replays a HIP graph, which cannot host per-kernel events)"},
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.config == "small":
             res["cpu_baseline"] = cpu_baseline()
         print(json.dumps(res), flush=True)
     if dist:

@@ -486,6 +486,27 @@ __global__ void im2col_kernel(int B, int C, int HW, int p, const float* __restri
   }
 }
 
+// any patch size (ViT-L/14: p = 14, C p p = 588): one thread per element of the 8-padded patch row, pad zeros
+template <typename T>
+__global__ void im2col_any_kernel(int B, int C, int HW, int p, int Kp, const float* __restrict__ px,
+                                  T* __restrict__ out) {
+  const int G = HW / p;
+  const int K = C * p * p;
+  const int64_t total = (int64_t)B * G * G * Kp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / Kp;
+    const int col = (int)(i - row * Kp);
+    float v = 0.f;
+    if (col < K) {
+      const int c = col / (p * p), r = col - c * p * p, ky = r / p, kx = r - ky * p;
+      const int64_t b = row / (G * G);
+      const int gy = (int)((row - b * G * G) / G), gx = (int)(row - b * G * G - (int64_t)gy * G);
+      v = px[((b * C + c) * HW + gy * p + ky) * HW + gx * p + kx];
+    }
+    io<T>::st(out + i, v);
+  }
+}
+
 template <typename T>
 __global__ void vit_embed_kernel(int B, int G2, int D, const T* __restrict__ pe, const float* __restrict__ cls,
                                  const float* __restrict__ pos, T* __restrict__ x) {
@@ -828,8 +849,16 @@ extern "C" int icap_broadcast_rows(int32_t dtype, int32_t B, int64_t R, int64_t 
 extern "C" int icap_im2col_patches(int32_t dtype, int32_t B, int32_t C, int32_t HW, int32_t patch, const float* pixels,
                                    void* patches, void* stream) {
   ICAP_REQUIRE(pixels && patches, "icap_im2col_patches: null pointer");
-  ICAP_REQUIRE(patch > 0 && patch % 4 == 0 && HW % patch == 0, "icap_im2col_patches: patch must divide HW and be a multiple of 4");
+  ICAP_REQUIRE(patch > 0 && HW % patch == 0, "icap_im2col_patches: patch must divide HW");
   const int G = HW / patch;
+  const int K = C * patch * patch, Kp = (K + 7) / 8 * 8;
+  if (patch % 4 != 0 || Kp != K) {  // rows of Kp elements (zero pad) so the patch GEMM keeps K % 8 == 0
+    const int64_t n = (int64_t)B * G * G * Kp;
+    if (n == 0) return ICAP_OK;
+    DISPATCH_T(dtype, hipLaunchKernelGGL(im2col_any_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B,
+                                         C, HW, patch, Kp, pixels, TP(patches)));
+    return check_launch("icap_im2col_patches");
+  }
   const int64_t n = (int64_t)B * G * G * C * patch * (patch / 4);
   if (n == 0) return ICAP_OK;
   DISPATCH_T(dtype, hipLaunchKernelGGL(im2col_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B, C, HW,

@@ -189,7 +189,12 @@ class ClipCore:
     @torch.no_grad()
     def refresh(self):
         vm, dt = self.m.vision_model, self.dtype
-        self.w_patch = self._cvt(vm.embeddings.patch_embedding.weight.data)  # [D, C*p*p] (c, ky, kx) order
+        # [D, C*p*p] (c, ky, kx) order, zero-padded to the 8-multiple row of icap_im2col_patches (p = 14: 592)
+        wp = vm.embeddings.patch_embedding.weight.data.reshape(self.D, -1)
+        self.Kp = (wp.shape[1] + 7) // 8 * 8
+        if self.Kp != wp.shape[1]:
+            wp = torch.nn.functional.pad(wp, (0, self.Kp - wp.shape[1]))
+        self.w_patch = self._cvt(wp)
         self.cls = vm.embeddings.class_embedding.data
         self.pos = vm.embeddings.position_embedding.weight.data
         self.pre = (vm.pre_layrnorm.weight.data, vm.pre_layrnorm.bias.data)
@@ -215,7 +220,7 @@ class ClipCore:
         M = B * self.S
         e = lambda *shape, dtype=dt: torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
         ws = SimpleNamespace(B=B, M=M)
-        ws.patches = e(B * self.G * self.G, c.num_channels * c.patch_size * c.patch_size)
+        ws.patches = e(B * self.G * self.G, self.Kp)
         ws.pe = e(B * self.G * self.G, D)
         ws.x, ws.h1, ws.a, ws.o = e(M, D), e(M, D), e(M, D), e(M, D)
         ws.qkv = e(M, 3 * D)

@@ -265,7 +265,8 @@ int icap_broadcast_rows(int32_t dtype, int32_t B, int64_t R, int64_t D, const fl
 /* CLIP ViT image tower helpers (HF/models/clip/modeling_clip.py:148-219,     */
 /* 650-651,751; src/embeddings/clip.py:132-137).                              */
 /* ------------------------------------------------------------------------- */
-/* patches[(b*G*G + gy*G + gx), c*p*p + ky*p + kx] = pixels[b, c, gy*p+ky, gx*p+kx] (fp32 in) */
+/* patches[(b*G*G + gy*G + gx), c*p*p + ky*p + kx] = pixels[b, c, gy*p+ky, gx*p+kx] (fp32 in); */
+/* rows hold round_up(C*p*p, 8) elements, the pad zero (ViT-L/14: 588 -> 592)                 */
 int icap_im2col_patches(int32_t dtype, int32_t B, int32_t C, int32_t HW, int32_t patch,
                         const float* pixels, void* patches, void* stream);
 /* x[b, 0] = cls + pos[0];  x[b, 1+i] = patch_emb[b*G2 + i] + pos[1+i] */

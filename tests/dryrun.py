@@ -119,7 +119,8 @@ def accesses(name, args):
         out.append(("counter", a[0], 8))
     elif name == "icap_im2col_patches":
         dt, B, Cc, HW, p, px, pt, _s = a
-        out += [("pixels", px, B * Cc * HW * HW * 4), ("patches", pt, B * (HW // p) ** 2 * Cc * p * p * ES[dt])]
+        kp = (Cc * p * p + 7) // 8 * 8  # rows padded to a multiple of 8 elements
+        out += [("pixels", px, B * Cc * HW * HW * 4), ("patches", pt, B * (HW // p) ** 2 * kp * ES[dt])]
     elif name == "icap_vit_embed":
         dt, B, G2, D, pe, cls, pos, x, _s = a
         out += [("pe", pe, B * G2 * D * ES[dt]), ("cls", cls, D * 4), ("pos", pos, (G2 + 1) * D * 4),

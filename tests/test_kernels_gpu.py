@@ -198,6 +198,22 @@ def test_gemm_fused_layernorm(dev, dtype, M, N):
     assert rel_err(out, ref) < tol
 
 
+@pytest.mark.parametrize("patch", [32, 14])
+def test_im2col_patches(dev, patch):
+    """Conv2d(stride=patch) patch rows (HF/models/clip/modeling_clip.py:148-154), incl. ViT-L/14's p = 14
+    (588 values per patch, rows padded to 592 with zeros)."""
+    B, C, HW = 2, 3, 224
+    px = rnd((B, C, HW, HW), dev, seed=71)
+    G, K = HW // patch, C * patch * patch
+    Kp = (K + 7) // 8 * 8
+    out = torch.full((B * G * G, Kp), 7.0, device=dev)
+    ops.im2col_patches(px, out, patch)
+    ref = px.unfold(2, patch, patch).unfold(3, patch, patch)  # [B, C, G, G, p, p]
+    ref = ref.permute(0, 2, 3, 1, 4, 5).reshape(B * G * G, K)
+    assert torch.equal(out[:, :K], ref)
+    assert torch.all(out[:, K:] == 0)
+
+
 def test_gemm_dropout_statistics(dev):
     M, N, K = 512, 512, 64
     A = torch.ones((M, K), device=dev)
