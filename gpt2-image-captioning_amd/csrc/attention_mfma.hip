@@ -790,6 +790,9 @@ static bool mfma_fwd3_ok(const icap_attn_args* a) {
 
 bool mfma_attention_ok(const icap_attn_args* a, bool bwd) {
   if (!bwd && mfma_fwd3_ok(a)) return true;
+  // head dim 128 (the mapper at gpt_dim 1024, BASELINE configs[3]): the transpose-free v2 kernels only
+  if (a->dtype == ICAP_BF16 && a->hd == 128 && a->S <= 16 * amfma::MAXKT && !(a->ld_qkv & 7))
+    return bwd ? ((a->ld_dout & 7) == 0 && mfma_bwd2_ok(a)) : mfma_fwd2_ok(a);
   if (a->dtype != ICAP_BF16 || (a->hd != 64 && a->hd != 96) || a->S > 16 * amfma::MAXKT) return false;
   if ((a->ld_qkv & 7) || (bwd && (a->ld_dout & 7))) return false;
   const amfma::Geo g = mfma_geo(a);
@@ -826,6 +829,9 @@ int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float
     if (a->hd == 64) {
       static bool once = (lds_limit(amfma::fwd2_kernel<64>), true); (void)once;
       hipLaunchKernelGGL(amfma::fwd2_kernel<64>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+    } else if (a->hd == 128) {
+      static bool once = (lds_limit(amfma::fwd2_kernel<128>), true); (void)once;
+      hipLaunchKernelGGL(amfma::fwd2_kernel<128>, grid, block2, lds2, s, *a, g, thr, inv_keep);
     } else {
       static bool once = (lds_limit(amfma::fwd2_kernel<96>), true); (void)once;
       hipLaunchKernelGGL(amfma::fwd2_kernel<96>, grid, block2, lds2, s, *a, g, thr, inv_keep);
@@ -848,6 +854,9 @@ int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float
       if (a->hd == 64) {
         static bool once = (lds_limit(amfma::bwd2_kernel<64>), true); (void)once;
         hipLaunchKernelGGL(amfma::bwd2_kernel<64>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+      } else if (a->hd == 128) {
+        static bool once = (lds_limit(amfma::bwd2_kernel<128>), true); (void)once;
+        hipLaunchKernelGGL(amfma::bwd2_kernel<128>, grid, block2, lds2, s, *a, g, thr, inv_keep);
       } else {
         static bool once = (lds_limit(amfma::bwd2_kernel<96>), true); (void)once;
         hipLaunchKernelGGL(amfma::bwd2_kernel<96>, grid, block2, lds2, s, *a, g, thr, inv_keep);

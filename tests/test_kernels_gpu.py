@@ -274,7 +274,8 @@ def ref_attention(q, k, v, scale, causal, key_mask):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,S,H,hd,causal,masked", [(3, 65, 12, 64, True, True), (2, 25, 8, 96, False, False),
-                                                    (2, 50, 12, 64, False, False)])
+                                                    (2, 50, 12, 64, False, False), (2, 25, 8, 128, False, False),
+                                                    (2, 60, 4, 128, True, True)])
 def test_attention(dev, dtype, B, S, H, hd, causal, masked):
     D = H * hd
     qkv = rnd((B * S, 3 * D), dev, dtype, seed=20)
