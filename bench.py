@@ -152,6 +152,25 @@ def greedy_rate(model, Bd, dev, world, edim=512):
     return caps_per_s, dt, nd, lens
 
 
+def topp_rate(model, Bd, dev, world, edim=512, temperature=1.0, top_p=0.9):
+    """50-token KV-cached nucleus-sampled captions/s (src/models.py:400-449 branch: HIP top-p filter + draw per
+    step, host EOS check per step as in the reference loop). Random-init weights rarely emit EOS, so every
+    caption runs all 50 steps."""
+    g = torch.Generator().manual_seed(6)
+    emb = torch.randn((Bd, edim), generator=g)
+    emb = (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
+    model.generate(emb, max_length=50, temperature=temperature, top_p=top_p)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nd, lens = 2, []
+    for _ in range(nd):
+        lens.append(model.generate(emb, max_length=50, temperature=temperature, top_p=top_p).shape[1])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"captions_per_s": round(world * Bd * nd / dt, 1), "batch_per_gpu": Bd, "temperature": temperature,
+            "top_p": top_p, "returned_len": lens[-1], "ms_per_batch": round(dt / nd * 1e3, 3)}
+
+
 def preprocess_rate(dev):
     """CLIP image preprocessing: device (icap_clip_preprocess, Pillow-exact) vs the host
     PIL processor on the same decoded 480x640 RGB images; images/s (JPEG decode excluded on both sides)."""
@@ -279,6 +298,7 @@ def main():
     caps_per_s, dt, nd, lens = None, None, 1, [None]
     if not args.no_decode:
         caps_per_s, dt, nd, lens = greedy_rate(model, Bd, dev, world, 768 if args.config == "medium" else 512)
+    topp = None if args.no_decode else topp_rate(model, Bd, dev, world, 768 if args.config == "medium" else 512)
     traffic, traffic_src = pmc_traffic(dom)
     prep = None if args.no_decode else preprocess_rate(dev)
 
@@ -303,6 +323,7 @@ def main():
             "greedy_captions_per_s": round(caps_per_s, 1) if caps_per_s else None,
             "greedy": {"batch_per_gpu": Bd, "decode_steps": 50, "returned_len": lens[-1], "kv_cache": True,
                        "ms_per_batch": round(dt / nd * 1e3, 3) if dt else None},
+            "topp_sampling": topp,
             "clip_preprocess": prep,
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1),
                          "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),

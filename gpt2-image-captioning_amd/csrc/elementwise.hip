@@ -623,6 +623,171 @@ __global__ void add_position_kernel(int B, int npos, int D, const T* __restrict_
   }
 }
 
+
+// ---- nucleus (top-p) sampling: src/models.py:400-449 ---------------------------------
+// One 1024-thread block per row. The row lives in registers, NPT elements per thread (index k*1024 + tid), as a
+// monotone uint32 key of the temperature-scaled logit l = logit / temperature and a fixed-point probability
+// q = trunc(float(e) * float(2^31 / Z)), e = expf(l - max), Z = sum(trunc(e * 2^40)) / 2^40. Every mass below
+// is an exact integer sum, so nothing depends on the reduction order (deterministic; oracle/icap_oracle.py
+// topp_sample_fixed restates it in numpy).
+// The reference filter (sort descending, cumsum(softmax), remove where cumsum > top_p, shifted right by one)
+// keeps ranks 0..r, r = the first rank whose inclusive cumsum exceeds top_p; ranks run by descending logit and,
+// among equal logits, ascending index (a stable sort). Here K* = min{K : mass(key > K) <= T} (32-step
+// bisection over the key space) is the key of rank r; of the c tokens tied at K* the first (T - A) / q* + 1 by
+// index are kept, A = mass(key > K*). The draw is an inverse CDF over the kept tokens in vocabulary order with
+// u = hash32(seed, step << 32 | row) / 2^32: torch.multinomial's stream is not reproducible across devices,
+// its distribution (softmax over the kept logits) is what is matched.
+namespace topp {
+constexpr int NT = 1024, NW = NT / 64;
+__device__ __forceinline__ uint32_t fkey(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+// block-wide sum, result in every thread; callers alternate `buf` between consecutive calls so one barrier
+// per call suffices (a buffer is rewritten only after the next call's barrier, which follows every read of it)
+__device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* buf) {
+  unsigned long long x = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  if ((threadIdx.x & 63) == 0) buf[threadIdx.x >> 6] = x;
+  __syncthreads();
+  uint64_t s = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) s += buf[w];
+  return s;
+}
+}  // namespace topp
+
+template <typename T, int NPT>
+__global__ __launch_bounds__(1024) void topp_sample_kernel(int64_t V, const T* __restrict__ logits, int64_t ld,
+                                                         float temperature, float top_p,
+                                                         const int32_t* __restrict__ finished, uint64_t seed,
+                                                         const uint64_t* __restrict__ seed_ptr, int step, int64_t eos,
+                                                         int64_t* __restrict__ out) {
+  using namespace topp;
+  __shared__ uint64_t sbuf[2][NW];
+  __shared__ float fbuf[NW];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  // finished rows: the reference samples from zeroed logits and then overwrites the draw with EOS (:410,:456)
+  if (finished && finished[b]) {
+    if (tid == 0) out[b] = eos;
+    return;
+  }
+  const T* row = logits + (int64_t)b * ld;
+  uint32_t key[NPT], q[NPT];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int64_t j = (int64_t)k * NT + tid;
+    const float l = j < V ? io<T>::ld(row + j) / temperature : -INFINITY;
+    key[k] = fkey(l);
+    q[k] = __float_as_uint(l);
+    m = fmaxf(m, l);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((tid & 63) == 0) fbuf[tid >> 6] = m;
+  __syncthreads();
+  m = fbuf[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) m = fmaxf(m, fbuf[w]);
+  // Z as an exact 2^-40 fixed-point sum (order independent, so q below is reproducible bit for bit)
+  uint64_t zi = 0;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const float e = expf(__uint_as_float(q[k]) - m);
+    q[k] = __float_as_uint(e);
+    zi += (uint64_t)((double)e * 1099511627776.0);
+  }
+  int ci = 0;
+  zi = block_sum(zi, sbuf[ci]);
+  ci ^= 1;
+  const double z = (double)zi * (1.0 / 1099511627776.0);
+  if (!(z > 0.0)) {  // every logit -inf / NaN: nothing to sample
+    if (tid == 0) out[b] = 0;
+    return;
+  }
+  const float scale = (float)(2147483648.0 / z);
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) q[k] = (uint32_t)(__uint_as_float(q[k]) * scale);
+
+  uint32_t kstar = 0, jt = (uint32_t)V;
+  if (top_p < 1.0f) {
+    const uint64_t thr = (uint64_t)((double)top_p * 2147483648.0);
+    uint32_t lo = 0, hi = 0xFFFFFFFFu;  // invariant: mass(key > hi) <= thr
+    while (lo < hi) {
+      const uint32_t mid = lo + ((hi - lo) >> 1);
+      uint64_t s = 0;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) s += key[k] > mid ? q[k] : 0u;
+      s = block_sum(s, sbuf[ci]);
+      ci ^= 1;
+      if (s <= thr) hi = mid; else lo = mid + 1;
+    }
+    kstar = lo;
+    if (kstar != 0) {  // kstar == 0: the whole row's mass is <= top_p, everything stays
+      uint64_t a = 0, c = 0, mt = 0;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        a += key[k] > kstar ? q[k] : 0u;
+        c += key[k] == kstar ? 1u : 0u;
+        mt += key[k] == kstar ? q[k] : 0u;
+      }
+      a = block_sum(a, sbuf[ci]); ci ^= 1;
+      c = block_sum(c, sbuf[ci]); ci ^= 1;
+      mt = block_sum(mt, sbuf[ci]); ci ^= 1;
+      const uint64_t qs = mt / c;  // all tied tokens share one q (same logit)
+      const uint64_t ntie = (thr - a) / qs + 1;
+#ifdef ICAP_TOPP_DEBUG
+      if (tid == 0)
+        printf("row %d a %llu c %llu mt %llu qs %llu thr %llu ntie %llu\n", b, (unsigned long long)a,
+               (unsigned long long)c, (unsigned long long)mt, (unsigned long long)qs, (unsigned long long)thr,
+               (unsigned long long)ntie);
+#endif
+      if (ntie < c) {  // keep the ntie lowest indices of the tie group: jt = min{J : count(tie, j < J) >= ntie}
+        uint32_t jlo = 1, jhi = (uint32_t)V;
+        while (jlo < jhi) {
+          const uint32_t mid = jlo + ((jhi - jlo) >> 1);
+          uint64_t s = 0;
+#pragma unroll
+          for (int k = 0; k < NPT; ++k) s += (key[k] == kstar && (uint32_t)(k * NT + tid) < mid) ? 1u : 0u;
+          s = block_sum(s, sbuf[ci]);
+          ci ^= 1;
+          if (s >= ntie) jhi = mid; else jlo = mid + 1;
+        }
+        jt = jlo;
+      }
+    }
+  }
+  uint64_t keep = 0, tot = 0;  // keep: bit k <=> element k of this thread is in the nucleus
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const bool kk = key[k] > kstar || (key[k] == kstar && (uint32_t)(k * NT + tid) < jt);
+    keep |= (uint64_t)kk << k;
+    tot += kk ? q[k] : 0u;
+  }
+  tot = block_sum(tot, sbuf[ci]);
+  ci ^= 1;
+  const uint32_t u = hash32(eff_seed(seed, seed_ptr), ((uint64_t)(uint32_t)step << 32) | (uint32_t)b);
+  const uint64_t target = (tot * (uint64_t)u) >> 32;  // tot <= 2^31: no overflow; target < tot
+  uint32_t jlo = 1, jhi = (uint32_t)V;  // min{J : kept mass of j < J  > target}
+  while (jlo < jhi) {
+    const uint32_t mid = jlo + ((jhi - jlo) >> 1);
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) s += (((keep >> k) & 1) && (uint32_t)(k * NT + tid) < mid) ? q[k] : 0u;
+    s = block_sum(s, sbuf[ci]);
+    ci ^= 1;
+    if (s > target) jhi = mid; else jlo = mid + 1;
+  }
+#ifdef ICAP_TOPP_DEBUG
+  if (tid == 0)
+    printf("row %d z %.9g kstar %08x jt %u tot %llu u %u target %llu -> %u\n", b, z, kstar, jt,
+           (unsigned long long)tot, u, (unsigned long long)target, jlo - 1);
+#endif
+  if (tid == 0) out[b] = tot ? (int64_t)(jlo - 1) : 0;
+}
+
 }  // namespace icap
 
 using namespace icap;
@@ -897,6 +1062,23 @@ extern "C" int icap_greedy_next(int32_t dtype, int32_t B, int64_t V, const void*
                                        CTP(logits), ld, eos, forced, finished, tokens, ld_tokens, step, CTP(wte), CTP(wpe),
                                        pos, D, TP(x), vec));
   return check_launch("icap_greedy_next");
+}
+
+extern "C" int icap_topp_sample(int32_t dtype, int32_t B, int64_t V, const void* logits, int64_t ld, float temperature,
+                                float top_p, const int32_t* finished, uint64_t seed, const uint64_t* seed_ptr,
+                                int32_t step, int64_t eos, int64_t* out, void* stream) {
+  ICAP_REQUIRE(logits && out, "icap_topp_sample: null pointer");
+  ICAP_REQUIRE(V > 0 && V <= 64 * 1024 && ld >= V, "icap_topp_sample: need 0 < V <= 65536 and ld >= V");
+  ICAP_REQUIRE(temperature > 0.f, "icap_topp_sample: temperature must be > 0 (0 is the greedy branch)");
+  if (B == 0) return ICAP_OK;
+  if (V <= 50 * 1024) {
+    DISPATCH_T(dtype, hipLaunchKernelGGL((topp_sample_kernel<T, 50>), dim3((unsigned)B), dim3(1024), 0, S_(stream), V,
+                                         CTP(logits), ld, temperature, top_p, finished, seed, seed_ptr, step, eos, out));
+  } else {
+    DISPATCH_T(dtype, hipLaunchKernelGGL((topp_sample_kernel<T, 64>), dim3((unsigned)B), dim3(1024), 0, S_(stream), V,
+                                         CTP(logits), ld, temperature, top_p, finished, seed, seed_ptr, step, eos, out));
+  }
+  return check_launch("icap_topp_sample");
 }
 
 extern "C" int icap_add_position(int32_t dtype, int32_t B, int32_t npos, int32_t D, const void* src,

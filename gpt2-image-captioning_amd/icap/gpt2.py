@@ -570,14 +570,18 @@ class GPT2Core:
         return toks[:, :n].clone()
 
     @torch.no_grad()
-    def sample_decode(self, prefix: Tensor, max_length: int, temperature: float, top_p: float) -> Tensor:
-        """Temperature / nucleus sampling branch of src/models.py:400-449 over the KV-cached decoder. The logits
-        come from the HIP kernels; the top-p filter and multinomial draw use torch device ops on the [B, V]
-        last-position logits (not on the training hot path)."""
+    def sample_decode(self, prefix: Tensor, max_length: int, temperature: float, top_p: float,
+                      seed: Optional[int] = None) -> Tensor:
+        """Temperature / nucleus sampling branch of src/models.py:400-449 over the KV-cached decoder. Logits,
+        the top-p filter and the draw are HIP kernels (ops.topp_sample); the draw's seed comes
+        from torch's CPU generator unless given, so torch.manual_seed makes a run reproducible."""
         B, P, D = prefix.shape
         if max_length <= 0:
             return torch.empty((B, 0), dtype=torch.long, device=prefix.device)
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         ds = self.alloc_decode(B, P, max_length)
+        nxt = torch.empty(B, dtype=torch.long, device=prefix.device)
         pre = prefix if (prefix.dtype == self.dtype and prefix.stride(-1) == 1) else prefix.to(self.dtype).contiguous()
         ops.add_position(pre, pre.stride(0), pre.stride(1), self.wpe, ds.x, B=B, npos=P, D=D, pos0=0)
         self._decode_block(ds, P * B, ds.x, 0, P, prefill=True)
@@ -593,17 +597,7 @@ class GPT2Core:
             a = ds.a[:B]
             ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
             ops.gemm(a, self.wte, ds.logits, M=B, alg_flops=2.0 * B * self.V * self.D)
-            logits = ds.logits[:, : self.V].float() / temperature
-            fin = ds.finished.bool()
-            if top_p < 1.0:
-                logits[fin, :] = 0.0
-                sl, si = torch.sort(logits, descending=True)
-                cp = torch.cumsum(torch.softmax(sl, dim=-1), dim=-1)
-                rm = cp > top_p
-                rm[:, 1:] = rm[:, :-1].clone()
-                rm[:, 0] = False
-                logits = logits.masked_fill(rm.scatter(1, si, rm), float("-inf"))
-            nxt = torch.multinomial(torch.softmax(logits, dim=-1), 1).reshape(B).contiguous()
+            ops.topp_sample(ds.logits, self.V, temperature, top_p, ds.finished, seed, s, self.cfg.eos_token_id, nxt)
             pos_next = P + s
             nxt_x = ds.x[:B] if pos_next < ds.T else None
             ops.greedy_next(ds.logits, self.V, self.cfg.eos_token_id, ds.finished, ds.tokens, s,

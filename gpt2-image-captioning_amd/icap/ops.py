@@ -353,6 +353,17 @@ def greedy_next(logits: Tensor, V: int, eos: int, finished: Tensor, tokens: Tens
          finished.data_ptr(), tokens.data_ptr(), _ld(tokens), step, _p(wte), _p(wpe), pos, D, _p(x), _stream())
 
 
+def topp_sample(logits: Tensor, V: int, temperature: float, top_p: float, finished: Optional[Tensor], seed: int,
+                step: int, eos: int, out: Tensor, seed_ptr: Optional[Tensor] = None) -> Tensor:
+    """Temperature + nucleus draw of one token per row (src/models.py:400-449) -> out int64 [B]."""
+    B = out.shape[0]
+    if B and logits.shape[0] < B:
+        raise ValueError("topp_sample: logits has fewer rows than out")
+    call("icap_topp_sample", dtype_code(logits.dtype), B, V, logits.data_ptr(), _ld(logits), float(temperature),
+         float(top_p), _p(finished), seed & (2**64 - 1), _p(seed_ptr), step, eos, out.data_ptr(), _stream())
+    return out
+
+
 def add_position(src: Tensor, src_bstride: int, src_tstride: int, wpe: Tensor, x: Tensor, *, B: int, npos: int,
                  D: int, pos0: int) -> Tensor:
     call("icap_add_position", dtype_code(x.dtype), B, npos, D, src.data_ptr(), src_bstride, src_tstride,

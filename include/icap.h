@@ -287,6 +287,17 @@ int icap_greedy_next(int32_t dtype, int32_t B, int64_t V, const void* logits, in
                      int64_t eos, const int64_t* forced, int32_t* finished, int64_t* tokens, int64_t ld_tokens,
                      int32_t step, const void* wte, const void* wpe, int32_t pos, int32_t D,
                      void* x, void* stream);
+/* Nucleus sampling of one next token per row (the temperature / top-p branch of   */
+/* src/models.py:400-449): l = logits[b] / temperature; keep the */
+/* reference's filter set (stable descending sort, cumsum(softmax) > top_p removed */
+/* after a shift right by one; top_p >= 1 keeps all); draw by inverse CDF over the */
+/* kept tokens in index order with u = hash32(seed', step << 32 | b) / 2^32, where  */
+/* seed' = seed + (*seed_ptr) * golden when seed_ptr != NULL. Probabilities are    */
+/* 2^31 fixed point (exact integer sums, deterministic). finished[b] != 0 -> eos.  */
+/* out: int64 [B]. Needs V <= 65536, temperature > 0.                            */
+int icap_topp_sample(int32_t dtype, int32_t B, int64_t V, const void* logits, int64_t ld, float temperature,
+                     float top_p, const int32_t* finished, uint64_t seed, const uint64_t* seed_ptr,
+                     int32_t step, int64_t eos, int64_t* out, void* stream);
 /* x[(t*B + b)*D + d] = src[b*src_bstride + t*src_tstride + d] + wpe[(pos0+t)*D + d], t < npos */
 /* (prefix rows into the position-major decode input, modeling_gpt2.py:571-577).            */
 int icap_add_position(int32_t dtype, int32_t B, int32_t npos, int32_t D, const void* src,

@@ -358,6 +358,88 @@ def greedy_generate(gpt_sd, gcfg: GPT2Cfg, prefix: Tensor, max_length: int = 50)
     return torch.cat(out, dim=1)
 
 
+# --------------------------------------------------------------------------- top-p sampling (a14)
+
+
+def topp_filter_reference(logits: Tensor, temperature: float, top_p: float,
+                          finished: Optional[Tensor] = None) -> Tensor:
+    """The reference's filter, src/models.py:400-433, in torch fp32: returns the kept mask [B, V]. Deviation
+    (documented): the sort is stable, so equal logits rank by ascending index; the reference's torch.sort is
+    unspecified on ties."""
+    lg = logits.float() / (temperature if temperature > 0 else 1.0)
+    if top_p < 1.0 and temperature > 0:
+        if finished is not None:
+            lg[finished.bool(), :] = 0.0
+        sl, si = torch.sort(lg, descending=True, stable=True)
+        cp = torch.cumsum(F.softmax(sl, dim=-1), dim=-1)
+        rm = cp > top_p
+        rm[:, 1:] = rm[:, :-1].clone()
+        rm[:, 0] = False
+        return ~rm.scatter(1, si, rm)
+    return torch.ones_like(lg, dtype=torch.bool)
+
+
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def _hash32(seed: int, idx: np.ndarray) -> np.ndarray:
+    """common.h hash32 (the counter RNG shared with dropout), uint32 results."""
+    idx = np.asarray(idx).astype(np.uint64)
+    s0, s1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    lo, hi = idx & _M32, idx >> np.uint64(32)
+    x = ((((lo ^ s0) * np.uint64(0x9E3779B9)) + hi) & _M32) ^ s1
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & _M32
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & _M32
+    x ^= x >> np.uint64(16)
+    return x.astype(np.uint32)
+
+
+def _fkey(l: np.ndarray) -> np.ndarray:
+    u = l.astype(np.float32).view(np.uint32)
+    return np.where(u & np.uint32(0x80000000), ~u, u | np.uint32(0x80000000)).astype(np.uint32)
+
+
+def topp_sample_fixed(logits: np.ndarray, temperature: float, top_p: float, seed: int, step: int,
+                      finished: Optional[np.ndarray] = None, eos: int = 50256):
+    """Nucleus draw restated with the kernel's arithmetic conventions (icap_topp_sample, include/icap.h) over
+    the reference filter of src/models.py:400-449: stable descending rank, probabilities as 2^31 fixed point
+    q = trunc(f32(e) * f32(2^31 / Z)), Z = sum(trunc(e * 2^40)) / 2^40, keep ranks 0..r with r the first rank whose inclusive mass exceeds
+    trunc(top_p * 2^31), then inverse CDF in index order at u = hash32(seed, step << 32 | row).
+    Returns (tokens int64 [B], kept bool [B, V])."""
+    lg = np.asarray(logits, dtype=np.float32)
+    B, V = lg.shape
+    toks = np.zeros(B, dtype=np.int64)
+    kept = np.zeros((B, V), dtype=bool)
+    for b in range(B):
+        if finished is not None and finished[b]:
+            toks[b] = eos
+            continue
+        l = (lg[b] / np.float32(temperature)).astype(np.float32)
+        e = np.exp(l - l.max()).astype(np.float32)
+        z = float(int((e.astype(np.float64) * 1099511627776.0).astype(np.uint64).sum())) / 1099511627776.0
+        q = (e * np.float32(2147483648.0 / z)).astype(np.float32).astype(np.uint64)
+        keep = np.ones(V, dtype=bool)
+        if np.float32(top_p) < 1.0:
+            thr = np.uint64(int(float(np.float32(top_p)) * 2147483648.0))
+            key = _fkey(l)
+            order = np.argsort(~key, kind="stable")  # descending key, ascending index on ties
+            cum = np.cumsum(q[order])
+            over = np.nonzero(cum > thr)[0]
+            if over.size:
+                keep[:] = False
+                keep[order[: over[0] + 1]] = True
+        kept[b] = keep
+        qk = np.where(keep, q, np.uint64(0))
+        tot = int(qk.sum())
+        u = int(_hash32(seed, np.array([(step << 32) | b], dtype=np.uint64))[0])
+        target = (tot * u) >> 32
+        c = np.cumsum(qk)
+        toks[b] = int(np.nonzero(c > np.uint64(target))[0][0]) if tot else 0
+    return toks, kept
+
+
 # --------------------------------------------------------------------------- CLIP
 
 
