@@ -44,6 +44,7 @@ def train(train_dataset, model, batch_size: int, num_epochs: int, num_workers: i
     model = model.to(device)
     model.train()
     dist = torch.distributed.is_available() and torch.distributed.is_initialized()
+    is_main = (not dist) or torch.distributed.get_rank() == 0  # replicated weights: rank 0 writes the files
     sampler = None
     if dist:
         sampler = torch.utils.data.distributed.DistributedSampler(train_dataset, shuffle=True, seed=seed)
@@ -96,7 +97,7 @@ def train(train_dataset, model, batch_size: int, num_epochs: int, num_workers: i
         avg = float(loss_acc.item()) / max(nb, 1)
         epoch_loss_values.append(avg)
         print(f"Epoch {epoch + 1} completed. Average Loss: {avg:.4f}")
-        if (epoch + 1) % save_every_epoch == 0 or (epoch + 1) == num_epochs:
+        if is_main and ((epoch + 1) % save_every_epoch == 0 or (epoch + 1) == num_epochs):
             path = os.path.join(outputs_dir, f"model_epoch_{epoch + 1}.pt")
             model.save_parameters(path)
         if val_dataset is not None and (epoch + 1) % eval_every_epoch == 0:
@@ -108,7 +109,8 @@ def train(train_dataset, model, batch_size: int, num_epochs: int, num_workers: i
             cider = m.get("cider", -1.0)
             if cider > best_val_cider:
                 best_val_cider, best_epoch = cider, epoch + 1
-                model.save_parameters(os.path.join(outputs_dir, f"best_model_epoch_{best_epoch}.pt"))
+                if is_main:
+                    model.save_parameters(os.path.join(outputs_dir, f"best_model_epoch_{best_epoch}.pt"))
             model.train()
     return {"epoch_losses": epoch_loss_values, "val_metrics": val_metrics_history, "best_val_cider": best_val_cider,
             "best_epoch": best_epoch}
