@@ -9,7 +9,9 @@ data (no COCO download offline): `real` caption tokens + EOS (mask 1), pad = EOS
 
 from __future__ import annotations
 
+import hashlib
 import json
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -25,8 +27,17 @@ class CaptionData:  # dataset.py:88-95
 
 
 class CocoDataset(Dataset):
+    """src/dataset.py:98-215. Extra keyword arguments (defaults keep the reference's items bit for bit):
+    `pretokenize` tokenises every caption once at construction, in batches, with the same tokenizer call as the
+    reference's per-item __getitem__ (dataset.py:181-188: caption + eos_token, max_length, padding="max_length",
+    truncation) and keeps int32 ids / int8 mask arrays, so __getitem__ is a row slice instead of a tokenizer
+    call (the per-item BPE gates the loader at device rates). `token_cache_path` stores
+    those arrays (torch.save of plain tensors, loaded with weights_only=True) keyed by a digest of the
+    caption texts, max_length and the tokenizer's eos token."""
+
     def __init__(self, embeddings_path: str, annotations_path: str, tokenizer=None, max_length: int = 50,
-                 normalize_embeddings: bool = False):
+                 normalize_embeddings: bool = False, *, pretokenize: bool = True,
+                 token_cache_path: Optional[str] = None):
         if tokenizer is None:
             from .models import load_gpt2_tokenizer
 
@@ -42,11 +53,43 @@ class CocoDataset(Dataset):
             coco = json.load(f)
         self.captions = [CaptionData(a["image_id"], self.image_id_to_index[a["image_id"]], a["caption"])
                          for a in coco["annotations"]]
+        self.token_ids: Optional[torch.Tensor] = None  # int32 [n, max_length] when pretokenised
+        self.token_mask: Optional[torch.Tensor] = None  # int8 [n, max_length]
+        if pretokenize:
+            self._pretokenize(token_cache_path)
         print(f"Dataset ready: {len(self.image_filenames)} images, {len(self.captions)} captions.")
 
     @staticmethod
     def get_image_id_from_filename(filename: str) -> int:
         return int(filename.split("_")[-1].split(".")[0])  # dataset.py:155-167
+
+    def _texts(self):
+        eos = self.tokenizer.eos_token
+        return [c.caption_text + eos for c in self.captions]
+
+    def _pretokenize(self, cache_path: Optional[str], chunk: int = 8192) -> None:
+        texts = self._texts()
+        h = hashlib.sha1(f"{self.max_length}|{self.tokenizer.eos_token}|{len(texts)}".encode())
+        for t in texts:
+            h.update(t.encode("utf-8"))
+            h.update(b"\0")
+        digest = h.hexdigest()
+        if cache_path and os.path.exists(cache_path):
+            d = torch.load(cache_path, map_location="cpu", weights_only=True)
+            if d.get("digest") == digest:
+                self.token_ids, self.token_mask = d["ids"], d["mask"]
+                return
+        n, L = len(texts), self.max_length
+        ids = torch.empty((n, L), dtype=torch.int32)
+        mask = torch.empty((n, L), dtype=torch.int8)
+        for s in range(0, n, chunk):
+            enc = self.tokenizer(texts[s: s + chunk], max_length=L, padding="max_length", truncation=True,
+                                 return_tensors="pt")
+            ids[s: s + chunk] = enc.input_ids
+            mask[s: s + chunk] = enc.attention_mask
+        self.token_ids, self.token_mask = ids, mask
+        if cache_path:
+            torch.save({"digest": digest, "ids": ids, "mask": mask}, cache_path)
 
     def __len__(self) -> int:
         return len(self.captions)
@@ -56,10 +99,14 @@ class CocoDataset(Dataset):
         emb = self.image_embeddings[c.embedding_index]
         if self.normalize_embeddings:
             emb = emb / emb.norm(2, -1)
-        enc = self.tokenizer(c.caption_text + self.tokenizer.eos_token, max_length=self.max_length,
-                             padding="max_length", truncation=True, return_tensors="pt")
-        ids = enc.input_ids.squeeze(0)
-        mask = enc.attention_mask.squeeze(0)
+        if self.token_ids is not None:
+            ids = self.token_ids[idx].long()
+            mask = self.token_mask[idx].long()
+        else:
+            enc = self.tokenizer(c.caption_text + self.tokenizer.eos_token, max_length=self.max_length,
+                                 padding="max_length", truncation=True, return_tensors="pt")
+            ids = enc.input_ids.squeeze(0)
+            mask = enc.attention_mask.squeeze(0)
         labels = ids.clone()
         labels[mask == 0] = -100
         return {"token_ids": ids, "labels": labels, "image_embedding": emb, "attention_mask": mask,
