@@ -70,8 +70,10 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          resid: Optional[Tensor] = None, alpha: float = 1.0, beta: float = 0.0, drop: Dropout = NO_DROP,
          M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None,
          alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None,
-         trans_ab: bool = False, ln: Optional[tuple] = None) -> Tensor:
+         trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
+    workspace: fp32 split-K scratch for launches on a stream other than the package's main one (the per-device
+    default serves every GEMM ordered on one stream; splits are capped to what the scratch holds).
     trans_ab: A and B are K-outer ([K, M] / [K, N] row-major: out = epi(alpha * A^T @ B)), bf16 only.
     ln: (gamma, beta, eps) — A is LayerNorm-ed over its K columns inside the GEMM (M <= 128 launches).
     alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).
@@ -106,7 +108,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     if resid is not None:
         a.resid, a.ldr = resid.data_ptr(), _ld(resid)
     a.drop_p, a.seed, a.offset, a.seed_ptr = drop.p, drop.seed, drop.offset, drop.ptr
-    ws = gemm_workspace(A.device)
+    ws = gemm_workspace(A.device) if workspace is None else workspace
     a.workspace, a.workspace_bytes, a.split_k = ws.data_ptr(), ws.numel() * 4, split_k
     a.m_dev = _p(m_dev)
     if ln is not None:

@@ -301,3 +301,4 @@ def test_compact_head_equals_full_head(dev, dropout):
     assert np.allclose(res[0][0], res[1][0], rtol=1e-6, atol=0), (res[0][0], res[1][0])
     for k in res[0][1]:
         assert torch.allclose(res[0][1][k], res[1][1][k], rtol=1e-6, atol=1e-9), k
+
