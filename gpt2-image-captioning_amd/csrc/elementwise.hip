@@ -625,23 +625,26 @@ __global__ void add_position_kernel(int B, int npos, int D, const T* __restrict_
 
 
 // ---- nucleus (top-p) sampling: src/models.py:400-449 ---------------------------------
-// One 1024-thread block per row. The row lives in registers, NPT elements per thread (index k*1024 + tid), as a
-// monotone uint32 key of the temperature-scaled logit l = logit / temperature and a fixed-point probability
-// q = trunc(float(e) * float(2^31 / Z)), e = expf(l - max), Z = sum(trunc(e * 2^40)) / 2^40. Every mass below
-// is an exact integer sum, so nothing depends on the reduction order (deterministic; oracle/icap_oracle.py
-// topp_sample_fixed restates it in numpy).
+// One 512-thread block per row. The row lives in registers, NPT elements per thread (index k*512 + tid), as a
+// fixed-point probability q = trunc(float(e) * float(2^31 / Z)) of the temperature-scaled logit l = logit / T,
+// e = expf(l - max), Z = sum(trunc(e * 2^40)) / 2^40: one register per element, 100 per lane for GPT-2's
+// vocabulary within the 256 VGPRs a 512-thread block allows (1024 threads cap a lane at 128 and spilled). Every mass below is an exact integer sum, so nothing depends on the
+// reduction order (deterministic; oracle/icap_oracle.py topp_sample_fixed restates it in numpy).
 // The reference filter (sort descending, cumsum(softmax), remove where cumsum > top_p, shifted right by one)
-// keeps ranks 0..r, r = the first rank whose inclusive cumsum exceeds top_p; ranks run by descending logit and,
-// among equal logits, ascending index (a stable sort). Here K* = min{K : mass(key > K) <= T} (32-step
-// bisection over the key space) is the key of rank r; of the c tokens tied at K* the first (T - A) / q* + 1 by
-// index are kept, A = mass(key > K*). The draw is an inverse CDF over the kept tokens in vocabulary order with
+// keeps ranks 0..r, r = the first rank whose inclusive cumsum exceeds top_p. Ranks here run by descending q
+// and, among equal q, ascending index (a stable sort): equal logits tie exactly as in the reference; distinct
+// logits whose probabilities differ by less than 2^-31 also tie here (the one documented deviation).
+// K* = min{K : mass(q > K) <= T} (bisection over q) is the q of rank r; of the c tokens tied at K* the first
+// (T - A) / K* + 1 by index are kept, A = mass(q > K*). The draw is an inverse CDF over the kept tokens in vocabulary order with
 // u = hash32(seed, step << 32 | row) / 2^32: torch.multinomial's stream is not reproducible across devices,
 // its distribution (softmax over the kept logits) is what is matched.
 namespace topp {
-constexpr int NT = 1024, NW = NT / 64;
-__device__ __forceinline__ uint32_t fkey(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+constexpr int NT = 512, NW = NT / 64;
+// q as an opaque 32-bit value inside a loop: keeps the compiler from hoisting 64-bit zero-extended copies of
+// the whole register-resident row out of the bisection loops (that doubled the row's registers and spilled)
+__device__ __forceinline__ uint32_t opaque(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
 }
 // block-wide sum, result in every thread; callers alternate `buf` between consecutive calls so one barrier
 // per call suffices (a buffer is rewritten only after the next call's barrier, which follows every read of it)
@@ -659,7 +662,7 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v, uint64_t* buf) {
 }  // namespace topp
 
 template <typename T, int NPT>
-__global__ __launch_bounds__(1024) void topp_sample_kernel(int64_t V, const T* __restrict__ logits, int64_t ld,
+__global__ __launch_bounds__(512) void topp_sample_kernel(int64_t V, const T* __restrict__ logits, int64_t ld,
                                                          float temperature, float top_p,
                                                          const int32_t* __restrict__ finished, uint64_t seed,
                                                          const uint64_t* __restrict__ seed_ptr, int step, int64_t eos,
@@ -674,13 +677,12 @@ __global__ __launch_bounds__(1024) void topp_sample_kernel(int64_t V, const T* _
     return;
   }
   const T* row = logits + (int64_t)b * ld;
-  uint32_t key[NPT], q[NPT];
+  uint32_t q[NPT];
   float m = -INFINITY;
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     const int64_t j = (int64_t)k * NT + tid;
     const float l = j < V ? io<T>::ld(row + j) / temperature : -INFINITY;
-    key[k] = fkey(l);
     q[k] = __float_as_uint(l);
     m = fmaxf(m, l);
   }
@@ -714,43 +716,45 @@ __global__ __launch_bounds__(1024) void topp_sample_kernel(int64_t V, const T* _
   uint32_t kstar = 0, jt = (uint32_t)V;
   if (top_p < 1.0f) {
     const uint64_t thr = (uint64_t)((double)top_p * 2147483648.0);
-    uint32_t lo = 0, hi = 0xFFFFFFFFu;  // invariant: mass(key > hi) <= thr
+    uint32_t lo = 0, hi = 0x80000000u;  // q <= 2^31; invariant: mass(q > hi) <= thr
     while (lo < hi) {
       const uint32_t mid = lo + ((hi - lo) >> 1);
       uint64_t s = 0;
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) s += key[k] > mid ? q[k] : 0u;
+      for (int k = 0; k < NPT; ++k) {
+        const uint32_t v = opaque(q[k]);
+        s += v > mid ? v : 0u;
+      }
       s = block_sum(s, sbuf[ci]);
       ci ^= 1;
       if (s <= thr) hi = mid; else lo = mid + 1;
     }
     kstar = lo;
-    if (kstar != 0) {  // kstar == 0: the whole row's mass is <= top_p, everything stays
-      uint64_t a = 0, c = 0, mt = 0;
+    if (kstar != 0) {  // kstar == 0: every positive-mass token fits under top_p, everything stays
+      uint64_t a = 0, c = 0;
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
-        a += key[k] > kstar ? q[k] : 0u;
-        c += key[k] == kstar ? 1u : 0u;
-        mt += key[k] == kstar ? q[k] : 0u;
+        const uint32_t v = opaque(q[k]);
+        a += v > kstar ? v : 0u;
+        c += v == kstar ? 1u : 0u;
       }
       a = block_sum(a, sbuf[ci]); ci ^= 1;
       c = block_sum(c, sbuf[ci]); ci ^= 1;
-      mt = block_sum(mt, sbuf[ci]); ci ^= 1;
-      const uint64_t qs = mt / c;  // all tied tokens share one q (same logit)
+      const uint64_t qs = kstar;
       const uint64_t ntie = (thr - a) / qs + 1;
 #ifdef ICAP_TOPP_DEBUG
       if (tid == 0)
-        printf("row %d a %llu c %llu mt %llu qs %llu thr %llu ntie %llu\n", b, (unsigned long long)a,
-               (unsigned long long)c, (unsigned long long)mt, (unsigned long long)qs, (unsigned long long)thr,
-               (unsigned long long)ntie);
+        printf("row %d a %llu c %llu qs %llu thr %llu ntie %llu\n", b, (unsigned long long)a,
+               (unsigned long long)c, (unsigned long long)qs, (unsigned long long)thr, (unsigned long long)ntie);
 #endif
       if (ntie < c) {  // keep the ntie lowest indices of the tie group: jt = min{J : count(tie, j < J) >= ntie}
         uint32_t jlo = 1, jhi = (uint32_t)V;
         while (jlo < jhi) {
           const uint32_t mid = jlo + ((jhi - jlo) >> 1);
+          const int lim = (int)mid - tid;  // j = k*NT + tid < mid  <=>  k*NT < lim (no per-element index registers)
           uint64_t s = 0;
 #pragma unroll
-          for (int k = 0; k < NPT; ++k) s += (key[k] == kstar && (uint32_t)(k * NT + tid) < mid) ? 1u : 0u;
+          for (int k = 0; k < NPT; ++k) s += (opaque(q[k]) == kstar && k * NT < lim) ? 1u : 0u;
           s = block_sum(s, sbuf[ci]);
           ci ^= 1;
           if (s >= ntie) jhi = mid; else jlo = mid + 1;
@@ -759,12 +763,13 @@ __global__ __launch_bounds__(1024) void topp_sample_kernel(int64_t V, const T* _
       }
     }
   }
-  uint64_t keep = 0, tot = 0;  // keep: bit k <=> element k of this thread is in the nucleus
+  uint64_t keep[(NPT + 63) / 64] = {}, tot = 0;  // bit k: element k of this thread is in the nucleus
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
-    const bool kk = key[k] > kstar || (key[k] == kstar && (uint32_t)(k * NT + tid) < jt);
-    keep |= (uint64_t)kk << k;
-    tot += kk ? q[k] : 0u;
+    const uint32_t v = opaque(q[k]);
+    const bool kk = v > kstar || (v == kstar && k * NT < (int)jt - tid);
+    keep[k >> 6] |= (uint64_t)kk << (k & 63);
+    tot += kk ? v : 0u;
   }
   tot = block_sum(tot, sbuf[ci]);
   ci ^= 1;
@@ -773,9 +778,13 @@ __global__ __launch_bounds__(1024) void topp_sample_kernel(int64_t V, const T* _
   uint32_t jlo = 1, jhi = (uint32_t)V;  // min{J : kept mass of j < J  > target}
   while (jlo < jhi) {
     const uint32_t mid = jlo + ((jhi - jlo) >> 1);
+    const int lim = (int)mid - tid;
     uint64_t s = 0;
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) s += (((keep >> k) & 1) && (uint32_t)(k * NT + tid) < mid) ? q[k] : 0u;
+    for (int k = 0; k < NPT; ++k) {
+      const uint32_t v = opaque(q[k]);
+      s += (((keep[k >> 6] >> (k & 63)) & 1) && k * NT < lim) ? v : 0u;
+    }
     s = block_sum(s, sbuf[ci]);
     ci ^= 1;
     if (s > target) jhi = mid; else jlo = mid + 1;
@@ -1071,11 +1080,11 @@ extern "C" int icap_topp_sample(int32_t dtype, int32_t B, int64_t V, const void*
   ICAP_REQUIRE(V > 0 && V <= 64 * 1024 && ld >= V, "icap_topp_sample: need 0 < V <= 65536 and ld >= V");
   ICAP_REQUIRE(temperature > 0.f, "icap_topp_sample: temperature must be > 0 (0 is the greedy branch)");
   if (B == 0) return ICAP_OK;
-  if (V <= 50 * 1024) {
-    DISPATCH_T(dtype, hipLaunchKernelGGL((topp_sample_kernel<T, 50>), dim3((unsigned)B), dim3(1024), 0, S_(stream), V,
+  if (V <= 100 * 512) {
+    DISPATCH_T(dtype, hipLaunchKernelGGL((topp_sample_kernel<T, 100>), dim3((unsigned)B), dim3(512), 0, S_(stream), V,
                                          CTP(logits), ld, temperature, top_p, finished, seed, seed_ptr, step, eos, out));
   } else {
-    DISPATCH_T(dtype, hipLaunchKernelGGL((topp_sample_kernel<T, 64>), dim3((unsigned)B), dim3(1024), 0, S_(stream), V,
+    DISPATCH_T(dtype, hipLaunchKernelGGL((topp_sample_kernel<T, 128>), dim3((unsigned)B), dim3(512), 0, S_(stream), V,
                                          CTP(logits), ld, temperature, top_p, finished, seed, seed_ptr, step, eos, out));
   }
   return check_launch("icap_topp_sample");

@@ -512,16 +512,24 @@ class GPT2Core:
                 ops.gemm(a, lw.w_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows)
             ops.gemm(f, lw.w_mp_t, x, bias=lw.b_mp, resid=h1, M=rows)
 
-    def _decode_head(self, ds, x_last: Tensor, step: int, pos_next: int):
+    def _decode_head(self, ds, x_last: Tensor, step: int, pos_next: int, samp=None):
+        """ln_f + LM head on the last position, then the next token: argmax (greedy) or, with samp = (temperature,
+        top_p, seed_dev, nxt), the nucleus draw of src/models.py:400-449 (ops.topp_sample); then the EOS latch
+        and the next step's input embedding (ops.greedy_next)."""
         D = self.D
         B = ds.B
         a = ds.a[:B]
         ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
         ops.gemm(a, self.wte, ds.logits, M=B, alg_flops=2.0 * B * self.V * self.D)
+        forced = None
+        if samp is not None:
+            temperature, top_p, seed_dev, forced = samp
+            ops.topp_sample(ds.logits, self.V, temperature, top_p, ds.finished, 0, step, self.cfg.eos_token_id,
+                            forced, seed_ptr=seed_dev)
         nxt_x = ds.x[:B] if pos_next < ds.T else None
         ops.greedy_next(ds.logits, self.V, self.cfg.eos_token_id, ds.finished, ds.tokens, step,
                         self.wte if nxt_x is not None else None, self.wpe if nxt_x is not None else None,
-                        min(pos_next, self.cfg.n_positions - 1), D, nxt_x)
+                        min(pos_next, self.cfg.n_positions - 1), D, nxt_x, forced=forced)
 
     @torch.no_grad()
     def greedy_decode(self, prefix: Tensor, max_length: int, check_every: int = 8, early_exit: bool = True) -> Tensor:
@@ -552,14 +560,14 @@ class GPT2Core:
 
     graph_decode = True  # replay captured HIP graphs of the decode chunks (per batch shape)
 
-    def _runner(self, B: int, P: int, max_length: int) -> "DecodeRunner":
+    def _runner(self, B: int, P: int, max_length: int, sampling=None) -> "DecodeRunner":
         if not hasattr(self, "_runners"):
             self._runners = {}
-        key = (B, P, max_length)
+        key = (B, P, max_length, sampling)
         if key not in self._runners:
             if len(self._runners) >= 2:
                 self._runners.pop(next(iter(self._runners)))
-            self._runners[key] = DecodeRunner(self, B, P, max_length)
+            self._runners[key] = DecodeRunner(self, B, P, max_length, sampling=sampling)
         return self._runners[key]
 
     def _truncate(self, toks: Tensor, steps: int) -> Tensor:
@@ -573,49 +581,48 @@ class GPT2Core:
     def sample_decode(self, prefix: Tensor, max_length: int, temperature: float, top_p: float,
                       seed: Optional[int] = None) -> Tensor:
         """Temperature / nucleus sampling branch of src/models.py:400-449 over the KV-cached decoder. Logits,
-        the top-p filter and the draw are HIP kernels (ops.topp_sample); the draw's seed comes
-        from torch's CPU generator unless given, so torch.manual_seed makes a run reproducible."""
+        the top-p filter and the draw are HIP kernels (ops.topp_sample), replayed as HIP-graph
+        chunks like greedy decode. The draw's seed comes from torch's CPU generator unless given (so
+        torch.manual_seed makes a run reproducible); it lives in device memory, so one graph serves every seed."""
         B, P, D = prefix.shape
         if max_length <= 0:
             return torch.empty((B, 0), dtype=torch.long, device=prefix.device)
         if seed is None:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        if prefix.is_cuda and self.graph_decode:
+            return self._runner(B, P, max_length, (float(temperature), float(top_p))).run(prefix, seed=seed)
         ds = self.alloc_decode(B, P, max_length)
-        nxt = torch.empty(B, dtype=torch.long, device=prefix.device)
+        samp = (temperature, top_p, torch.full((1,), seed, dtype=torch.int64, device=prefix.device),
+                torch.empty(B, dtype=torch.long, device=prefix.device))
         pre = prefix if (prefix.dtype == self.dtype and prefix.stride(-1) == 1) else prefix.to(self.dtype).contiguous()
         ops.add_position(pre, pre.stride(0), pre.stride(1), self.wpe, ds.x, B=B, npos=P, D=D, pos0=0)
         self._decode_block(ds, P * B, ds.x, 0, P, prefill=True)
-        x_last = ds.x[(P - 1) * B: P * B]
-        steps = 0
-        for s in range(max_length):
-            if s > 0:
-                if bool(ds.finished.bool().all()):
-                    break
-                pos = P + s - 1
-                self._decode_block(ds, B, ds.x[:B], pos, 1, prefill=False)
-                x_last = ds.x[:B]
-            a = ds.a[:B]
-            ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
-            ops.gemm(a, self.wte, ds.logits, M=B, alg_flops=2.0 * B * self.V * self.D)
-            ops.topp_sample(ds.logits, self.V, temperature, top_p, ds.finished, seed, s, self.cfg.eos_token_id, nxt)
-            pos_next = P + s
-            nxt_x = ds.x[:B] if pos_next < ds.T else None
-            ops.greedy_next(ds.logits, self.V, self.cfg.eos_token_id, ds.finished, ds.tokens, s,
-                            self.wte if nxt_x is not None else None, self.wpe if nxt_x is not None else None,
-                            min(pos_next, self.cfg.n_positions - 1), D, nxt_x, forced=nxt)
+        self._decode_head(ds, ds.x[(P - 1) * B: P * B], 0, P, samp)
+        steps = 1
+        for s in range(1, max_length):
+            if bool(ds.finished.bool().all()):
+                break
+            pos = P + s - 1
+            self._decode_block(ds, B, ds.x[:B], pos, 1, prefill=False)
+            self._decode_head(ds, ds.x[:B], s, pos + 1, samp)
             steps = s + 1
         return self._truncate(ds.tokens[:, :steps], steps)
 
 
 class DecodeRunner:
-    """Greedy decode of one batch shape as HIP-graph chunks: chunk 0 = prefill + token 0 (+ state reset),
+    """Greedy (or, with sampling = (temperature, top_p), nucleus-sampled) decode of one batch shape as HIP-graph
+    chunks: chunk 0 = prefill + token 0 (+ state reset),
     chunk c = tokens [c*C, (c+1)*C). Between chunks the host reads the EOS latch once (early exit,
     src/models.py:390-391); the returned ids are truncated to the reference loop's length either way."""
 
-    def __init__(self, core: GPT2Core, B: int, P: int, max_length: int, chunk: int = 8):
+    def __init__(self, core: GPT2Core, B: int, P: int, max_length: int, chunk: int = 8, sampling=None):
         self.core, self.B, self.P, self.T = core, B, P, max_length
         self.chunk = chunk
         self.ds = core.alloc_decode(B, P, max_length)
+        self.samp = None  # sampling = (temperature, top_p): nucleus draws, seed read from seed_dev at replay
+        if sampling is not None:
+            self.seed_dev = torch.zeros(1, dtype=torch.int64, device=core.dev)
+            self.samp = (sampling[0], sampling[1], self.seed_dev, torch.empty(B, dtype=torch.long, device=core.dev))
         self.prefix = torch.zeros((B, P, core.D), dtype=core.dtype, device=core.dev)
         self.bounds = [(0, min(chunk, max_length))]
         s = chunk
@@ -632,16 +639,18 @@ class DecodeRunner:
             ds.tokens.fill_(core.cfg.eos_token_id)
             ops.add_position(self.prefix, P * D, D, core.wpe, ds.x, B=B, npos=P, D=D, pos0=0)
             core._decode_block(ds, P * B, ds.x, 0, P, prefill=True)
-            core._decode_head(ds, ds.x[(P - 1) * B: P * B], 0, P)
+            core._decode_head(ds, ds.x[(P - 1) * B: P * B], 0, P, self.samp)
             s0 = 1
         for s in range(s0, s1):
             pos = P + s - 1
             core._decode_block(ds, B, ds.x[:B], pos, 1, prefill=False)
-            core._decode_head(ds, ds.x[:B], s, pos + 1)
+            core._decode_head(ds, ds.x[:B], s, pos + 1, self.samp)
 
     @torch.no_grad()
-    def run(self, prefix: Tensor, early_exit: bool = True, check_every: int = 8) -> Tensor:
+    def run(self, prefix: Tensor, early_exit: bool = True, check_every: int = 8, seed: int = 0) -> Tensor:
         self.prefix.copy_(prefix)
+        if self.samp is not None:
+            self.seed_dev.fill_(seed)
         if self.graphs is None:
             for c in range(len(self.bounds)):  # eager warm-up pass (initialises every kernel once)
                 self._chunk(c)

@@ -396,15 +396,12 @@ def _hash32(seed: int, idx: np.ndarray) -> np.ndarray:
     return x.astype(np.uint32)
 
 
-def _fkey(l: np.ndarray) -> np.ndarray:
-    u = l.astype(np.float32).view(np.uint32)
-    return np.where(u & np.uint32(0x80000000), ~u, u | np.uint32(0x80000000)).astype(np.uint32)
-
-
 def topp_sample_fixed(logits: np.ndarray, temperature: float, top_p: float, seed: int, step: int,
                       finished: Optional[np.ndarray] = None, eos: int = 50256):
     """Nucleus draw restated with the kernel's arithmetic conventions (icap_topp_sample, include/icap.h) over
-    the reference filter of src/models.py:400-449: stable descending rank, probabilities as 2^31 fixed point
+    the reference filter of src/models.py:400-449: stable rank by descending fixed-point probability (equal
+    logits tie as in the reference; distinct logits closer than 2^-31 in probability also tie, by index),
+    probabilities as 2^31 fixed point
     q = trunc(f32(e) * f32(2^31 / Z)), Z = sum(trunc(e * 2^40)) / 2^40, keep ranks 0..r with r the first rank whose inclusive mass exceeds
     trunc(top_p * 2^31), then inverse CDF in index order at u = hash32(seed, step << 32 | row).
     Returns (tokens int64 [B], kept bool [B, V])."""
@@ -423,8 +420,7 @@ def topp_sample_fixed(logits: np.ndarray, temperature: float, top_p: float, seed
         keep = np.ones(V, dtype=bool)
         if np.float32(top_p) < 1.0:
             thr = np.uint64(int(float(np.float32(top_p)) * 2147483648.0))
-            key = _fkey(l)
-            order = np.argsort(~key, kind="stable")  # descending key, ascending index on ties
+            order = np.argsort(-q.astype(np.int64), kind="stable")  # descending q, ascending index on ties
             cum = np.cumsum(q[order])
             over = np.nonzero(cum > thr)[0]
             if over.size:

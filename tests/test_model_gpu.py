@@ -99,6 +99,17 @@ def test_tiny_generate_sampling_branch(dev):
     for row in a.tolist():
         if TINY_G.eos in row:
             assert all(t == TINY_G.eos for t in row[row.index(TINY_G.eos):])
+    gc = model._gcore()
+    gc.graph_decode = False  # the eager loop draws the same tokens as the graph-chunk runner for one seed
+    try:
+        torch.manual_seed(0)
+        c = model.generate(emb, max_length=12, temperature=1.2, top_p=0.9).cpu()
+    finally:
+        gc.graph_decode = True
+    assert torch.equal(a, c)
+    torch.manual_seed(1)
+    d = model.generate(emb, max_length=12, temperature=1.2, top_p=0.9).cpu()
+    assert not torch.equal(a, d)  # the seed reaches the captured graphs through device memory
     gen = model.generate(emb, max_length=20, temperature=0.0)
     assert np.array_equal(gen.cpu().numpy(), g["greedy"])
 
