@@ -299,7 +299,8 @@ def main():
     if not args.no_decode:
         caps_per_s, dt, nd, lens = greedy_rate(model, Bd, dev, world, 768 if args.config == "medium" else 512)
     topp = None if args.no_decode else topp_rate(model, Bd, dev, world, 768 if args.config == "medium" else 512)
-    traffic, traffic_src = pmc_traffic(dom)
+    # the committed PMC pass measured the configs[1] step: its per-launch bytes do not describe other configs
+    traffic, traffic_src = pmc_traffic(dom) if args.config == "small" else (None, None)
     prep = None if args.no_decode else preprocess_rate(dev)
 
     if rank == 0:
