@@ -134,6 +134,10 @@ def accesses(name, args):
         out += [("logits", lg, _rows(B, ld, V, es)), ("forced", forced, B * 8), ("finished", fin, B * 4),
                 ("tokens", tok, ((B - 1) * ldt + step + 1) * 8), ("wte", wte, D * es),
                 ("wpe", wpe, (pos + 1) * D * es), ("x", x, B * D * es)]
+    elif name == "icap_topp_sample":
+        dt, B, V, lg, ld, _t, _p, fin, _seed, seed_ptr, _step, _eos, outp, _s = a
+        out += [("logits", lg, _rows(B, ld, V, ES[dt])), ("finished", fin, B * 4), ("seed_ptr", seed_ptr, 8),
+                ("out", outp, B * 8)]
     elif name == "icap_add_position":
         dt, B, npos, D, src, sbs, sts, wpe, pos0, x, _s = a
         es = ES[dt]

@@ -86,6 +86,7 @@ def test_inference_and_greedy_in_bounds():
         with torch.no_grad():
             model(ids, emb, mask, labels)
         model.generate(emb, max_length=9, temperature=0.0)
+        model.generate(emb, max_length=9, temperature=0.8, top_p=0.9)
         model.gpt(inputs_embeds=torch.randn(2, 7, 128), attention_mask=torch.ones(2, 7, dtype=torch.int64))
         _assert_clean(rec)
 
