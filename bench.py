@@ -154,8 +154,9 @@ def greedy_rate(model, Bd, dev, world, edim=512):
 
 def topp_rate(model, Bd, dev, world, edim=512, temperature=1.0, top_p=0.9):
     """50-token KV-cached nucleus-sampled captions/s (src/models.py:400-449 branch: HIP top-p filter + draw per
-    step, host EOS check per step as in the reference loop). Random-init weights rarely emit EOS, so every
-    caption runs all 50 steps."""
+    step). The decode runs as HIP-graph chunks of 8 tokens and the host reads the EOS latch once per chunk (the
+    reference checks it every step; the returned ids are truncated to the reference loop's length either way).
+    Random-init weights rarely emit EOS, so every caption runs all 50 steps."""
     g = torch.Generator().manual_seed(6)
     emb = torch.randn((Bd, edim), generator=g)
     emb = (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
@@ -221,9 +222,45 @@ def pmc_traffic(kernel: str):
     return best if best else (None, None)
 
 
+def launch_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` without a torchrun environment: start N data-parallel ranks (one process per GPU)
+    through torch.distributed.run on 127.0.0.1 and return their exit status. This parent makes no GPU call (it
+    only spawns and waits), so the ranks own the devices; rank 0 prints the one JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL peer setup)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd, env=env)
+
+
+def launcher_probe():
+    """--launcher-probe: what each rank sees (CPU / gloo only, no GPU): one JSON line from rank 0 listing every
+    rank's (RANK, LOCAL_RANK, WORLD_SIZE). Lets the CPU test suite check the --gpus N launcher."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    me = torch.tensor([rank, local, world], dtype=torch.int64)
+    seen = [me]
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+        seen = [torch.zeros_like(me) for _ in range(world)]
+        torch.distributed.all_gather(seen, me)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks": [s.tolist() for s in seen]}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--launcher-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=128)
@@ -235,7 +272,13 @@ def main():
                     help="small = BASELINE configs[1] (default, the headline); medium = configs[3]")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.launcher_probe:
+        return launcher_probe()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1

@@ -633,7 +633,9 @@ __global__ void add_position_kernel(int B, int npos, int D, const T* __restrict_
 // The reference filter (sort descending, cumsum(softmax), remove where cumsum > top_p, shifted right by one)
 // keeps ranks 0..r, r = the first rank whose inclusive cumsum exceeds top_p. Ranks here run by descending q
 // and, among equal q, ascending index (a stable sort): equal logits tie exactly as in the reference; distinct
-// logits whose probabilities differ by less than 2^-31 also tie here (the one documented deviation).
+// logits whose probabilities differ by less than 2^-31 also tie here (documented deviation 1). Tokens whose
+// probability is below 2^-31 get q = 0 and are never drawn, even with top_p >= 1 (documented deviation 2: the
+// reference's multinomial would draw such a token with probability < 2^-31 per row and step).
 // K* = min{K : mass(q > K) <= T} (bisection over q) is the q of rank r; of the c tokens tied at K* the first
 // (T - A) / K* + 1 by index are kept, A = mass(q > K*). The draw is an inverse CDF over the kept tokens in vocabulary order with
 // u = hash32(seed, step << 32 | row) / 2^32: torch.multinomial's stream is not reproducible across devices,

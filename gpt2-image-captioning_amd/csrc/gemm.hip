@@ -1444,10 +1444,12 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   } else if (p.split_k == 0 && p.workspace && (p.N & 3) == 0 && nk >= 2 && (tiles <= 64 || (tiles < 256 && nk >= 16))) {
     // decode-sized launches (<= 64 tiles): as many splits as fill ~2 blocks/CU; under-filled long-K launches
     // (dW products over all tokens, K = 3200+): keep >= 4 stages per split so the slab traffic stays small
+    // the count depends on the shape alone — never on the workspace a caller passes — so a product computed on
+    // another stream with its own scratch sums its K ranges in the same order and rounds identically (a
+    // workspace too small for the shape's split is an error below, not a silent change of the summation order)
     splits = (512 + tiles - 1) / tiles;
     if (tiles > 64 && splits > nk / 4) splits = nk / 4;
     if (splits > 32) splits = 32;
-    if (splits > p.workspace_bytes / slab) splits = p.workspace_bytes / slab;
   }
   if (splits > nk) splits = nk;
   if (splits < 1) splits = 1;

@@ -12,6 +12,7 @@ from __future__ import annotations
 import hashlib
 import json
 import os
+import tempfile
 from dataclasses import dataclass
 from typing import Optional
 
@@ -32,8 +33,9 @@ class CocoDataset(Dataset):
     reference's per-item __getitem__ (dataset.py:181-188: caption + eos_token, max_length, padding="max_length",
     truncation) and keeps int32 ids / int8 mask arrays, so __getitem__ is a row slice instead of a tokenizer
     call (the per-item BPE gates the loader at device rates). `token_cache_path` stores
-    those arrays (torch.save of plain tensors, loaded with weights_only=True) keyed by a digest of the
-    caption texts, max_length and the tokenizer's eos token."""
+    those arrays (torch.save of plain tensors, loaded with weights_only=True, written to a temporary file and
+    renamed into place) keyed by a digest of the caption texts, max_length and the tokenizer's identity (class,
+    vocabulary size and files, pad / eos, padding and truncation sides)."""
 
     def __init__(self, embeddings_path: str, annotations_path: str, tokenizer=None, max_length: int = 50,
                  normalize_embeddings: bool = False, *, pretokenize: bool = True,
@@ -67,9 +69,28 @@ class CocoDataset(Dataset):
         eos = self.tokenizer.eos_token
         return [c.caption_text + eos for c in self.captions]
 
+    def _tokenizer_key(self) -> str:
+        """What makes two tokenizers produce the same ids: class, vocabulary size, pad / eos, padding and
+        truncation sides, and the bytes of its vocabulary files when it names them."""
+        tok = self.tokenizer
+        parts = [type(tok).__name__, str(getattr(tok, "vocab_size", None)), str(len(tok) if hasattr(tok, "__len__")
+                                                                               else None),
+                 str(getattr(tok, "pad_token_id", None)), str(getattr(tok, "eos_token", None)),
+                 str(getattr(tok, "padding_side", None)), str(getattr(tok, "truncation_side", None))]
+        files = getattr(tok, "vocab_files_names", None) or {}
+        init = getattr(tok, "init_kwargs", None) or {}
+        h = hashlib.sha1()
+        for key in sorted(files):
+            path = init.get(key)
+            if isinstance(path, str) and os.path.isfile(path):
+                with open(path, "rb") as f:
+                    h.update(f.read())
+        parts.append(h.hexdigest())
+        return "|".join(parts)
+
     def _pretokenize(self, cache_path: Optional[str], chunk: int = 8192) -> None:
         texts = self._texts()
-        h = hashlib.sha1(f"{self.max_length}|{self.tokenizer.eos_token}|{len(texts)}".encode())
+        h = hashlib.sha1(f"{self.max_length}|{self._tokenizer_key()}|{len(texts)}".encode())
         for t in texts:
             h.update(t.encode("utf-8"))
             h.update(b"\0")
@@ -88,8 +109,16 @@ class CocoDataset(Dataset):
             ids[s: s + chunk] = enc.input_ids
             mask[s: s + chunk] = enc.attention_mask
         self.token_ids, self.token_mask = ids, mask
-        if cache_path:
-            torch.save({"digest": digest, "ids": ids, "mask": mask}, cache_path)
+        if cache_path:  # write-then-rename: concurrent builders (one per DP rank) never expose a partial file
+            d = os.path.dirname(os.path.abspath(cache_path))
+            fd, tmp = tempfile.mkstemp(prefix=".tokcache.", dir=d)
+            os.close(fd)
+            try:
+                torch.save({"digest": digest, "ids": ids, "mask": mask}, tmp)
+                os.replace(tmp, cache_path)
+            finally:
+                if os.path.exists(tmp):
+                    os.remove(tmp)
 
     def __len__(self) -> int:
         return len(self.captions)

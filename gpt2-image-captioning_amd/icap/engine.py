@@ -83,7 +83,7 @@ class CaptionTrainer:
         self.adam_state = torch.zeros(16, dtype=torch.float32, device=self.dev)
         self.adam_ws = torch.empty(ops.adamw_workspace(flat.n), dtype=torch.uint8, device=self.dev)
         self.loss_sum = torch.zeros(1, dtype=torch.float32, device=self.dev)
-        self.graph = None
+        self.graphs = {}  # (zero, with_optimizer) -> captured HIP graph
         self.graph_opt = None
         self._micro = 0
         self._eager_steps = 0
@@ -165,55 +165,78 @@ class CaptionTrainer:
     def grad_scale(self) -> float:
         return 1.0 / (self.grad_accum_steps * self.world)
 
-    def micro_step(self, use_graph: bool = False) -> bool:
-        """One micro-batch (forward + backward). Returns True when an optimizer step was taken
-        (every grad_accum_steps micro-batches, src/train.py:146-159). With use_graph the first call runs
-        eagerly (warm-up) and every later call replays one captured HIP graph of the whole step."""
+    def micro_step(self, use_graph: bool = False, zero: Optional[bool] = None, step: Optional[bool] = None) -> bool:
+        """One micro-batch (forward + backward). Returns True when an optimizer step was taken.
+
+        zero: start a new accumulation cycle (the gradients are cleared first); step: take the optimizer step
+        after this micro-batch. Both default to this trainer's own count (a step every grad_accum_steps
+        micro-batches); icap.train passes them explicitly from the batch index, as src/train.py:128-159 does
+        (step when (batch_idx + 1) % grad_accum_steps == 0 or at the last batch), so a cycle may span trainers
+        of different batch shapes (a short last batch) — they share one flat gradient buffer.
+        With use_graph the first call runs eagerly (warm-up) and every later call replays a captured HIP graph
+        (one per (zero, step) form)."""
         self.model.sync_compute_copies()
-        first = self._micro == 0
-        if use_graph and self.graph is None and self._eager_steps >= 1 and self.grad_accum_steps == 1:
-            self.capture()
-        if self.graph is not None and self.grad_accum_steps == 1:
-            self.graph.replay()
-            if self.world > 1:
+        if zero is None:
+            zero = self._micro == 0
+        if step is None:
+            step = self._micro + 1 >= self.grad_accum_steps
+        if use_graph and self._eager_steps >= 1:
+            with_opt = step and self.world == 1
+            g = self.graphs.get((zero, with_opt))
+            if g is None:
+                g = self._capture(zero, with_opt)
+            g.replay()
+            if step and self.world > 1:
                 self._allreduce()
+                if self.graph_opt is None:
+                    self.graph_opt = self._capture_opt()
                 self.graph_opt.replay()
-            self._micro = 0
-            return True
-        self._fwd_bwd(first, self.grad_scale())
-        self._micro += 1
-        self._eager_steps += 1
-        if self._micro == self.grad_accum_steps:
-            self._allreduce()
-            self._optimizer()
-            self._micro = 0
-            return True
-        return False
+        else:
+            self._fwd_bwd(zero, self.grad_scale())
+            self._eager_steps += 1
+            if step:
+                self._allreduce()
+                self._optimizer()
+        self._micro = 0 if step else self._micro + 1
+        return step
 
     def flush(self) -> None:
-        """Apply a pending partial accumulation (src/train.py:146-148 last-batch rule)."""
+        """Apply a pending partial accumulation of this trainer's own count (the last-batch rule of
+        src/train.py:146-148 for callers that use the default micro_step flags)."""
         if self._micro:
             self._allreduce()
             self._optimizer()
             self._micro = 0
 
-    def capture(self) -> None:
-        """Capture fwd+bwd(+optimizer when single-process) into HIP graphs (recording only: nothing executes;
-        call after at least one eager step so every kernel and attribute has been initialised)."""
-        if self.grad_accum_steps != 1:
-            return
+    @property
+    def graph(self):
+        """The plain-step graph (new cycle + optimizer step), once captured."""
+        return self.graphs.get((True, self.world == 1))
+
+    def _capture(self, zero: bool, with_opt: bool):
+        """Capture fwd+bwd (+ optimizer) into a HIP graph (recording only: nothing executes; called after at
+        least one eager step so every kernel and attribute has been initialised)."""
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._fwd_bwd(True, self.grad_scale())
-            if self.world == 1:
+            self._fwd_bwd(zero, self.grad_scale())
+            if with_opt:
                 self._optimizer()
-        self.graph = g
-        if self.world > 1:
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2):
-                self._optimizer()
-            self.graph_opt = g2
+        self.graphs[(zero, with_opt)] = g
+        return g
+
+    def _capture_opt(self):
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._optimizer()
+        return g
+
+    def capture(self) -> None:
+        """Capture the plain step (new cycle + optimizer) ahead of time."""
+        self._capture(True, self.world == 1)
+        if self.world > 1 and self.graph_opt is None:
+            self.graph_opt = self._capture_opt()
 
     def take_loss_sum(self) -> float:
         v = float(self.loss_sum.item())

@@ -220,6 +220,8 @@ class ImageCaptioningModel(nn.Module):
         prefix = pre.as_strided((B, P, D), (pbs, D, 1))
         if temperature == 0:
             return gc.greedy_decode(prefix, max_length, early_exit=early_exit)
+        if temperature < 0:  # src/models.py:401-407: divide by 1.0 and skip the top-p filter (full softmax draw)
+            temperature, top_p = 1.0, 1.0
         return gc.sample_decode(prefix, max_length, temperature, top_p)
 
     def generate_captions(self, image_embeddings: Tensor, **kwargs) -> List[str]:

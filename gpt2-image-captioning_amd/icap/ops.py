@@ -73,7 +73,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
     workspace: fp32 split-K scratch for launches on a stream other than the package's main one (the per-device
-    default serves every GEMM ordered on one stream; splits are capped to what the scratch holds).
+    default serves every GEMM ordered on one stream). The split count depends on the shape alone, so the result
+    is bitwise the same with any workspace; one too small for the shape's split raises.
     trans_ab: A and B are K-outer ([K, M] / [K, N] row-major: out = epi(alpha * A^T @ B)), bf16 only.
     ln: (gamma, beta, eps) — A is LayerNorm-ed over its K columns inside the GEMM (M <= 128 launches).
     alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).

@@ -69,42 +69,53 @@ def train(train_dataset, model, batch_size: int, num_epochs: int, num_workers: i
     val_metrics_history: list[dict[str, Any]] = []
     best_val_cider, best_epoch = -1.0, 0
     step_idx = 0
+    n_batches = len(dl)
     for epoch in range(num_epochs):
         model.train()
         if sampler is not None:
             sampler.set_epoch(epoch)
         nb = 0
-        loss_acc = torch.zeros(1, device=device)
-        active = None
+        loss_acc = torch.zeros(2, dtype=torch.float64, device=device)  # [sum of batch losses, batch count]
         for batch_idx, batch in enumerate(dl):
             ids, mask, labels = batch["token_ids"], batch["attention_mask"], batch["labels"]
             t = trainer_for(ids.shape[0], ids.shape[1])
-            if active is not None and active is not t:
-                active.flush()
-            active = t
             pixels = batch.get("pixel_values") if clip_model is not None else None
             t.load_batch(ids.to(device, non_blocking=True), mask.to(device, non_blocking=True),
                          labels.to(device, non_blocking=True), emb=batch["image_embedding"].to(device, non_blocking=True),
                          pixels=pixels.to(device, non_blocking=True) if pixels is not None else None)
-            t.micro_step(use_graph=use_graph)
-            loss_acc += t.last_loss
+            # train.py:128-159: a cycle starts after each optimizer step; the step is taken every grad_accum_steps
+            # batches and at the last batch of the epoch. The cycle's micro-batches accumulate into one shared
+            # gradient buffer even when a short last batch runs on another trainer (its own batch shape).
+            zero = batch_idx % grad_accum_steps == 0
+            step = (batch_idx + 1) % grad_accum_steps == 0 or batch_idx + 1 == n_batches
+            t.micro_step(use_graph=use_graph, zero=zero, step=step)
+            loss_acc[0] += t.last_loss[0]
             nb += 1
             step_idx += 1
             if log_every and (batch_idx + 1) % log_every == 0:
                 print(f"Epoch {epoch + 1}/{num_epochs} batch {batch_idx + 1} loss {t.last_loss.item():.4f}")
-        if active is not None:
-            active.flush()
-        avg = float(loss_acc.item()) / max(nb, 1)
+        loss_acc[1] = nb
+        if dist:  # every rank's batches count towards the epoch mean (train.py:169 over the whole dataloader)
+            torch.distributed.all_reduce(loss_acc)
+        avg = float(loss_acc[0].item()) / max(float(loss_acc[1].item()), 1.0)
         epoch_loss_values.append(avg)
-        print(f"Epoch {epoch + 1} completed. Average Loss: {avg:.4f}")
+        if is_main:
+            print(f"Epoch {epoch + 1} completed. Average Loss: {avg:.4f}")
         if is_main and ((epoch + 1) % save_every_epoch == 0 or (epoch + 1) == num_epochs):
             path = os.path.join(outputs_dir, f"model_epoch_{epoch + 1}.pt")
             model.save_parameters(path)
         if val_dataset is not None and (epoch + 1) % eval_every_epoch == 0:
             from .evaluate import evaluate_epoch
 
-            m = evaluate_epoch(model, val_dataset, val_annotations_path, epoch + 1, "val", eval_batch_size,
-                               num_workers, eval_max_length, eval_temperature, eval_top_p, device, eval_dir)
+            # replicated weights: rank 0 decodes and writes the predictions file, then shares the metrics
+            m = None
+            if is_main:
+                m = evaluate_epoch(model, val_dataset, val_annotations_path, epoch + 1, "val", eval_batch_size,
+                                   num_workers, eval_max_length, eval_temperature, eval_top_p, device, eval_dir)
+            if dist:
+                box = [m]
+                torch.distributed.broadcast_object_list(box, src=0)
+                m = box[0]
             val_metrics_history.append({"epoch": epoch + 1, "loss": avg, **m})
             cider = m.get("cider", -1.0)
             if cider > best_val_cider:

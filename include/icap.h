@@ -87,7 +87,9 @@ typedef struct {
   /* split-K: fp32 scratch of >= splits*M*N*4 bytes (16-byte aligned) or NULL.   */
   /* split_k: 0 = automatic (only launches of <= 64 output tiles, N % 4 == 0,   */
   /* and only when the workspace is given), 1 = never, > 1 = forced.            */
-  /* The partial sums are reduced in a fixed order (deterministic).             */
+  /* The partial sums are reduced in a fixed order (deterministic). The split   */
+  /* count is a function of (M, N, K, dtype) only: a workspace smaller than     */
+  /* that split needs is ICAP_ERR_ARG, never a different summation order.       */
   void* workspace; int64_t workspace_bytes; int32_t split_k;
   /* optional device-side row count (int32, <= M): only rows < *m_dev are     */
   /* computed and stored; the launch geometry stays sized for M, so a graph   */

@@ -83,13 +83,21 @@ def test_token_cache_reused_and_invalidated(tok, files):
     first = CocoDataset(emb, ann, tokenizer=tok, max_length=20, token_cache_path=cache)
     assert os.path.exists(cache)
 
-    class NoCall:  # the cache must be used: calling the tokenizer again would fail
-        eos_token = tok.eos_token
+    def no_call(*a, **k):  # the cache must be used: calling the tokenizer again would fail
+        raise AssertionError("tokenizer called despite a valid cache")
 
-        def __call__(self, *a, **k):
-            raise AssertionError("tokenizer called despite a valid cache")
+    from unittest import mock
 
-    again = CocoDataset(emb, ann, tokenizer=NoCall(), max_length=20, token_cache_path=cache)
-    assert torch.equal(again.token_ids, first.token_ids) and torch.equal(again.token_mask, first.token_mask)
-    with pytest.raises(AssertionError, match="despite"):  # other max_length -> digest mismatch -> re-tokenise
-        CocoDataset(emb, ann, tokenizer=NoCall(), max_length=21, token_cache_path=cache)
+    with mock.patch.object(type(tok), "__call__", no_call):
+        again = CocoDataset(emb, ann, tokenizer=tok, max_length=20, token_cache_path=cache)
+        assert torch.equal(again.token_ids, first.token_ids) and torch.equal(again.token_mask, first.token_mask)
+        with pytest.raises(AssertionError, match="despite"):  # other max_length -> digest mismatch -> re-tokenise
+            CocoDataset(emb, ann, tokenizer=tok, max_length=21, token_cache_path=cache)
+        side = tok.padding_side
+        tok.padding_side = "left" if side == "right" else "right"
+        try:  # a tokenizer that pads differently must not reuse the cache either
+            with pytest.raises(AssertionError, match="despite"):
+                CocoDataset(emb, ann, tokenizer=tok, max_length=20, token_cache_path=cache)
+        finally:
+            tok.padding_side = side
+    assert not [f for f in os.listdir(d) if f.startswith(".tokcache.")]  # no temporary file left behind

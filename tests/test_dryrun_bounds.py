@@ -91,6 +91,39 @@ def test_inference_and_greedy_in_bounds():
         _assert_clean(rec)
 
 
+def test_train_grad_accum_short_last_batch_steps_like_reference(tmp_path):
+    """src/train.py:128-159 with grad_accum_steps=4 over 6 batches (11 samples, batch 2: the last batch has 1
+    sample and runs on its own trainer): optimizer steps after batches 4 and 6 only — 2 AdamW calls per epoch —
+    and the short batch accumulates into the same cycle (its gradients are not cleared first)."""
+    import icap
+    from icap.dataset import SyntheticCaptionDataset
+
+    ds = SyntheticCaptionDataset(11, max_length=12, real=5, vocab_size=512, eos=511, embed_dim=64)
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model()
+        flags = []
+        orig = icap.CaptionTrainer.micro_step
+
+        def micro_step(self, use_graph=False, zero=None, step=None):
+            flags.append((self.B, zero, step))
+            return orig(self, use_graph=use_graph, zero=zero, step=step)
+
+        icap.CaptionTrainer.micro_step = micro_step
+        try:
+            icap.train(ds, model, batch_size=2, num_epochs=2, num_workers=0, device=CPU, grad_accum_steps=4,
+                       outputs_dir=str(tmp_path), save_every_epoch=10, use_graph=False)
+        finally:
+            icap.CaptionTrainer.micro_step = orig
+        _assert_clean(rec)
+    n_adamw = sum(1 for c in rec.calls if c[0] == "icap_adamw_step")
+    assert n_adamw == 4, n_adamw  # 2 per epoch
+    epoch = flags[:6]
+    assert [f[0] for f in epoch] == [2, 2, 2, 2, 2, 1]
+    assert [f[1] for f in epoch] == [True, False, False, False, True, False]
+    assert [f[2] for f in epoch] == [False, False, False, True, False, True]
+
+
 def test_gpt2_small_bench_shape_with_clip_in_bounds():
     """The benchmarked configuration (GPT-2 small + ViT-B/32 + transformer mapper, bf16) at B=8."""
     with dry_run() as rec:
