@@ -1,7 +1,7 @@
 // Multi-head softmax attention for the short sequences of the captioning path
 // (GPT-2 S=65 causal+padding, CLIP S=50, mapper S=25 with head_dim 96).
 //
-// One workgroup per (batch, head): Q, K, V (and dO in backward) are staged once
+// One workgroup per (batch, head) (forward: per query chunk when S x S overflows LDS): Q, K, V (and dO in backward) are staged once
 // from HBM into LDS as fp32 (rows padded to hd+1 floats so column walks are
 // bank-conflict free), the S x S score block lives in LDS, softmax row
 // reductions use wave shuffles, and P.V / dS.K / dS^T.Q / P^T.dO are LDS dot
@@ -40,27 +40,40 @@ __device__ __forceinline__ bool allowed(int causal, const int32_t* key_mask, int
   return true;
 }
 
+// Query rows [q0, q0 + QT) of one (batch, head) per workgroup (blockIdx.y = chunk): K and V stay whole in LDS, the
+// score block is QT x S. QT == S for the short sequences (one chunk); the towers' S=197/257 fp32 parity mode uses
+// QT < S so the block fits the 160 KB LDS. Every row's arithmetic is the same whatever QT is.
 template <typename T>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeom g, uint32_t thr, float inv_keep) {
+__global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeom g, int QT, uint32_t thr, float inv_keep) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int bh = blockIdx.x;
   const int b = bh / g.H, h = bh - b * g.H;
   const int S = g.S, hd = g.hd, ldp = hd + 1;
-  float* Qs = sm;
-  float* Ks = Qs + S * ldp;
+  const int q0 = blockIdx.y * QT, nq = min(QT, S - q0);
+  float* Ks = sm;
   float* Vs = Ks + S * ldp;
-  float* P = Vs + S * ldp;
+  float* Qs = Vs + S * ldp;
+  float* P = Qs + QT * ldp;
   const T* qkv = reinterpret_cast<const T*>(p.qkv);
-  stage_head<T>(qkv, p.ld_qkv, h * hd, g, b, Qs, ldp, p.scale);
   stage_head<T>(qkv, p.ld_qkv, g.D + h * hd, g, b, Ks, ldp, 1.f);
   stage_head<T>(qkv, p.ld_qkv, 2 * g.D + h * hd, g, b, Vs, ldp, 1.f);
+  {
+    const int nv = hd >> 2;
+    for (int idx = threadIdx.x; idx < nq * nv; idx += blockDim.x) {
+      const int s = idx / nv, c = idx - s * nv;
+      float v[4];
+      io<T>::ld4(qkv + tok_row(g, b, q0 + s) * p.ld_qkv + h * hd + 4 * c, v);
+      float* d = Qs + s * ldp + 4 * c;
+      d[0] = v[0] * p.scale; d[1] = v[1] * p.scale; d[2] = v[2] * p.scale; d[3] = v[3] * p.scale;
+    }
+  }
   __syncthreads();
 
-  for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
-    const int i = idx / S, j = idx - i * S;
+  for (int idx = threadIdx.x; idx < nq * S; idx += blockDim.x) {
+    const int il = idx / S, j = idx - il * S;
     float s = -INFINITY;
-    if (allowed(p.causal, p.key_mask, b, S, i, j)) {
-      const float* q = Qs + i * ldp;
+    if (allowed(p.causal, p.key_mask, b, S, q0 + il, j)) {
+      const float* q = Qs + il * ldp;
       const float* k = Ks + j * ldp;
       float a0 = 0.f, a1 = 0.f;
       for (int d = 0; d < hd; d += 2) {
@@ -76,8 +89,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeo
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   const uint64_t drop_base = p.offset + (uint64_t)bh * S * S;
   const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
-  for (int i = wv; i < S; i += nwv) {
-    float* row = P + i * S;
+  for (int il = wv; il < nq; il += nwv) {
+    const int i = q0 + il;
+    float* row = P + il * S;
     float m = -INFINITY;
     for (int j = lane; j < S; j += 64) m = fmaxf(m, row[j]);
     m = wave_max(m);
@@ -95,9 +109,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeo
   __syncthreads();
 
   T* out = reinterpret_cast<T*>(p.out);
-  for (int idx = threadIdx.x; idx < S * hd; idx += blockDim.x) {
-    const int i = idx / hd, d = idx - i * hd;
-    const float* row = P + i * S;
+  for (int idx = threadIdx.x; idx < nq * hd; idx += blockDim.x) {
+    const int il = idx / hd, d = idx - il * hd;
+    const float* row = P + il * S;
     float a0 = 0.f, a1 = 0.f;
     int j = 0;
     for (; j + 1 < S; j += 2) {
@@ -105,7 +119,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeo
       a1 = fmaf(row[j + 1], Vs[(j + 1) * ldp + d], a1);
     }
     if (j < S) a0 = fmaf(row[j], Vs[j * ldp + d], a0);
-    io<T>::st(out + tok_row(g, b, i) * p.ld_out + h * hd + d, a0 + a1);
+    io<T>::st(out + tok_row(g, b, q0 + il) * p.ld_out + h * hd + d, a0 + a1);
   }
 }
 
@@ -250,13 +264,24 @@ static bool force_valu() {
   return f;
 }
 
-static size_t fwd_lds(int S, int hd) { return sizeof(float) * ((size_t)3 * S * (hd + 1) + (size_t)S * S); }
+static size_t fwd_lds(int S, int hd, int QT) {
+  return sizeof(float) * ((size_t)(2 * S + QT) * (hd + 1) + (size_t)QT * S);
+}
 static size_t bwd_lds(int S, int hd) { return sizeof(float) * ((size_t)4 * S * (hd + 1) + (size_t)2 * S * S); }
 constexpr size_t LDS_CAP = 160 * 1024;
 
 template <typename K>
 static void raise_lds_limit(K kernel) {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_CAP);
+}
+
+// Query rows per forward workgroup: the whole sequence when it fits, else the largest power of two that does
+// (0 = K and V alone overflow LDS).
+static int fwd_rows(int S, int hd) {
+  if (fwd_lds(S, hd, S) <= LDS_CAP) return S;
+  for (int qt = 128; qt >= 4; qt >>= 1)
+    if (qt < S && fwd_lds(S, hd, qt) <= LDS_CAP) return qt;
+  return 0;
 }
 
 static int check_attn(const icap_attn_args* a, bool bwd) {
@@ -281,17 +306,18 @@ extern "C" int icap_attention_fwd(const icap_attn_args* a, void* stream) {
   AttnGeom g{a->S, a->H, a->hd, a->H * a->hd, a->row_stride_b, a->row_stride_s};
   const uint32_t thr = a->drop_p > 0.f ? drop_threshold(a->drop_p) : 0u;
   const float inv_keep = a->drop_p > 0.f ? 1.f / (1.f - a->drop_p) : 1.f;
-  const size_t lds = fwd_lds(a->S, a->hd);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!force_valu() && mfma_attention_ok(a, false)) return mfma_attention_launch(a, false, thr, inv_keep, s);
-  ICAP_REQUIRE(fwd_lds(a->S, a->hd) <= LDS_CAP, "icap_attention: sequence/head too large for the LDS-resident kernel");
-  dim3 grid((unsigned)(a->B * a->H)), block(256);
+  const int QT = fwd_rows(a->S, a->hd);
+  ICAP_REQUIRE(QT > 0, "icap_attention: sequence/head too large for the LDS-resident kernel");
+  const size_t lds = fwd_lds(a->S, a->hd, QT);
+  dim3 grid((unsigned)(a->B * a->H), (unsigned)((a->S + QT - 1) / QT)), block(256);
   if (a->dtype == ICAP_BF16) {
     static bool once = (raise_lds_limit(attn_fwd_kernel<bf16_t>), true); (void)once;
-    hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, grid, block, lds, s, *a, g, thr, inv_keep);
+    hipLaunchKernelGGL(attn_fwd_kernel<bf16_t>, grid, block, lds, s, *a, g, QT, thr, inv_keep);
   } else {
     static bool once = (raise_lds_limit(attn_fwd_kernel<float>), true); (void)once;
-    hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, block, lds, s, *a, g, thr, inv_keep);
+    hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, block, lds, s, *a, g, QT, thr, inv_keep);
   }
   return check_launch("icap_attention_fwd");
 }

@@ -139,6 +139,7 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
     case ICAP_ACT_RELU: return x > 0.f ? x : 0.f;
     case ICAP_ACT_QUICK_GELU: return x / (1.f + __expf(-1.702f * x));
     case ICAP_ACT_TANH: return tanhf(x);
+    case ICAP_ACT_GELU_ERF: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));  // HF ACT2FN["gelu"]
     default: return x;
   }
 }
@@ -160,6 +161,8 @@ __device__ __forceinline__ float act_bwd(int act, float a) {
       return s + a * 1.702f * s * (1.f - s);
     }
     case ICAP_ACT_TANH: return 1.f - a * a;
+    case ICAP_ACT_GELU_ERF:  // Phi(a) + a phi(a)
+      return 0.5f * (1.f + erff(a * 0.70710678118654752f)) + a * 0.3989422804014327f * __expf(-0.5f * a * a);
     default: return 1.f;
   }
 }

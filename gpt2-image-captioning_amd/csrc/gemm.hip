@@ -151,6 +151,51 @@ __device__ __forceinline__ void unpack_bf16(const uint4 w, float v[8]) {
   unpack_bf16(make_uint2(w.z, w.w), v + 4);
 }
 
+// The epilogue arithmetic, shared by every GEMM kernel (tile, split-K reduce, skinny, ring): one formula with a
+// fixed contraction (explicit fma for alpha*acc + bias, no other fusing), so two kernels that accumulate a product
+// in the same order store bitwise-identical outputs (tests/test_gemm_ring_gpu.py).
+// backward form: x = alpha * acc * dropmask * act'(a)
+template <int W>
+__device__ __forceinline__ void epi_bwd_math(const icap_gemm_args& p, float x[W], const float a[W], uint64_t seed,
+                                             uint64_t didx, uint32_t drop_thresh, float inv_keep) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int e = 0; e < W; ++e) {
+    float y = p.alpha * x[e];
+    if (drop_thresh != 0u) y = y * drop_scale(seed, didx + e, drop_thresh, inv_keep);
+    x[e] = y * act_bwd(p.dact, a[e]);
+  }
+}
+// forward form, first half: x = act(alpha * acc + bias); a = the aux value (pre-activation, or tanh output)
+template <int W>
+__device__ __forceinline__ void epi_fwd_act(const icap_gemm_args& p, float x[W], const float biasw[W], float a[W]) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int e = 0; e < W; ++e) x[e] = __builtin_fmaf(p.alpha, x[e], biasw[e]);
+  if (p.act != ICAP_ACT_NONE || p.aux) {
+#pragma unroll
+    for (int e = 0; e < W; ++e) {
+      const float y = act_fwd(p.act, x[e]);
+      a[e] = (p.act == ICAP_ACT_TANH) ? y : x[e];
+      x[e] = y;
+    }
+  }
+}
+// forward form, second half: x = x * dropmask (+ r)
+template <int W>
+__device__ __forceinline__ void epi_fwd_tail(float x[W], const float r[W], bool add_r, uint64_t seed, uint64_t didx,
+                                             uint32_t drop_thresh, float inv_keep) {
+#pragma clang fp contract(off)
+  if (drop_thresh != 0u) {
+#pragma unroll
+    for (int e = 0; e < W; ++e) x[e] = x[e] * drop_scale(seed, didx + e, drop_thresh, inv_keep);
+  }
+  if (add_r) {
+#pragma unroll
+    for (int e = 0; e < W; ++e) x[e] = x[e] + r[e];
+  }
+}
+
 // Epilogue of W consecutive columns [col, col+W) of row `row` (the order is the one include/icap.h documents).
 // x: alpha-unscaled fp32 accumulators; biasw: bias[col..col+W-1] (0 past N); fullw: all W columns in range;
 // W-wide vector access is used per operand where its leading dimension and base pointer are W-aligned.
@@ -165,7 +210,6 @@ __device__ __forceinline__ void epiw(const icap_gemm_args& p, int64_t row, int64
   TC* aux = reinterpret_cast<TC*>(p.aux);
   const TC* resid = reinterpret_cast<const TC*>(p.resid);
   const TC* dsrc = reinterpret_cast<const TC*>(p.dact_src);
-  const bool use_drop = drop_thresh != 0u;
   const uint64_t didx = p.offset + (uint64_t)(row * N + col);
   float a[W], r[W], c[W];
   // W-wide vector access needs the leading dimension AND the base pointer aligned to W elements (16 B suffices
@@ -177,38 +221,19 @@ __device__ __forceinline__ void epiw(const icap_gemm_args& p, int64_t row, int64
     if (pre) unpack_bf16(*pre, a);
     else if (fullw && vok(p.ld_dact, dsrc)) vecio<TC, W>::ld(dsrc + row * p.ld_dact + col, a);
     else for (int e = 0; e < W; ++e) a[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
-#pragma unroll
-    for (int e = 0; e < W; ++e) {
-      float y = p.alpha * x[e];
-      if (use_drop) y *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
-      x[e] = y * act_bwd(p.dact, a[e]);
-    }
+    epi_bwd_math<W>(p, x, a, seed, didx, drop_thresh, inv_keep);
   } else {
-#pragma unroll
-    for (int e = 0; e < W; ++e) x[e] = p.alpha * x[e] + biasw[e];
-    if (p.act != ICAP_ACT_NONE || aux) {
-#pragma unroll
-      for (int e = 0; e < W; ++e) {
-        const float y = act_fwd(p.act, x[e]);
-        a[e] = (p.act == ICAP_ACT_TANH) ? y : x[e];
-        x[e] = y;
-      }
-      if (aux) {
-        if (fullw && vok(p.ldaux, aux)) vecio<TC, W>::st(aux + row * p.ldaux + col, a);
-        else for (int e = 0; e < W; ++e) if (col + e < N) io<TC>::st(aux + row * p.ldaux + col + e, a[e]);
-      }
-    }
-    if (use_drop) {
-#pragma unroll
-      for (int e = 0; e < W; ++e) x[e] *= drop_scale(seed, didx + e, drop_thresh, inv_keep);
+    epi_fwd_act<W>(p, x, biasw, a);
+    if (aux) {
+      if (fullw && vok(p.ldaux, aux)) vecio<TC, W>::st(aux + row * p.ldaux + col, a);
+      else for (int e = 0; e < W; ++e) if (col + e < N) io<TC>::st(aux + row * p.ldaux + col + e, a[e]);
     }
     if (resid) {
       if (pre) unpack_bf16(*pre, r);
       else if (fullw && vok(p.ldr, resid)) vecio<TC, W>::ld(resid + row * p.ldr + col, r);
       else for (int e = 0; e < W; ++e) r[e] = (col + e < N) ? io<TC>::ld(resid + row * p.ldr + col + e) : 0.f;
-#pragma unroll
-      for (int e = 0; e < W; ++e) x[e] += r[e];
     }
+    epi_fwd_tail<W>(x, r, resid != nullptr, seed, didx, drop_thresh, inv_keep);
   }
   TC* cp = C + row * p.ldc + col;
   if (fullw) {
@@ -562,553 +587,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   }
 }
 
-// Double-buffered variant with the two stages in two distinct __shared__ objects and the K loop unrolled by two,
-// so each stage's buffer is a compile-time object: hipcc's LDS-DMA alias tracking then lets the fragment reads of
-// one buffer run while the DMA into the other is in flight (with one array it waits vmcnt(0) before every read
-// after a DMA issue). Fragment reads are issued in MFMA-group order (k half 0: rows of A in two halves, then
-// k half 1), so the LDS reads of the next group overlap the MFMAs of the current one.
-template <typename TI, typename TC, int MINB, int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm2b_kernel(icap_gemm_args p, int tiles_n, int splits,
-                                                                    int nk_split, uint32_t drop_thresh,
-                                                                    float inv_keep) {
-  constexpr int NW = WM * WN;
-  constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
-  constexpr int STB = (BM + BN) * GROWB;    // bytes per stage
-  constexpr int EPR = 16;                   // rows per LDS-staged epilogue pass
-  constexpr int ELD = 16 * TN + 4;          // fp32 row stride of the epilogue staging tile
-  static_assert(NW * EPR * ELD * 4 <= STB, "epilogue staging must fit one stage buffer");
-  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "each wave stages whole 8-row DMA pieces");
-  static_assert(TM % 2 == 0, "A fragments are read in two halves");
-  constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW);  // DMA instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) char smem0[STB];
-  __shared__ __attribute__((aligned(16))) char smem1[STB];
-  constexpr int ES = sizeof(TI);
-  constexpr int EPC = 16 / ES;
-  constexpr int BKE = GROWB / ES;
-  constexpr int HM = TM / 2;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WN, wn = wave - wm * WN;
-  const int bid = blockIdx.x, nwg = gridDim.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tiles = (int)(gridDim.x / splits);
-  const int split = wgid / tiles, tile = wgid - split * tiles;
-  // row tiles fastest when the row count is device-side: the live tiles (low rows) then spread over every XCD
-  const int tiles_m = tiles / tiles_n;
-  const int tm = p.m_dev ? tile % tiles_m : tile / tiles_n;
-  const int tn = p.m_dev ? tile / tiles_m : tile - tm * tiles_n;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int64_t M = p.M, N = p.N, K = p.K;
-  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;  // device row count
-  if (m0 >= Mv) return;
-  const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
-  const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
-  const int64_t mrows = Mv - m0 < BM ? Mv - m0 : BM;
-  const int64_t nrows = N - n0 < BN ? N - n0 : BN;
-  const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
-  const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
-  const int lrow = lane >> 3;
-  const int lchunk = ((lane & 7) ^ lrow) * EPC;
-  uint32_t a_off[APW], b_off[BPW];
-#pragma unroll
-  for (int i = 0; i < APW; ++i) a_off[i] = (uint32_t)(((wave * APW + i) * 8 + lrow) * p.lda + lchunk) * ES;
-#pragma unroll
-  for (int i = 0; i < BPW; ++i) b_off[i] = (uint32_t)(((wave * BPW + i) * 8 + lrow) * p.ldb + lchunk) * ES;
-  auto load_stage = [&](int64_t k0, char* As) {
-    const uint32_t kb = (uint32_t)(k0 * ES);
-    const bool kin = k0 + lchunk < K;
-    char* Bs = As + BM * GROWB;
-#pragma unroll
-    for (int i = 0; i < APW; ++i) dma16(ra_rsrc, As + (wave * APW + i) * 8 * GROWB, kin ? a_off[i] + kb : OOB);
-#pragma unroll
-    for (int i = 0; i < BPW; ++i) dma16(rb_rsrc, Bs + (wave * BPW + i) * 8 * GROWB, kin ? b_off[i] + kb : OOB);
-  };
-
-  f32x4_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  const int nk_all = (int)((K + BKE - 1) / BKE);
-  const int kt0 = split * nk_split;
-  const int nk = (nk_all - kt0 < nk_split ? nk_all - kt0 : nk_split);
-  const int64_t kbase = (int64_t)kt0 * BKE;
-  const int fr = lane & 15, fg = lane >> 4;
-  auto rdA = [&](const char* As, int i, int ks) {
-    return *reinterpret_cast<const uint4*>(As + lds_off(wm * 16 * TM + i * 16 + fr, ks * 4 + fg));
-  };
-  auto rdB = [&](const char* As, int j, int ks) {
-    return *reinterpret_cast<const uint4*>(As + BM * GROWB + lds_off(wn * 16 * TN + j * 16 + fr, ks * 4 + fg));
-  };
-  // one K stage from `cur` while the next one streams into `nxt`
-  auto step = [&](const char* cur, char* nxt, int kt) {
-    uint4 b[TN], a0[HM], a1[HM];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) b[j] = rdB(cur, j, 0);
-#pragma unroll
-    for (int i = 0; i < HM; ++i) a0[i] = rdA(cur, i, 0);
-    if (kt + 1 < nk) load_stage(kbase + (int64_t)(kt + 1) * BKE, nxt);
-#pragma unroll
-    for (int i = 0; i < HM; ++i) a1[i] = rdA(cur, HM + i, 0);
-#pragma unroll
-    for (int i = 0; i < HM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[i][j], a0[i], b[j]);
-#pragma unroll
-    for (int i = 0; i < HM; ++i) a0[i] = rdA(cur, i, 1);
-#pragma unroll
-    for (int i = 0; i < HM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[HM + i][j], a1[i], b[j]);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) b[j] = rdB(cur, j, 1);
-#pragma unroll
-    for (int i = 0; i < HM; ++i) a1[i] = rdA(cur, HM + i, 1);
-#pragma unroll
-    for (int i = 0; i < HM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[i][j], a0[i], b[j]);
-#pragma unroll
-    for (int i = 0; i < HM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[HM + i][j], a1[i], b[j]);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA into nxt has landed
-    __syncthreads();                                      // ... every wave's, and cur is free again
-  };
-
-  load_stage(kbase, smem0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; kt += 2) {
-    step(smem0, smem1, kt);
-    if (kt + 1 < nk) step(smem1, smem0, kt + 1);
-  }
-
-  uint64_t seed = 0;
-  if (splits == 1 && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
-  float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
-  float* cs = reinterpret_cast<float*>(smem0) + wave * (EPR * ELD);
-  constexpr int LPR = 4 * TN;
-  constexpr int RPI = 64 / LPR;
-  const int er = lane / LPR;
-  const int ec = (lane - er * LPR) * 4;
-  const int64_t col = n0 + wn * 16 * TN + ec;
-  const bool full4 = col + 4 <= N;
-  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
-  }
-#pragma unroll
-  for (int h = 0; h < 16 * TM / EPR; ++h) {
-#pragma unroll
-    for (int ii = 0; ii < EPR / 16; ++ii)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-          cs[(ii * 16 + fg * 4 + v) * ELD + j * 16 + fr] = acc[(EPR / 16) * h + ii][j][v];
-    __syncthreads();
-#pragma unroll 2
-    for (int t = 0; t < EPR / RPI; ++t) {
-      const int lr = t * RPI + er;
-      const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
-      float x[4];
-      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
-      if (row < Mv && col < N) {
-        if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
-        else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// Three-stage ring: stages k+1 and k+2 stream in (LDS-DMA) while stage k is consumed, so a load has two stage
-// computes to land (PMC: the two-stage kernels leave MFMA busy at ~44 %, parked on the DMA of the next stage).
-// Three distinct __shared__ buffers with the K loop unrolled by three keep every buffer a compile-time object
-// (no hipcc vmcnt(0) before the fragment reads); the stage hand-off is a counted vmcnt (the newest stage may stay
-// in flight) plus a raw s_barrier (a __syncthreads() would drain every DMA: cdna_hip_programming.md "Pipelining
-// across barriers").
-template <typename TI, typename TC, int MINB, int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm3b_kernel(icap_gemm_args p, int tiles_n, int splits,
-                                                                    int nk_split, uint32_t drop_thresh,
-                                                                    float inv_keep) {
-  constexpr int NW = WM * WN;
-  constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
-  constexpr int STB = (BM + BN) * GROWB;
-  constexpr int EPR = 16;
-  constexpr int ELD = 16 * TN + 4;
-  static_assert(NW * EPR * ELD * 4 <= STB, "epilogue staging must fit one stage buffer");
-  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "each wave stages whole 8-row DMA pieces");
-  constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW);
-  constexpr int DPS = APW + BPW;  // DMA instructions per wave per stage (the vmcnt unit)
-  __shared__ __attribute__((aligned(16))) char smem0[STB];
-  __shared__ __attribute__((aligned(16))) char smem1[STB];
-  __shared__ __attribute__((aligned(16))) char smem2[STB];
-  constexpr int ES = sizeof(TI);
-  constexpr int EPC = 16 / ES;
-  constexpr int BKE = GROWB / ES;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave - wm * WN;
-  const int bid = blockIdx.x, nwg = gridDim.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tiles = (int)(gridDim.x / splits);
-  const int split = wgid / tiles, tile = wgid - split * tiles;
-  // row tiles fastest when the row count is device-side: the live tiles (low rows) then spread over every XCD
-  const int tiles_m = tiles / tiles_n;
-  const int tm = p.m_dev ? tile % tiles_m : tile / tiles_n;
-  const int tn = p.m_dev ? tile / tiles_m : tile - tm * tiles_n;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int64_t M = p.M, N = p.N, K = p.K;
-  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;  // device row count
-  if (m0 >= Mv) return;
-  const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * ES;
-  const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * ES;
-  const int64_t mrows = Mv - m0 < BM ? Mv - m0 : BM;
-  const int64_t nrows = N - n0 < BN ? N - n0 : BN;
-  const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(Ab, (uint64_t)((mrows - 1) * p.lda + K) * ES);
-  const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * ES);
-  const int lrow = lane >> 3;
-  const int lchunk = ((lane & 7) ^ lrow) * EPC;
-  uint32_t a_off[APW], b_off[BPW];
-#pragma unroll
-  for (int i = 0; i < APW; ++i) a_off[i] = (uint32_t)(((wave * APW + i) * 8 + lrow) * p.lda + lchunk) * ES;
-#pragma unroll
-  for (int i = 0; i < BPW; ++i) b_off[i] = (uint32_t)(((wave * BPW + i) * 8 + lrow) * p.ldb + lchunk) * ES;
-  const int nk_all = (int)((K + BKE - 1) / BKE);
-  const int kt0 = split * nk_split;
-  const int nk = (nk_all - kt0 < nk_split ? nk_all - kt0 : nk_split);
-  const int64_t kbase = (int64_t)kt0 * BKE;
-  // stage kt -> buffer; stages past nk issue nothing
-  auto load_stage = [&](int kt, char* As) {
-    if (kt >= nk) return;
-    const int64_t k0 = kbase + (int64_t)kt * BKE;
-    const uint32_t kb = (uint32_t)(k0 * ES);
-    const bool kin = k0 + lchunk < K;
-    char* Bs = As + BM * GROWB;
-#pragma unroll
-    for (int i = 0; i < APW; ++i) dma16(ra_rsrc, As + (wave * APW + i) * 8 * GROWB, kin ? a_off[i] + kb : OOB);
-#pragma unroll
-    for (int i = 0; i < BPW; ++i) dma16(rb_rsrc, Bs + (wave * BPW + i) * 8 * GROWB, kin ? b_off[i] + kb : OOB);
-  };
-
-  f32x4_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  const int fr = lane & 15, fg = lane >> 4;
-  auto step = [&](const char* cur, char* nxt2, int kt) {
-    uint4 af[2][TM], bfr[2][TN];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[ks][i] = *reinterpret_cast<const uint4*>(cur + lds_off(wm * 16 * TM + i * 16 + fr, ks * 4 + fg));
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[ks][j] =
-            *reinterpret_cast<const uint4*>(cur + BM * GROWB + lds_off(wn * 16 * TN + j * 16 + fr, ks * 4 + fg));
-    }
-    load_stage(kt + 2, nxt2);  // into the buffer every wave finished reading one barrier ago
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[i][j], af[ks][i], bfr[ks][j]);
-    __builtin_amdgcn_sched_barrier(0);
-    // stage kt+1 must have landed; stage kt+2 (issued above) may stay in flight
-    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  load_stage(0, smem0);
-  load_stage(1, smem1);
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPS) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; kt += 3) {
-    step(smem0, smem2, kt);
-    if (kt + 1 >= nk) break;
-    step(smem1, smem0, kt + 1);
-    if (kt + 2 >= nk) break;
-    step(smem2, smem1, kt + 2);
-  }
-
-  uint64_t seed = 0;
-  if (splits == 1 && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
-  float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
-  float* cs = reinterpret_cast<float*>(smem0) + wave * (EPR * ELD);
-  constexpr int LPR = 4 * TN;
-  constexpr int RPI = 64 / LPR;
-  const int er = lane / LPR;
-  const int ec = (lane - er * LPR) * 4;
-  const int64_t col = n0 + wn * 16 * TN + ec;
-  const bool full4 = col + 4 <= N;
-  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
-  }
-#pragma unroll
-  for (int h = 0; h < 16 * TM / EPR; ++h) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) cs[(fg * 4 + v) * ELD + j * 16 + fr] = acc[h][j][v];
-    __syncthreads();
-#pragma unroll 2
-    for (int t = 0; t < EPR / RPI; ++t) {
-      const int lr = t * RPI + er;
-      const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
-      float x[4];
-      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
-      if (row < Mv && col < N) {
-        if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
-        else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14) for the
-// builtin form, which hipcc's wait-count tracking sees (inline asm is opaque to it, so it adds its own vmcnt(0)
-// before the next read of a stage it believes still has DMA pending)
-constexpr int wait_vm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
-
-// Phase-interleaved 8-wave GEMM (bf16 in, fp32 accumulate) for the large products of the step: 256-row tiles,
-// BN = 256 or 128 columns, 8 waves as 2 (M) x 4 (N), each wave a (128) x (BN/4) accumulator block (two waves per
-// SIMD, so one wave's LDS reads and waits overlap the other's MFMAs). Per-wave LDS reads per MFMA are 25-40 %
-// below the 128x128/4-wave kernels (the operand fragments of a 128-row wave block are reused over BN/4 columns).
-//
-// K advances 64 at a time through two LDS stages E (even k-tiles) and O (odd), each one compile-time
-// __shared__ object so hipcc's LDS-DMA alias tracking never drains the DMA queue before a fragment read. One
-// k-tile is four phases, one quadrant (64 rows x BN/8 columns, 16 MFMAs at BN=256) each:
-//   ph1: read A rows 0-63 + B cols 0..   -> Q00      ph2: read B cols BN/8.. -> Q01
-//   ph3: read A rows 64-127; DMA the B halves of k-tile t+2 into this stage (last read in ph2) -> Q11
-//   ph4: DMA the A halves of k-tile t+2 (last read in ph3); counted vmcnt: k-tile t+1 has landed -> Q10
-// Every phase: reads, [DMA], s_barrier, lgkmcnt(0), setprio(1) MFMAs setprio(0), s_barrier. The counted vmcnt
-// leaves k-tile t+2's DMA in flight across four phases (cdna_hip_programming.md §5 "The 256² 8-phase
-// template", "Pipelining across barriers"; raw s_barrier so no vmcnt(0) is emitted). Reads of a stage follow
-// the wait + barrier that retire its DMA; a stage is re-filled one phase after its last read retired (lgkmcnt(0)
-// before the MFMAs, barrier after them).
-template <typename TC, int BN>
-__global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int tiles_n, int splits, int nk_split,
-                                                      uint32_t drop_thresh, float inv_keep) {
-  constexpr int BM = 256, WN = 4;
-  constexpr int TM = BM / 32, TN = BN / (16 * WN);  // per-wave 16x16 tiles: 8 x (4 | 2)
-  constexpr int QM = TM / 2, QN = TN / 2;           // per-phase quadrant tiles
-  constexpr int STA = BM * GROWB;                   // A bytes per stage
-  constexpr int ST = (BM + BN) * GROWB;             // bytes per stage
-  constexpr int GA = BM / 128, GB = BN / 128;       // DMA instructions per thread per A / B half
-  constexpr int GT = 2 * (GA + GB);                 // per k-tile (the vmcnt unit)
-  constexpr int EPR = 16, ELD = 16 * TN + 4;
-  static_assert(8 * EPR * ELD * 4 <= ST, "epilogue staging must fit one stage");
-  __shared__ __attribute__((aligned(16))) char smE[ST];
-  __shared__ __attribute__((aligned(16))) char smO[ST];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int bid = blockIdx.x, nwg = gridDim.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tiles = (int)(gridDim.x / splits);
-  const int split = wgid / tiles, tile = wgid - split * tiles;
-  const int tiles_m = tiles / tiles_n;
-  const int tm = p.m_dev ? tile % tiles_m : tile / tiles_n;
-  const int tn = p.m_dev ? tile / tiles_m : tile - tm * tiles_n;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int64_t M = p.M, N = p.N, K = p.K;
-  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;
-  if (m0 >= Mv) return;
-  const char* Ab = reinterpret_cast<const char*>(p.A) + m0 * p.lda * 2;
-  const char* Bb = reinterpret_cast<const char*>(p.B) + n0 * p.ldb * 2;
-  const int64_t mrows = Mv - m0 < BM ? Mv - m0 : BM;
-  const int64_t nrows = N - n0 < BN ? N - n0 : BN;
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc_u(Ab, (uint64_t)((mrows - 1) * p.lda + K) * 2);
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc_u(Bb, (uint64_t)((nrows - 1) * p.ldb + K) * 2);
-  // lane l of a DMA wave-instruction fills row l>>3, physical 16-byte chunk l&7 of an 8-row piece; the source
-  // chunk is XOR-swizzled by the row (the fragment reads apply the same involution: lds_off)
-  const int lrow = lane >> 3;
-  const int lchunk = ((lane & 7) ^ lrow) * 8;
-  // per-lane part of the source offset in one VGPR per operand; the row piece and k offsets are wave-uniform
-  const uint32_t va = (uint32_t)((lrow * p.lda + lchunk) * 2), vb = (uint32_t)((lrow * p.ldb + lchunk) * 2);
-  const uint32_t lda8 = (uint32_t)(p.lda * 16), ldb8 = (uint32_t)(p.ldb * 16);  // bytes per 8 rows
-  const int nk_all = (int)((K + 63) / 64);
-  const int kt0 = split * nk_split;
-  const int nk = (nk_all - kt0 < nk_split ? nk_all - kt0 : nk_split);
-  const int64_t kbase = (int64_t)kt0 * 64;
-  auto dmaA = [&](char* st, int t, int h) {
-    const int64_t k0 = kbase + (int64_t)t * 64;
-    const uint32_t v = k0 + lchunk < K ? va : OOB;
-#pragma unroll
-    for (int i = 0; i < GA; ++i) {
-      const int pc = h * (BM / 16) + i * 8 + wave;  // 8-row piece of the stage's A image
-      dma16s(ra, st + pc * 8 * GROWB, v, __builtin_amdgcn_readfirstlane((uint32_t)pc * lda8 + (uint32_t)(k0 * 2)));
-    }
-  };
-  auto dmaB = [&](char* st, int t, int h) {
-    const int64_t k0 = kbase + (int64_t)t * 64;
-    const uint32_t v = k0 + lchunk < K ? vb : OOB;
-#pragma unroll
-    for (int i = 0; i < GB; ++i) {
-      const int pc = h * (BN / 16) + i * 8 + wave;
-      dma16s(rb, st + STA + pc * 8 * GROWB, v, __builtin_amdgcn_readfirstlane((uint32_t)pc * ldb8 + (uint32_t)(k0 * 2)));
-    }
-  };
-
-  f32x4_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  const int fr = lane & 15, fg = lane >> 4;
-  // Fragment reads are inline-asm ds_read_b128: hipcc then sees no LDS read it could order against the LDS-DMA
-  // (it otherwise drains the DMA queue with vmcnt(0) at the loop head), and the waits are ours: lgkmcnt(0) +
-  // sched_barrier before the MFMAs that consume a phase's reads (cdna_hip_programming.md §5.4 rule 18).
-  const uint32_t baseE = (uint32_t)reinterpret_cast<uintptr_t>(smE);
-  const uint32_t baseO = (uint32_t)reinterpret_cast<uintptr_t>(smO);
-  uint32_t la[2], lb[2];  // per-lane byte offsets of the k-half ks fragment within a stage
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const uint32_t sw = (uint32_t)(((ks * 4 + fg) ^ (fr & 7)) << 4);
-    la[ks] = (uint32_t)((wm * (BM / 2) + fr) * GROWB) + sw;
-    lb[ks] = (uint32_t)(STA + (wn * (BN / 4) + fr) * GROWB) + sw;
-  }
-  // fragment registers: A rows 0-63 (fa0) / 64-127 (fa1) of the wave block; B column halves in fb[0], fb[1]
-  // (which half each holds alternates per k-tile: B-sub0 of k-tile t sits in fb[t & 1])
-  uint4 fa0[2][QM], fa1[2][QM], fb[2][2][QN];
-  auto rdA = [&](uint32_t st, auto qi_c, uint4 (&f)[2][QM]) {
-    constexpr int qi = decltype(qi_c)::value;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const uint32_t a = st + la[ks];
-#pragma unroll
-      for (int i = 0; i < QM; ++i)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][i]) : "v"(a), "i"((qi * (BM / 4) + i * 16) * GROWB));
-    }
-  };
-  auto rdB = [&](uint32_t st, auto qj_c, uint4 (&f)[2][QN]) {
-    constexpr int qj = decltype(qj_c)::value;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const uint32_t a = st + lb[ks];
-#pragma unroll
-      for (int j = 0; j < QN; ++j)
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[ks][j]) : "v"(a), "i"((qj * (BN / 8) + j * 16) * GROWB));
-    }
-  };
-  using C0 = std::integral_constant<int, 0>;
-  using C1 = std::integral_constant<int, 1>;
-  auto reads_done = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  auto mm = [&](int qi, int qj, const uint4 (&a)[2][QM], const uint4 (&b)[2][QN]) {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < QM; ++i)
-#pragma unroll
-        for (int j = 0; j < QN; ++j) mfma_chunk<bf16_t>(acc[qi * QM + i][qj * QN + j], a[ks][i], b[ks][j]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  // k-tile t from stage X (parity P = t & 1), stage Y holds k-tile t+1. Fragment reads run one phase ahead of the
-  // MFMAs that consume them, so LDS latency hides under the previous quadrant; one barrier per k-tile.
-  auto ktile = [&](char* X, uint32_t bx, uint32_t by, int t, uint4 (&bs0)[2][QN], uint4 (&bs1)[2][QN]) {
-    const bool next = t + 1 < nk;
-    reads_done();              // fa0 / bs0 (read during the previous k-tile) are in registers
-    rdB(bx, C1{}, bs1);        // B cols BN/8.. of k-tile t
-    mm(0, 0, fa0, bs0);
-    reads_done();
-    rdA(bx, C1{}, fa1);        // A rows 64-127 of k-tile t
-    mm(0, 1, fa0, bs1);
-    // every read of X for k-tile t has retired and k-tile t+1 has landed in Y, on every wave
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (next) rdA(by, C0{}, fa0);  // A rows 0-63 of k-tile t+1
-    if (t + 2 < nk) { dmaB(X, t + 2, 0); dmaB(X, t + 2, 1); dmaA(X, t + 2, 0); dmaA(X, t + 2, 1); }
-    mm(1, 1, fa1, bs1);
-    reads_done();
-    if (next) rdB(by, C0{}, bs1);  // B cols 0.. of k-tile t+1 (bs1 is free after Q11)
-    mm(1, 0, fa1, bs0);
-  };
-
-  dmaA(smE, 0, 0); dmaA(smE, 0, 1); dmaB(smE, 0, 0); dmaB(smE, 0, 1);
-  if (nk > 1) {
-    dmaA(smO, 1, 0); dmaA(smO, 1, 1); dmaB(smO, 1, 0); dmaB(smO, 1, 1);
-    __builtin_amdgcn_s_waitcnt(wait_vm(GT));
-  } else {
-    __builtin_amdgcn_s_waitcnt(wait_vm(0));
-  }
-  __builtin_amdgcn_s_barrier();
-  rdA(baseE, C0{}, fa0);
-  rdB(baseE, C0{}, fb[0]);
-  for (int t = 0; t < nk; t += 2) {
-    ktile(smE, baseE, baseO, t, fb[0], fb[1]);
-    if (t + 1 < nk) ktile(smO, baseO, baseE, t + 1, fb[1], fb[0]);
-  }
-  reads_done();
-  __syncthreads();  // the epilogue stages through smE
-
-  uint64_t seed = 0;
-  if (splits == 1 && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
-  float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
-  float* cs = reinterpret_cast<float*>(smE) + wave * (EPR * ELD);
-  constexpr int LPR = 4 * TN;
-  constexpr int RPI = 64 / LPR;
-  const int er = lane / LPR;
-  const int ec = (lane - er * LPR) * 4;
-  const int64_t col = n0 + wn * 16 * TN + ec;
-  const bool full4 = col + 4 <= N;
-  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
-  }
-#pragma unroll
-  for (int h = 0; h < TM; ++h) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) cs[(fg * 4 + v) * ELD + j * 16 + fr] = acc[h][j][v];
-    __syncthreads();
-#pragma unroll 2
-    for (int t = 0; t < EPR / RPI; ++t) {
-      const int lr = t * RPI + er;
-      const int64_t row = m0 + wm * (BM / 2) + h * EPR + lr;
-      float x[4];
-      *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec);
-      if (row < Mv && col < N) {
-        if (slab) *reinterpret_cast<float4*>(slab + row * N + col) = *reinterpret_cast<const float4*>(x);
-        else epi4<TC>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // Skinny-M GEMM (M <= 128: greedy-decode steps over the batch, CLIP projection, mapper input Linear).
 // A weight-streaming, latency-bound problem: block = 8 waves over a 16*NT-column slab of B (= W rows) and a
 // 16*MT-row slab of A (grid.y walks M, so no block streams all of A through its CU: per-CU L2 bandwidth, not
@@ -1330,40 +808,390 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(icap_gemm_args p, int 
   epi4<TC>(p, row, col, x, bias4, true, seed, drop_thresh, inv_keep);
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Persistent ring GEMM (bf16 in, bf16 out, fp32 accumulate) for the mid-sized products of the train step
+// (M = 3200 ... 8320 tokens, N = 768 ... 3072, K = 768 ... 3072: GPT-2 / CLIP / mapper projections and their dX).
+//
+// Why: the 128 x 128 tile kernels above keep ONE 32 KiB stage in flight per block; at 2-3 blocks/CU that is
+// ~64-96 KiB in flight per CU against ~1 us of loaded L2/MALL latency, so they stage at ~50 GB/s per CU and run
+// at ~0.23 of the bf16 peak (profiles/r01_*). Here one workgroup per CU owns the whole LDS:
+//   - tile BM x 128 (BM = 64 WM; WM = 4: 256 x 128, 8 waves as 4 (M) x 2 (N), each wave 64 x 64 = 4 x 4 MFMA
+//     16x16x32 tiles), K advancing 64 per step (128-byte LDS rows, XOR-swizzled 16-byte chunks as lds_off);
+//   - an NSLOT-deep ring of LDS stages filled by LDS-DMA (buffer_load ... lds) with AHEAD = NSLOT - 1 steps in
+//     flight while a step is computed: counted `s_waitcnt vmcnt(N)` + raw s_barrier, never vmcnt(0) in steady
+//     state (cdna_hip_programming.md §5 "Pipelining across barriers");
+//   - persistent: the grid is one block per CU and each block walks its output tiles (units u = wg, wg + G, ...)
+//     as ONE continuous stream of k-steps, so the DMA of the next tile's first stages is already in flight while
+//     the current tile's epilogue runs (short-K products no longer pay a pipeline fill per tile);
+//   - fragment reads, the epilogue's operand prefetch and its LDS staging are inline asm, so hipcc never drains
+//     the DMA queue in front of them (it would wait vmcnt(0) before any LDS read following an LDS-DMA issue);
+//     the epilogue stores are range-checked buffer stores (exact instruction count, no branches).
+// Block -> tile placement is XCD-aware (consecutive units on one XCD share A row panels / B column panels in L2).
+// Constraints (checked by the host plan): bf16 A/B/C, K % 8 == 0, N % 8 == 0, every epilogue operand and its
+// leading dimension 16-byte aligned, beta == 0, one K split.
+namespace ring {
+constexpr int BN = 128;
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+
+// wave-uniform buffer descriptor as 4 SGPRs for inline asm (same fields as make_rsrc: stride 0, raw buffer)
+__device__ __forceinline__ v4i_t rsrc4(const void* base, uint64_t bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint32_t n = bytes > 0x7fffffffull ? 0x7fffffffu : (uint32_t)bytes;
+  v4i_t r;
+  r.x = (int)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  r.y = (int)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xffffu);
+  r.z = (int)__builtin_amdgcn_readfirstlane(n);
+  r.w = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t as_rsrc(v4i_t r) {
+  return __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(((uint64_t)(uint32_t)r.y << 32) | (uint32_t)r.x), (short)0, r.z, r.w);
+}
+
+// one fp32 to LDS (asm: invisible to hipcc's LDS-DMA alias tracking). FIRST: the value may come straight from an
+// MFMA accumulator, which an asm reader must not touch for 12 wait states (cdna_hip_programming.md §5.7 item 2)
+template <int OFF, bool FIRST>
+__device__ __forceinline__ void ds_w32(uint32_t a, float x) {
+  if constexpr (FIRST) asm volatile("s_nop 7\n\ts_nop 7\n\tds_write_b32 %0, %1 offset:%2" ::"v"(a), "v"(x), "i"(OFF));
+  else asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(a), "v"(x), "i"(OFF));
+}
+
+#define ICAP_RING_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+}  // namespace ring
+
+// ICAP_RING_ABL (diagnostic builds only, tools/ring_ablation.sh): 1 = no MFMA, 2 = no LDS-DMA, 3 = no fragment reads
+#ifndef ICAP_RING_ABL
+#define ICAP_RING_ABL 0
+#endif
+template <int WM, int NSLOT>
+__global__ __launch_bounds__(128 * WM, 1) void gemm_ring_kernel(icap_gemm_args p, int tiles_m, int tiles_n, int nunits,
+                                                                 uint32_t drop_thresh, float inv_keep) {
+  using namespace ring;
+  constexpr int NW = 2 * WM;                // waves
+  constexpr int BM = 64 * WM;
+  constexpr int SLOT = (BM + BN) * GROWB;   // bytes per ring slot (one 64-deep k-step of A and B)
+  constexpr int APW = BM / 8 / NW;          // 8-row DMA pieces per wave per step: A
+  constexpr int BPW = BN / 8 / NW;          //                                     B
+  constexpr int D = APW + BPW;              // DMA instructions per wave per step (the vmcnt unit)
+  constexpr int ELD = 68;                   // fp32 row stride of the epilogue staging tile (bank-conflict-free writes)
+  static_assert(NW * 16 * ELD * 4 <= SLOT, "epilogue staging must fit one ring slot");
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT + 2 * NW * 1024];  // ring + bias (2 units)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int64_t M = p.M, N = p.N, K = p.K;
+  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;
+  const int nk = (int)((K + 63) / 64);
+  const bf16_t* Ag = reinterpret_cast<const bf16_t*>(p.A);
+  const bf16_t* Bg = reinterpret_cast<const bf16_t*>(p.B);
+
+  auto unit_tm = [&](int u) { return p.m_dev ? u % tiles_m : u / tiles_n; };
+  auto unit_tn = [&](int u) { return p.m_dev ? u / tiles_m : u % tiles_n; };
+  auto next_valid = [&](int u) {
+    while (u < nunits && (int64_t)unit_tm(u) * BM >= Mv) u += G;
+    return u;
+  };
+
+  // ---- producer: LDS-DMA of k-step (pu, pk) into ring slot pslot (and, with a unit's first step, its bias) ------
+  const int lrow = lane >> 3;
+  const int lchunk = ((lane & 7) ^ lrow) * 8;  // logical K offset (elements) of this lane's 16 bytes
+  const uint32_t va0 = (uint32_t)((lrow * p.lda + lchunk) * 2), vb0 = (uint32_t)((lrow * p.ldb + lchunk) * 2);
+  const uint32_t lda8 = (uint32_t)(p.lda * 16), ldb8 = (uint32_t)(p.ldb * 16);  // bytes per 8 rows
+  const bool has_bias = p.bias && p.dact == ICAP_ACT_NONE;
+  int pu = next_valid(wg), pk = 0, pslot = 0, prod = 0, pbias = 0;
+  int64_t pn0 = 0;  // first column of the producer's unit
+  __amdgpu_buffer_rsrc_t pra = make_rsrc_u(Ag, 16), prb = make_rsrc_u(Bg, 16);
+  auto set_prod = [&]() {
+    if (pu < nunits) {
+      const int64_t m0 = (int64_t)unit_tm(pu) * BM, n0 = (int64_t)unit_tn(pu) * BN;
+      pn0 = n0;
+      const int64_t mr = Mv - m0 < BM ? Mv - m0 : BM, nr = N - n0 < BN ? N - n0 : BN;
+      pra = make_rsrc_u(Ag + m0 * p.lda, (uint64_t)((mr - 1) * p.lda + K) * 2);
+      prb = make_rsrc_u(Bg + n0 * p.ldb, (uint64_t)((nr - 1) * p.ldb + K) * 2);
+    }
+  };
+  set_prod();
+  // block-uniform: every wave issues the same DMA count (D, + 1 with a unit's first step when there is a bias), or
+  // none once the stream has ended
+  auto produce = [&]() {
+    if (pu >= nunits) return;
+    const int64_t k0 = (int64_t)pk * 64;
+    const bool kin = k0 + lchunk < K;  // K % 8 == 0: a 16-byte chunk is wholly inside or outside
+    const uint32_t va = kin ? va0 : OOB, vb = kin ? vb0 : OOB;
+    char* st = smem + pslot * SLOT;
+    if (pk == 0 && has_bias) {  // this unit's 128 bias values -> the wave's area of bias buffer (unit parity)
+      const __amdgpu_buffer_rsrc_t brs = make_rsrc_u(p.bias, (uint64_t)N * 4);
+      dma16(brs, smem + NSLOT * SLOT + (pbias * NW + wave) * 1024,
+            lane < 16 ? (uint32_t)((pn0 + wn * 64) * 4 + 16 * lane) : OOB);
+    }
+    if (ICAP_RING_ABL != 2) {
+#pragma unroll
+      for (int i = 0; i < APW; ++i) {
+        const int pc = wave * APW + i;
+        dma16s(pra, st + pc * 8 * GROWB, va, __builtin_amdgcn_readfirstlane((uint32_t)pc * lda8 + (uint32_t)(k0 * 2)));
+      }
+#pragma unroll
+      for (int j = 0; j < BPW; ++j) {
+        const int pc = wave * BPW + j;
+        dma16s(prb, st + BM * GROWB + pc * 8 * GROWB, vb,
+               __builtin_amdgcn_readfirstlane((uint32_t)pc * ldb8 + (uint32_t)(k0 * 2)));
+      }
+    }
+    ++prod;
+    pslot = pslot + 1 == NSLOT ? 0 : pslot + 1;
+    if (++pk == nk) {
+      pk = 0;
+      pbias ^= 1;
+      pu = next_valid(pu + G);
+      set_prod();
+    }
+  };
+
+  // ---- consumer fragment addressing (lds_off of rows wm*64 + i*16 + fr / BM + wn*64 + j*16 + fr) ----------------
+  const int fr = lane & 15, fg = lane >> 4;
+  const uint32_t smem_base = (uint32_t)reinterpret_cast<uintptr_t>(smem);
+  uint32_t la[2], lb[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const uint32_t sw = (uint32_t)(((ks * 4 + fg) ^ (fr & 7)) << 4);
+    la[ks] = (uint32_t)((wm * 64 + fr) * GROWB) + sw;
+    lb[ks] = (uint32_t)((BM + wn * 64 + fr) * GROWB) + sw;
+  }
+
+  // ---- epilogue geometry: lane -> 8 consecutive columns of one row, 8 rows per wave instruction ----------------
+  const int er = lane >> 3, ec = (lane & 7) * 8;
+  const bool use_dact = p.dact != ICAP_ACT_NONE;
+  const bf16_t* esrc = use_dact ? reinterpret_cast<const bf16_t*>(p.dact_src) : reinterpret_cast<const bf16_t*>(p.resid);
+  const int64_t eld = use_dact ? p.ld_dact : p.ldr;
+  const bool has_pre = esrc != nullptr;
+  const uint64_t seed = drop_thresh != 0u ? eff_seed(p.seed, p.seed_ptr) : 0ull;
+
+  // ---- main loop ------------------------------------------------------------------------------------------------
+  // A k-step g is two phases, one per 32-deep half (ks) of its 64-deep slot; fragment registers R0 (ks 0) and R1
+  // (ks 1), 8 ds_read_b128 each (A rows, B columns):
+  //   X(g): read R1 <- slot g ks 1;               16 MFMAs on R0 (read during Y(g-1))
+  //   Y(g): R1 reads retired (this wave is done with slot g); wait until step g+1 landed (counted vmcnt: the
+  //         AHEAD-1 younger steps stay in flight); s_barrier (every wave's DMA of g+1 landed, every wave done with
+  //         slot g); DMA step g+NSLOT into slot g; read R0 <- slot g+1 ks 0; 16 MFMAs on R1.
+  // So the LDS reads of one half overlap the MFMAs of the other and the DMA issue sits among MFMAs, with NSLOT - 1
+  // steps in flight. At a unit's last step the DMA of Y(g) is deferred past the epilogue, which stages the
+  // accumulators through slot g (free then); R0 then already holds the next unit's first half.
+  u32x4_t R0[8], R1[8];
+  auto read_half = [&](u32x4_t (&R)[8], int slot, int ks) __attribute__((always_inline)) {
+    if (ICAP_RING_ABL == 3) return;
+    const uint32_t a = smem_base + (uint32_t)(slot * SLOT) + la[ks], b = smem_base + (uint32_t)(slot * SLOT) + lb[ks];
+    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(R[0]) : "v"(a));
+    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(R[1]) : "v"(a));
+    asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(R[2]) : "v"(a));
+    asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(R[3]) : "v"(a));
+    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(R[4]) : "v"(b));
+    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(R[5]) : "v"(b));
+    asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(R[6]) : "v"(b));
+    asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(R[7]) : "v"(b));
+  };
+#define ICAP_RING_LGKM(n, R)                                                                                   \
+  asm volatile("s_waitcnt lgkmcnt(" #n ")"                                                                     \
+               : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7])); \
+  __builtin_amdgcn_sched_barrier(0)
+  // wait until step `s` landed in this wave: the steps produced after it may stay in flight
+  auto wait_step = [&](int s) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    const int younger = prod - 1 - s;
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * D) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(D) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int s = 0; s < NSLOT; ++s) produce();  // prologue: NSLOT steps in flight
+  int g = 0, cslot = 0, cbias = 0;
+  wait_step(0);
+  __builtin_amdgcn_s_barrier();
+  read_half(R0, 0, 0);
+
+  for (int cu = next_valid(wg); cu < nunits; cu = next_valid(cu + G)) {
+    const int64_t m0 = (int64_t)unit_tm(cu) * BM, n0 = (int64_t)unit_tn(cu) * BN;
+    f32x4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    auto mma_half = [&](u32x4_t (&R)[8], int from, int to) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = from; q < to; ++q) {
+        if (ICAP_RING_ABL == 1) asm volatile("" ::"v"(R[q >> 2]), "v"(R[4 + (q & 3)]));
+        else mfma_chunk<bf16_t>(acc[q >> 2][q & 3], __builtin_bit_cast(uint4, R[q >> 2]), __builtin_bit_cast(uint4, R[4 + (q & 3)]));
+      }
+    };
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool last = kt + 1 == nk;
+      const int nslot = cslot + 1 == NSLOT ? 0 : cslot + 1;
+      // X(g)
+      read_half(R1, cslot, 1);
+      ICAP_RING_LGKM(8, R0);
+      mma_half(R0, 0, 16);
+      // Y(g)
+      __builtin_amdgcn_sched_barrier(0);
+      ICAP_RING_LGKM(0, R1);
+      if (prod > g + 1) wait_step(g + 1);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      read_half(R0, nslot, 0);
+      mma_half(R1, 0, 8);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!last) produce();
+      __builtin_amdgcn_sched_barrier(0);
+      mma_half(R1, 8, 16);
+      cslot = nslot;
+      ++g;
+    }
+
+    // ---- epilogue of unit cu, staged through the slot of its last step --------------------------------------------
+    const int eslot = cslot == 0 ? NSLOT - 1 : cslot - 1;
+    const int64_t col_l = wn * 64 + ec;  // tile-relative column of this lane's 8
+    const int64_t mr = Mv - m0 < BM ? Mv - m0 : BM, nr = N - n0 < BN ? N - n0 : BN;
+    const bool cin = n0 + col_l < N;
+    // residual / activation-gradient operand of this lane's rows: plain buffer loads (hipcc waits for them at first
+    // use; no DMA is issued after them before that), overlapped with the first pass's LDS staging
+    uint4 pre[8];
+    {
+      const __amdgpu_buffer_rsrc_t ers =
+          has_pre ? make_rsrc_u(esrc + m0 * eld + n0, (uint64_t)((mr - 1) * eld + nr) * 2) : make_rsrc_u(Ag, 0);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int64_t rl = wm * 64 + (t >> 1) * 16 + (t & 1) * 8 + er;
+        pre[t] = has_pre ? bload(ers, cin ? (uint32_t)((rl * eld + col_l) * 2) : OOB) : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    const uint32_t wst = smem_base + (uint32_t)(eslot * SLOT + wave * 16 * ELD * 4);
+    float bias8[8];
+    {
+      u32x4_t b0 = (u32x4_t){0u, 0u, 0u, 0u}, b1 = b0;
+      if (has_bias) {  // this unit's bias landed with its first step (older than every step waited for since)
+        const uint32_t ba = smem_base + (uint32_t)(NSLOT * SLOT + (cbias * NW + wave) * 1024 + (lane & 7) * 32);
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(b0), "=&v"(b1) : "v"(ba));
+      }
+      const uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bias8[e] = __uint_as_float(w[e]);
+    }
+    cbias ^= 1;
+    const __amdgpu_buffer_rsrc_t crs = make_rsrc_u(reinterpret_cast<bf16_t*>(p.C) + m0 * p.ldc + n0,
+                                                  (uint64_t)((mr - 1) * p.ldc + nr) * 2);
+    __amdgpu_buffer_rsrc_t ars = crs;
+    if (p.aux)
+      ars = make_rsrc_u(reinterpret_cast<bf16_t*>(p.aux) + m0 * p.ldaux + n0, (uint64_t)((mr - 1) * p.ldaux + nr) * 2);
+    // per 16-row pass: raw accumulators -> LDS (per-wave region, fp32 [16][68]) -> 8 columns per lane
+    auto pass = [&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      const uint32_t wa = wst + (uint32_t)(((fg * 4) * ELD + fr) * 4);
+      static_for<0, 4>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        static_for<0, 4>([&](auto vc) {
+          constexpr int v = decltype(vc)::value;
+          constexpr int off = (v * ELD + j * 16) * 4;
+          const float x = acc[i][j][v];
+          ds_w32<off, i == 0 && j == 0 && v == 0>(wa, x);
+        });
+      });
+      const uint32_t ra = wst + (uint32_t)((er * ELD + ec) * 4);
+      u32x4_t r[2][2];
+      asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(r[0][0]) : "v"(ra));
+      asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(r[0][1]) : "v"(ra));
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[1][0]) : "v"(ra), "i"(8 * ELD * 4));
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[1][1]) : "v"(ra), "i"(8 * ELD * 4 + 16));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(r[1][0]), "+v"(r[1][1]));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int64_t rl = wm * 64 + i * 16 + t * 8 + er;  // tile-relative row
+        const int64_t row = m0 + rl;
+        float x[8] = {__uint_as_float(r[t][0].x), __uint_as_float(r[t][0].y), __uint_as_float(r[t][0].z),
+                      __uint_as_float(r[t][0].w), __uint_as_float(r[t][1].x), __uint_as_float(r[t][1].y),
+                      __uint_as_float(r[t][1].z), __uint_as_float(r[t][1].w)};
+        float a[8];
+        const bool keep_row = row < Mv;
+        const uint64_t didx = p.offset + (uint64_t)(row * N + n0 + col_l);
+        if (use_dact) {
+          unpack_bf16(pre[i * 2 + t], a);
+          epi_bwd_math<8>(p, x, a, seed, didx, drop_thresh, inv_keep);
+        } else {
+          epi_fwd_act<8>(p, x, bias8, a);
+          if (p.aux) {
+            const uint4 av = make_uint4(f2bf2(a[0], a[1]), f2bf2(a[2], a[3]), f2bf2(a[4], a[5]), f2bf2(a[6], a[7]));
+            const uint32_t aoff = (cin && keep_row) ? (uint32_t)((rl * p.ldaux + col_l) * 2) : OOB;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, av), ars, aoff, 0, 0);
+          }
+          float rr[8];
+          unpack_bf16(pre[i * 2 + t], rr);
+          epi_fwd_tail<8>(x, rr, has_pre, seed, didx, drop_thresh, inv_keep);
+        }
+        const uint4 cv = make_uint4(f2bf2(x[0], x[1]), f2bf2(x[2], x[3]), f2bf2(x[4], x[5]), f2bf2(x[6], x[7]));
+        const uint32_t coff = (cin && keep_row) ? (uint32_t)((rl * p.ldc + col_l) * 2) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, cv), crs, coff, 0, 0);
+      }
+    };
+    pass(std::integral_constant<int, 0>{});
+    pass(std::integral_constant<int, 1>{});
+    pass(std::integral_constant<int, 2>{});
+    pass(std::integral_constant<int, 3>{});
+    // every wave is done with the staging slot before the deferred DMA of the last step's Y phase refills it
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    produce();
+  }
+#undef ICAP_RING_LGKM
+  __builtin_amdgcn_sched_barrier(0);
+  ICAP_RING_VMCNT(0);  // nothing of ours in flight when the wave ends
+}
+#undef ICAP_RING_VMCNT
+
 }  // namespace icap
 
 using namespace icap;
 
-// kernel variant (see gemm_kernel): ICAP_GEMM_VARIANT=0..3 overrides the default, for A/B measurements only
-static int gemm_variant_override() {
-  static const int v = [] {
-    const char* e = getenv("ICAP_GEMM_VARIANT");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
-}
-
-// 128 x 64 tiles for under-filled bf16 launches: ICAP_GEMM_NARROW=0 disables them, 12 / 13 forces that variant on
-// every bf16 launch with M > 128 (A/B measurements only); unset = automatic (gemm_plan)
-static int gemm_narrow_override() {
-  static const int v = [] {
-    const char* e = getenv("ICAP_GEMM_NARROW");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
-}
-
-// Measured on MI355X (tools/gemm_bench.py, profiles/r01_gemm_variants.txt): short K (<= 16 stages) is bound by the
-// per-block prologue/epilogue, which co-resident blocks hide -> single LDS buffer, 3-4 blocks/CU (4 when the
-// epilogue is heavy); long K favours the double-buffered main loop at 2 blocks/CU.
+// Tile-kernel variant for the launches the ring kernel does not take (f32 parity mode, K-outer dW products, beta,
+// split-K). Measured on MI355X (tools/gemm_bench.py, profiles/r01_gemm_variants.txt): short K (<= 16 stages) is
+// bound by the per-block prologue/epilogue, which co-resident blocks hide -> single LDS buffer, 3-4 blocks/CU (4
+// when the epilogue moves a second M x N tensor: dact_src read / aux store); long K favours the double-buffered
+// main loop at 2 blocks/CU.
 static int gemm_variant(const icap_gemm_args& p, int64_t nk_per_block) {
-  const int o = gemm_variant_override();
-  if (o >= 0) return o;
   if (nk_per_block > 16) return 0;
-  // 4 blocks/CU only for the epilogues that move a second M x N tensor (dact_src read / aux store); with the
-  // epilogue-operand prefetch, activation / dropout / residual epilogues run faster at 3 (profiles/r01_gemm_ab3.txt)
   const bool heavy = p.dact != ICAP_ACT_NONE || p.aux;
   return heavy ? 5 : 4;
+}
+
+// The ring kernel is opt-in: per call with path == 2, or for every eligible launch with ICAP_GEMM_RING=1. r02
+// measured it bit-identical to the tile kernels but 2-25 % slower on the step's shapes ("ring GEMM"),
+// so the tile kernels stay the default.
+static bool gemm_ring_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("ICAP_GEMM_RING");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// compute units of the current device (the ring kernel's persistent grid: one workgroup per CU)
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
 }
 
 namespace {
@@ -1371,13 +1199,29 @@ namespace {
 struct GemmPlan {
   bool skinny = false;
   int nt = 1;            // skinny: 16-column slabs per block
+  int ring = 0;          // ring kernel: WM (4 = 256 x 128 tiles, 2 = 128 x 128), 0 = not used
   int variant = 0;       // tile kernel (see ICAP_GEMM_LAUNCH)
-  int splits = 1, nk_split = 0, tiles_n = 0;
+  int splits = 1, nk_split = 0, tiles_n = 0, tiles_m = 0, units = 0;
   dim3 grid, block;
   uint32_t thr = 0;
   float inv_keep = 1.f;
 };
 }  // namespace
+
+static bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
+
+// The ring kernel's preconditions (see gemm_ring_kernel).
+static bool ring_eligible(const icap_gemm_args& p) {
+  if (p.path == 1 || (p.path != 2 && !gemm_ring_enabled())) return false;
+  if (p.in_dtype != ICAP_BF16 || p.c_dtype != ICAP_BF16 || p.trans_ab || p.beta != 0.f || p.ln_gamma) return false;
+  // K > 128: three k-steps per tile at least (a unit's bias buffer is reused two units later; see the kernel)
+  if (p.split_k > 1 || p.M <= 128 || p.K <= 128 || (p.N & 7) || (p.K & 7) || (p.ldc & 7) || !al16(p.C)) return false;
+  if (p.aux && ((p.ldaux & 7) || !al16(p.aux))) return false;
+  if (p.dact != ICAP_ACT_NONE && ((p.ld_dact & 7) || !al16(p.dact_src))) return false;
+  if (p.dact == ICAP_ACT_NONE && p.resid && ((p.ldr & 7) || !al16(p.resid))) return false;
+  if (p.bias && (reinterpret_cast<uintptr_t>(p.bias) & 3)) return false;
+  return true;
+}
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
@@ -1395,6 +1239,8 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
                "icap_gemm: a 256-row operand panel must stay below 2 GiB");
   ICAP_REQUIRE(p.beta == 0.f || p.c_dtype == ICAP_F32, "icap_gemm: beta != 0 requires f32 C");
   ICAP_REQUIRE(p.dact == ICAP_ACT_NONE || p.dact_src != nullptr, "icap_gemm: dact requires dact_src");
+  ICAP_REQUIRE(p.act >= ICAP_ACT_NONE && p.act <= ICAP_ACT_GELU_ERF && p.dact >= ICAP_ACT_NONE &&
+                   p.dact <= ICAP_ACT_GELU_ERF, "icap_gemm: unknown activation");
   ICAP_REQUIRE(p.drop_p >= 0.f && p.drop_p < 1.f, "icap_gemm: drop_p out of range");
   if (p.trans_ab) {
     ICAP_REQUIRE(p.in_dtype == ICAP_BF16, "icap_gemm: trans_ab needs bf16 inputs");
@@ -1406,18 +1252,6 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   const int64_t tiles_m = (p.M + GBM - 1) / GBM;
   int64_t tiles_n = (p.N + GBN - 1) / GBN;
   int64_t tiles = tiles_m * tiles_n;
-  // Short-K launches (<= 16 stages) of fewer than 4 tiles of 128 x 128 per CU (the N = 768 products, the mapper's
-  // M = 3200 and CLIP's M = 6400 ones) run faster on 128 x 64 tiles: twice the blocks, so a CU holds more of them
-  // to hide each one's prologue / epilogue; longer K keeps 128 x 128 (profiles/r01_gemm_narrow.txt).
-  const int narrow_env = gemm_narrow_override();
-  const int64_t nk_all = (p.K + 128 / (p.in_dtype == ICAP_BF16 ? 2 : 4) - 1) / (128 / (p.in_dtype == ICAP_BF16 ? 2 : 4));
-  const bool narrow = p.in_dtype == ICAP_BF16 && p.M > 128 && narrow_env != 0 && !p.trans_ab &&
-                      (narrow_env > 0 || (tiles < 1024 && nk_all <= 16 && gemm_variant_override() < 0));
-  const int narrow_variant = narrow_env > 1 ? narrow_env : (tiles < 256 ? 12 : 13);
-  if (narrow) {
-    tiles_n = (p.N + 63) / 64;
-    tiles = tiles_m * tiles_n;
-  }
   ICAP_REQUIRE(tiles < (1ll << 26), "icap_gemm: too many tiles");
   ICAP_REQUIRE(p.split_k >= 0, "icap_gemm: split_k must be >= 0");
   pl.thr = p.drop_p > 0.f ? drop_threshold(p.drop_p) : 0u;
@@ -1425,12 +1259,26 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   const bool fuse_ln = p.ln_gamma != nullptr;
   ICAP_REQUIRE(!fuse_ln || (p.ln_beta && p.M <= 128 && p.split_k == 0 && !p.trans_ab && p.K <= 4096),
                "icap_gemm: ln_gamma needs ln_beta, M <= 128, K <= 4096, no split_k / trans_ab");
-  if (p.M <= 128 && p.split_k == 0 && (tiles <= 128 || fuse_ln) && (gemm_variant_override() < 0 || fuse_ln) &&
-      !p.trans_ab) {
+  if (p.M <= 128 && p.split_k == 0 && (tiles <= 128 || fuse_ln) && !p.trans_ab) {
     pl.skinny = true;
     pl.nt = p.N > 1536 ? 2 : 1;  // 32-column slabs once there are enough of them
     pl.grid = dim3((unsigned)((p.N + 16 * pl.nt - 1) / (16 * pl.nt)), (unsigned)((p.M + 31) / 32));
     pl.block = dim3(64 * SK_WAVES);
+    return ICAP_OK;
+  }
+  // persistent ring kernel (one workgroup per CU, many output tiles each) for every eligible launch except the
+  // decode-sized ones (<= 64 tiles of 128 x 128), which keep split-K unless the caller asks for one pass:
+  // 256 x 128 tiles when they give every CU work, 128 x 128 otherwise
+  if (ring_eligible(p) && (p.split_k == 1 || tiles > 64)) {
+    const int cus = device_cus();
+    const int64_t tn = (p.N + 127) / 128;
+    const int64_t tm4 = (p.M + 255) / 256, tm2 = (p.M + 127) / 128;
+    pl.ring = tm4 * tn >= cus * 3 / 4 ? 4 : 2;
+    pl.tiles_m = (int)(pl.ring == 4 ? tm4 : tm2);
+    pl.tiles_n = (int)tn;
+    pl.units = pl.tiles_m * pl.tiles_n;
+    pl.grid = dim3((unsigned)(pl.units < cus ? pl.units : cus));
+    pl.block = dim3(128 * pl.ring);
     return ICAP_OK;
   }
   // split-K over K stages for launches that cannot fill the chip (decode-time M = batch, small projections):
@@ -1442,8 +1290,6 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   if (p.split_k > 1) {
     splits = p.split_k;
   } else if (p.split_k == 0 && p.workspace && (p.N & 3) == 0 && nk >= 2 && (tiles <= 64 || (tiles < 256 && nk >= 16))) {
-    // decode-sized launches (<= 64 tiles): as many splits as fill ~2 blocks/CU; under-filled long-K launches
-    // (dW products over all tokens, K = 3200+): keep >= 4 stages per split so the slab traffic stays small
     // the count depends on the shape alone — never on the workspace a caller passes — so a product computed on
     // another stream with its own scratch sums its K ranges in the same order and rounds identically (a
     // workspace too small for the shape's split is an error below, not a silent change of the summation order)
@@ -1461,66 +1307,35 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
                      p.workspace_bytes >= splits * slab,
                  "icap_gemm: split-K workspace missing, misaligned or too small");
   }
+  // Short-K launches (<= 16 stages) of fewer than 4 tiles of 128 x 128 per CU (the N = 768 products, the mapper's
+  // M = 3200 and CLIP's M = 6400 ones) run faster on 128 x 64 tiles: twice the blocks, so a CU holds more of them
+  // to hide each one's prologue / epilogue; longer K keeps 128 x 128 (profiles/r01_gemm_narrow.txt).
+  const bool narrow = p.in_dtype == ICAP_BF16 && p.M > 128 && !p.trans_ab && tiles < 1024 && nk <= 16 && splits == 1;
   pl.splits = (int)splits;
   pl.nk_split = (int)nk_split;
   pl.variant = gemm_variant(p, nk_split);
-  if (narrow) pl.variant = narrow_variant;
+  if (narrow) {
+    tiles_n = (p.N + 63) / 64;
+    tiles = tiles_m * tiles_n;
+    pl.variant = tiles < 256 ? 12 : 13;
+  }
   if (p.trans_ab) pl.variant = nk_split > 16 ? 14 : 15;  // K-outer forms of variants 0 / 4
   pl.tiles_n = (int)tiles_n;
   pl.block = dim3(GNT);
   pl.grid = dim3((unsigned)(tiles * splits));
-  if (pl.variant == 6 || pl.variant == 8) {  // 256x256
-    const int64_t tm2 = (p.M + 255) / 256, tn2 = (p.N + 255) / 256;
-    pl.grid = dim3((unsigned)(tm2 * tn2 * splits));
-    pl.tiles_n = (int)tn2;
-    pl.block = dim3(512);
-  } else if (pl.variant == 9) {  // 256x128
-    const int64_t tm2 = (p.M + 255) / 256;
-    pl.grid = dim3((unsigned)(tm2 * tiles_n * splits));
-    pl.block = dim3(512);
-  } else if (pl.variant == 16 || pl.variant == 17) {  // 8 waves of 64 x 64: 256 x 128 / 128 x 256 (bf16 only)
-    if (p.in_dtype != ICAP_BF16) {
-      pl.variant = 0;
-    } else {
-      const int bm = pl.variant == 16 ? 256 : 128, bn = pl.variant == 16 ? 128 : 256;
-      const int64_t tm2 = (p.M + bm - 1) / bm, tn2 = (p.N + bn - 1) / bn;
-      pl.grid = dim3((unsigned)(tm2 * tn2 * splits));
-      pl.tiles_n = (int)tn2;
-      pl.block = dim3(512);
-    }
-  } else if (pl.variant == 10 || pl.variant == 11) {  // phase-interleaved 8-wave: 256x256 / 256x128 (bf16 only)
-    if (p.in_dtype != ICAP_BF16) {
-      pl.variant = 0;
-    } else {
-      const int bn = pl.variant == 10 ? 256 : 128;
-      const int64_t tm2 = (p.M + 255) / 256, tn2 = (p.N + bn - 1) / bn;
-      pl.grid = dim3((unsigned)(tm2 * tn2 * splits));
-      pl.tiles_n = (int)tn2;
-      pl.block = dim3(512);
-    }
-  }
   return ICAP_OK;
 }
 
-// "TI, TC, template ints" of each variant (keep in sync with ICAP_GEMM_LAUNCH)
+// "TI, TC, template ints" of each tile variant (keep in sync with the launch switch below)
 static const char* variant_kernel(int v) {
   switch (v) {
     case 0: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, false>";
     case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, false>";
     case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4, false>";
     case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2, false>";
-    case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true>";
-    case 16: return "gemm_kernel<%s, %s, 2, 1, 4, 2, 4, 4, false>";
-    case 17: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 4, 4, false>";
-    case 15: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true>";
     case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2, false>";
-    case 6: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 8, 4, false>";
-    case 7: return "gemm2b_kernel<%s, %s, 2, 2, 2, 4, 4>";
-    case 8: return "gemm2b_kernel<%s, %s, 1, 2, 4, 8, 4>";
-    case 9: return "gemm3b_kernel<%s, %s, 1, 4, 2, 4, 4>";
-    case 10: return "gemm8p_kernel<%s, 256>";
-    case 11: return "gemm8p_kernel<%s, 128>";
-    default: return "gemm3b_kernel<%s, %s, 1, 2, 2, 4, 4>";
+    case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true>";
+    default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true>";
   }
 }
 
@@ -1533,9 +1348,10 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
   const char* tc = a->c_dtype == ICAP_BF16 ? "unsigned short" : "float";
   char fmt[96];
   if (pl.skinny) snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2>", pl.nt);
+  else if (pl.ring) snprintf(fmt, sizeof fmt, "gemm_ring_kernel<%d, %d>", pl.ring, pl.ring == 4 ? 3 : 4);
   else snprintf(fmt, sizeof fmt, "%s", variant_kernel(pl.variant));
   char inner[128];
-  if (!pl.skinny && (pl.variant == 10 || pl.variant == 11)) snprintf(inner, sizeof inner, fmt, tc);
+  if (pl.ring) snprintf(inner, sizeof inner, "%s", fmt);
   else snprintf(inner, sizeof inner, fmt, ti, tc);
   snprintf(buf, sizeof buf, "icap::%s", inner);
   return buf;
@@ -1564,6 +1380,15 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
 #undef ICAP_SKINNY
     return check_launch("icap_gemm(skinny)");
   }
+  if (pl.ring) {
+    if (pl.ring == 4)
+      hipLaunchKernelGGL((gemm_ring_kernel<4, 3>), pl.grid, pl.block, 0, s, p, pl.tiles_m, pl.tiles_n, pl.units, thr,
+                         inv_keep);
+    else
+      hipLaunchKernelGGL((gemm_ring_kernel<2, 4>), pl.grid, pl.block, 0, s, p, pl.tiles_m, pl.tiles_n, pl.units, thr,
+                         inv_keep);
+    return check_launch("icap_gemm(ring)");
+  }
   const dim3 grid = pl.grid, block = pl.block;
   const int sp = pl.splits, nks = pl.nk_split, tn = pl.tiles_n;
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
@@ -1571,12 +1396,7 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   switch (pl.variant) {                                                                                        \
     case 0: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
     case 4: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 3, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 5: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 4, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 6: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 1, 2, 4, 8, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 7: hipLaunchKernelGGL((gemm2b_kernel<TI, TC, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 8: hipLaunchKernelGGL((gemm2b_kernel<TI, TC, 1, 2, 4, 8, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 9: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 4, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    default: hipLaunchKernelGGL((gemm3b_kernel<TI, TC, 1, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+    default: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 4, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
   }
   if (pl.variant == 14 || pl.variant == 15) {  // K-outer operands (bf16 inputs only)
     if (p.c_dtype == ICAP_BF16) {
@@ -1586,14 +1406,6 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
       if (pl.variant == 14) hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 2, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
       else hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 1, 3, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
     }
-  } else if (pl.variant == 16 || pl.variant == 17) {  // 256 x 128 / 128 x 256, 8 waves (bf16 inputs only)
-    if (p.c_dtype == ICAP_BF16) {
-      if (pl.variant == 16) hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 1, 4, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 1, 2, 4, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-    } else {
-      if (pl.variant == 16) hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 1, 4, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 1, 2, 4, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-    }
   } else if (pl.variant == 12 || pl.variant == 13) {  // 128 x 64 (bf16 inputs only)
     if (p.c_dtype == ICAP_BF16) {
       if (pl.variant == 12) hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 3, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
@@ -1601,14 +1413,6 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     } else {
       if (pl.variant == 12) hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 3, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
       else hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 1, 4, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-    }
-  } else if (pl.variant == 10 || pl.variant == 11) {  // bf16 inputs (the plan falls back to variant 0 otherwise)
-    if (pl.variant == 10) {
-      if (p.c_dtype == ICAP_BF16) hipLaunchKernelGGL((gemm8p_kernel<bf16_t, 256>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm8p_kernel<float, 256>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-    } else {
-      if (p.c_dtype == ICAP_BF16) hipLaunchKernelGGL((gemm8p_kernel<bf16_t, 128>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm8p_kernel<float, 128>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
     }
   } else if (p.in_dtype == ICAP_BF16) {
     if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(bf16_t, bf16_t) } else { ICAP_GEMM_LAUNCH(bf16_t, float) }

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libicap_hip.so")
 
 F32, BF16 = 0, 1
-ACT_NONE, ACT_GELU_NEW, ACT_RELU, ACT_QUICK_GELU, ACT_TANH = 0, 1, 2, 3, 4
+ACT_NONE, ACT_GELU_NEW, ACT_RELU, ACT_QUICK_GELU, ACT_TANH, ACT_GELU_ERF = 0, 1, 2, 3, 4, 5
 
 vp = C.c_void_p
 i32, i64, u64, f32, sz = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_size_t
@@ -44,6 +44,7 @@ class GemmArgs(C.Structure):
         ("m_dev", vp),
         ("trans_ab", i32),
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
+        ("path", i32),
     ]
 
 

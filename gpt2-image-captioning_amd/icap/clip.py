@@ -303,7 +303,8 @@ def resize_shortest_edge(wh, size: int):
 
 class CLIPProcessor:
     """Host-side CLIPImageProcessor equivalent: shortest-edge resize (bicubic) to 224, centre crop, /255,
-    mean/std normalise -> fp32 [B,3,224,224]. (Device-side preprocessing is SURVEY.md §8f rank 1: later.)"""
+    mean/std normalise -> fp32 [B,3,224,224]. Images: PIL images or RGB uint8 arrays. DeviceCLIPProcessor runs
+    the same arithmetic on the GPU."""
 
     def __init__(self, size: int = 224):
         self.size = size
@@ -316,7 +317,7 @@ class CLIPProcessor:
             images = [images]
         out = []
         for im in images:
-            im = im.convert("RGB")
+            im = Image.fromarray(np.asarray(im, dtype=np.uint8)) if isinstance(im, np.ndarray) else im.convert("RGB")
             im = im.resize(resize_shortest_edge(im.size, self.size), Image.BICUBIC)
             w, h = im.size
             left, top = (w - self.size) // 2, (h - self.size) // 2
@@ -362,16 +363,10 @@ def extract_clip_embedding_from_image(image, clip_model: CLIPVisionTower, clip_p
 def extract_clip_embeddings(image_dir: str, output_path: str, clip_model: CLIPVisionTower,
                             clip_processor: CLIPProcessor, batch_size: int = 32, num_workers: int = 4,
                             device: Optional[torch.device] = None) -> None:
-    """clip.py:79-149: every image of a directory -> {"filenames", "embeddings"} .pt file (same format)."""
-    from PIL import Image
+    """clip.py:79-149: every image of a directory -> {"filenames", "embeddings"} .pt file (same format, same file
+    order). JPEG decode runs in `num_workers` DataLoader processes as in the reference (icap.images)."""
+    from .images import extract_directory
 
-    exts = {".jpg", ".jpeg", ".png", ".webp"}
-    names = [f for f in os.listdir(image_dir) if os.path.splitext(f)[1].lower() in exts]
-    dev = device or clip_model.device
-    embs: List[Tensor] = []
-    for i in range(0, len(names), batch_size):
-        chunk = names[i:i + batch_size]
-        px = clip_processor(images=[Image.open(os.path.join(image_dir, n)) for n in chunk]).pixel_values
-        embs.append(clip_model.embed(px.to(dev)).cpu())
-    final = torch.cat(embs, 0) if embs else torch.empty((0, clip_model.config.projection_dim))
-    torch.save({"filenames": names, "embeddings": final}, output_path)
+    n = extract_directory(image_dir, output_path, clip_model.embed, clip_processor, clip_model.config.projection_dim,
+                          batch_size, num_workers, device or clip_model.device)
+    print(f"Saved {n} CLIP embeddings to {output_path}.")

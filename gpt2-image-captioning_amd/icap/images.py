@@ -1,0 +1,64 @@
+"""Image-directory loading shared by the embedding extractors (src/utils.py:119-173 ImageDirectoryDataset and the
+DataLoader loops of src/embeddings/clip.py:79-149 / vit.py:80-137).
+
+The reference decodes JPEGs in `num_workers` DataLoader processes and preprocesses each batch on the host; here the
+workers decode to RGB uint8 arrays (cheap to hand between processes) and the batch goes to the tower's processor
+(the device one runs resize / crop / normalise as HIP kernels). Filenames come in os.listdir order filtered by
+extension, exactly as the reference lists them, so the saved .pt rows line up with the reference's.
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Callable, List, Tuple
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader, Dataset
+
+IMAGE_EXTS = {".jpg", ".jpeg", ".png", ".webp"}  # src/utils.py:131
+
+
+class ImageDirectoryDataset(Dataset):
+    """src/utils.py:119-173: (filename, image) per file of a flat directory; images as RGB uint8 [H, W, 3]."""
+
+    def __init__(self, directory: str) -> None:
+        self.directory = directory
+        self.filenames = [f for f in os.listdir(directory) if os.path.splitext(f)[1].lower() in IMAGE_EXTS]
+
+    def __len__(self) -> int:
+        return len(self.filenames)
+
+    def __getitem__(self, idx: int) -> Tuple[str, np.ndarray]:
+        from PIL import Image
+
+        name = self.filenames[idx]
+        with Image.open(os.path.join(self.directory, name)) as im:
+            return name, np.asarray(im.convert("RGB"))
+
+    @staticmethod
+    def collate_fn(batch) -> Tuple[List[str], List[np.ndarray]]:
+        names, images = zip(*batch)
+        return list(names), list(images)
+
+
+@torch.no_grad()
+def extract_directory(image_dir: str, output_path: str, embed: Callable, processor, out_dim: int,
+                      batch_size: int = 32, num_workers: int = 4, device=None) -> int:
+    """Every image of `image_dir` -> {"filenames": [...], "embeddings": fp32 [N, out_dim]} saved with torch.save
+    (src/embeddings/clip.py:147-149 format). `embed(pixel_values)` returns L2-normalised features on the device.
+    Returns the number of images."""
+    ds = ImageDirectoryDataset(image_dir)
+    dl = DataLoader(ds, batch_size=batch_size, shuffle=False, num_workers=num_workers,
+                    collate_fn=ImageDirectoryDataset.collate_fn, persistent_workers=False)
+    names: List[str] = []
+    embs: List[torch.Tensor] = []
+    for batch_names, batch_images in dl:
+        px = processor(images=batch_images).pixel_values
+        if device is not None:
+            px = px.to(device, non_blocking=True)
+        embs.append(embed(px).cpu())
+        names.extend(batch_names)
+    final = torch.cat(embs, 0) if embs else torch.empty((0, out_dim))
+    torch.save({"filenames": names, "embeddings": final}, output_path)
+    return len(names)

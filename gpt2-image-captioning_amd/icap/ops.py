@@ -70,7 +70,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          resid: Optional[Tensor] = None, alpha: float = 1.0, beta: float = 0.0, drop: Dropout = NO_DROP,
          M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None,
          alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None,
-         trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None) -> Tensor:
+         trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None,
+         tile_only: bool = False, ring: bool = False) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
     workspace: fp32 split-K scratch for launches on a stream other than the package's main one (the per-device
     default serves every GEMM ordered on one stream). The split count depends on the shape alone, so the result
@@ -79,7 +80,9 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     ln: (gamma, beta, eps) — A is LayerNorm-ed over its K columns inside the GEMM (M <= 128 launches).
     alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).
     split_k: 0 = automatic split-K for launches of <= 64 output tiles, 1 = never, > 1 = forced.
-    m_dev: device int32 row count <= M (rows past it are neither computed nor stored)."""
+    m_dev: device int32 row count <= M (rows past it are neither computed nor stored).
+    tile_only: never the persistent ring kernel; ring: the persistent ring kernel wherever its preconditions hold
+    (it is opt-in: A/B measurements, path-equality tests)."""
     if trans_ab:
         M = A.shape[1] if M is None else M
         K = A.shape[0] if K is None else K
@@ -112,6 +115,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     ws = gemm_workspace(A.device) if workspace is None else workspace
     a.workspace, a.workspace_bytes, a.split_k = ws.data_ptr(), ws.numel() * 4, split_k
     a.m_dev = _p(m_dev)
+    a.path = 1 if tile_only else (2 if ring else 0)
     if ln is not None:
         a.ln_gamma, a.ln_beta, a.ln_eps = ln[0].data_ptr(), ln[1].data_ptr(), float(ln[2])
     if GEMM_TIMER is None:

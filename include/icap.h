@@ -42,7 +42,8 @@ enum {
   ICAP_ACT_GELU_NEW = 1,   /* HF/activations.py:59-66 (GPT-2 gelu_new)        */
   ICAP_ACT_RELU = 2,       /* TORCH/nn/modules/transformer.py (mapper FFN)     */
   ICAP_ACT_QUICK_GELU = 3, /* HF/activations.py:117-123 (CLIP)                 */
-  ICAP_ACT_TANH = 4        /* src/models.py:29 (MLPMappingNetwork activation)  */
+  ICAP_ACT_TANH = 4,       /* src/models.py:29 (MLPMappingNetwork activation)  */
+  ICAP_ACT_GELU_ERF = 5    /* exact erf GELU (HF ViT hidden_act "gelu", src/embeddings/vit.py) */
 };
 enum { ICAP_OK = 0, ICAP_ERR_ARG = 1, ICAP_ERR_LAUNCH = 2 };
 
@@ -103,6 +104,10 @@ typedef struct {
   /* then * ln_gamma[k] + ln_beta[k], rounded to the input dtype) — the decode step's ln_1 / ln_2 fused    */
   /* into the QKV / c_fc GEMMs (HF/models/gpt2/modeling_gpt2.py:281,301). Only for M <= 128 launches.     */
   const float* ln_gamma; const float* ln_beta; float ln_eps;
+  /* path: 0 = automatic kernel choice (tile kernels; the ring kernel too when ICAP_GEMM_RING=1);             */
+  /* 1 = the 128-row tile kernels only; 2 = the persistent ring kernel wherever its preconditions hold —       */
+  /* for A/B measurements and for tests that compare the two paths (identical MFMA chains: bitwise equal).     */
+  int32_t path;
 } icap_gemm_args;
 /* name of the kernel instantiation icap_gemm launches for these arguments    */
 /* (as rocprofv3 prints it, minus the parameter list); NULL on invalid args.   */

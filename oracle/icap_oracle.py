@@ -482,6 +482,86 @@ def clip_embed_normalized(sd, cfg: ClipCfg, pixels: Tensor) -> Tensor:
     return f / f.norm(p=2, dim=-1, keepdim=True)
 
 
+# --------------------------------------------------------------------------- ViT-B/16 (a16)
+
+
+@dataclass
+class ViTCfg:  # HF ViTConfig defaults = google/vit-base-patch16-224 (src/embeddings/vit.py:10-35)
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    patch: int = 16
+    image: int = 224
+    inter: int = 3072
+    eps: float = 1e-12
+    channels: int = 3
+
+
+def vit_state_dict(cfg: ViTCfg, seed: int = 0) -> Dict[str, Tensor]:
+    """HF ViTModel parameter names as transformers 4.57 (the reference's pin) spells them."""
+    d, g = cfg.hidden, cfg.image // cfg.patch
+    sd = {
+        "embeddings.cls_token": gen_tensor(seed, "v.cls", (1, 1, d), 0.5),
+        "embeddings.position_embeddings": gen_tensor(seed, "v.pos", (1, g * g + 1, d), 0.02),
+        "embeddings.patch_embeddings.projection.weight": gen_tensor(seed, "v.patch.w", (d, cfg.channels, cfg.patch, cfg.patch), 0.02),
+        "embeddings.patch_embeddings.projection.bias": gen_tensor(seed, "v.patch.b", (d,), 0.02),
+        "layernorm.weight": gen_tensor(seed, "v.ln.w", (d,), 0.05, 1.0),
+        "layernorm.bias": gen_tensor(seed, "v.ln.b", (d,), 0.02),
+        "pooler.dense.weight": gen_tensor(seed, "v.pool.w", (d, d), 0.02),
+        "pooler.dense.bias": gen_tensor(seed, "v.pool.b", (d,), 0.02),
+    }
+    for i in range(cfg.layers):
+        p = f"encoder.layer.{i}."
+        for nm in ("query", "key", "value"):
+            sd[p + f"attention.attention.{nm}.weight"] = gen_tensor(seed, p + nm + ".w", (d, d), 0.02)
+            sd[p + f"attention.attention.{nm}.bias"] = gen_tensor(seed, p + nm + ".b", (d,), 0.02)
+        sd[p + "attention.output.dense.weight"] = gen_tensor(seed, p + "ao.w", (d, d), 0.02)
+        sd[p + "attention.output.dense.bias"] = gen_tensor(seed, p + "ao.b", (d,), 0.02)
+        sd[p + "intermediate.dense.weight"] = gen_tensor(seed, p + "fc1.w", (cfg.inter, d), 0.02)
+        sd[p + "intermediate.dense.bias"] = gen_tensor(seed, p + "fc1.b", (cfg.inter,), 0.02)
+        sd[p + "output.dense.weight"] = gen_tensor(seed, p + "fc2.w", (d, cfg.inter), 0.02)
+        sd[p + "output.dense.bias"] = gen_tensor(seed, p + "fc2.b", (d,), 0.02)
+        sd[p + "layernorm_before.weight"] = gen_tensor(seed, p + "lnb.w", (d,), 0.05, 1.0)
+        sd[p + "layernorm_before.bias"] = gen_tensor(seed, p + "lnb.b", (d,), 0.02)
+        sd[p + "layernorm_after.weight"] = gen_tensor(seed, p + "lna.w", (d,), 0.05, 1.0)
+        sd[p + "layernorm_after.bias"] = gen_tensor(seed, p + "lna.b", (d,), 0.02)
+    return sd
+
+
+def vit_pooler_output(sd: Dict[str, Tensor], cfg: ViTCfg, pixels: Tensor) -> Tensor:
+    """ViTModel(pixel_values).pooler_output — HF/models/vit/modeling_vit.py: patch Conv2d (with bias) -> [CLS ||
+    patches] + position embeddings -> pre-LN layers (layernorm_before, MHA, +res, layernorm_after, dense + erf-GELU,
+    dense, +res; eps 1e-12) -> final layernorm -> pooler tanh(dense(CLS)) :289-301,385-386."""
+    d, H = cfg.hidden, cfg.heads
+    hd = d // H
+    B = pixels.shape[0]
+    pe = F.conv2d(pixels, sd["embeddings.patch_embeddings.projection.weight"],
+                  sd["embeddings.patch_embeddings.projection.bias"], stride=cfg.patch).flatten(2).transpose(1, 2)
+    x = torch.cat([sd["embeddings.cls_token"].expand(B, -1, -1), pe], dim=1) + sd["embeddings.position_embeddings"]
+    S = x.shape[1]
+    for i in range(cfg.layers):
+        p = f"encoder.layer.{i}."
+        a = F.layer_norm(x, (d,), sd[p + "layernorm_before.weight"], sd[p + "layernorm_before.bias"], cfg.eps)
+        q = a @ sd[p + "attention.attention.query.weight"].t() + sd[p + "attention.attention.query.bias"]
+        k = a @ sd[p + "attention.attention.key.weight"].t() + sd[p + "attention.attention.key.bias"]
+        v = a @ sd[p + "attention.attention.value.weight"].t() + sd[p + "attention.attention.value.bias"]
+        q, k, v = (t.view(B, S, H, hd).transpose(1, 2) for t in (q, k, v))
+        w = torch.softmax((q @ k.transpose(-1, -2)) / math.sqrt(hd), dim=-1)
+        o = (w @ v).transpose(1, 2).reshape(B, S, d)
+        x = x + (o @ sd[p + "attention.output.dense.weight"].t() + sd[p + "attention.output.dense.bias"])
+        a = F.layer_norm(x, (d,), sd[p + "layernorm_after.weight"], sd[p + "layernorm_after.bias"], cfg.eps)
+        f = F.gelu(a @ sd[p + "intermediate.dense.weight"].t() + sd[p + "intermediate.dense.bias"])  # erf GELU
+        x = x + (f @ sd[p + "output.dense.weight"].t() + sd[p + "output.dense.bias"])
+    x = F.layer_norm(x, (d,), sd["layernorm.weight"], sd["layernorm.bias"], cfg.eps)
+    return torch.tanh(x[:, 0] @ sd["pooler.dense.weight"].t() + sd["pooler.dense.bias"])
+
+
+def vit_embed_normalized(sd, cfg: ViTCfg, pixels: Tensor) -> Tensor:
+    """src/embeddings/vit.py:63-72 / :113-120: pooler_output then L2 normalise."""
+    f = vit_pooler_output(sd, cfg, pixels)
+    return f / f.norm(p=2, dim=-1, keepdim=True)
+
+
 # --------------------------------------------------------------------------- optimisation
 
 

@@ -85,8 +85,13 @@ def test_gemm_kernel_name_query_without_gpu():
     """icap_gemm_kernel_name names the instantiation icap_gemm would launch (bench.py keys its roofline by it,
     matching rocprofv3's kernel names)."""
     lib = _lib.load()
-    big = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 50304, 768))).decode()
-    assert big.startswith("icap::gemm") and "unsigned short, unsigned short" in big
+    big = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 50304, 768, path=2))).decode()
+    assert big == "icap::gemm_ring_kernel<4, 3>", big  # persistent ring kernel (opt-in), 256 x 128 tiles
+    mid = lib.icap_gemm_kernel_name(C.byref(_gemm_args(3200, 768, 3072, path=2, split_k=1))).decode()
+    assert mid == "icap::gemm_ring_kernel<2, 4>", mid  # too few 256-row tiles to fill the chip: 128 x 128
+    for path in (0, 1):  # the default is the tile kernels
+        tile = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 50304, 768, path=path))).decode()
+        assert tile.startswith("icap::gemm_kernel<") and "unsigned short, unsigned short" in tile
     skinny = lib.icap_gemm_kernel_name(C.byref(_gemm_args(128, 2304, 768))).decode()
     assert skinny.startswith("icap::gemm_skinny_kernel<unsigned short, unsigned short, 2")
     f32 = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 768, 768, c_dtype=_lib.F32))).decode()

@@ -149,3 +149,74 @@ def test_adamw_restatement_matches_torch():
         O.clip_and_adamw(ps, gr, st, 1e-3, 1, 6)
     for p, v in zip(tp, ps.values()):
         assert torch.allclose(p.detach(), v, rtol=1e-6, atol=1e-7)
+
+
+MED_G = O.GPT2Cfg(n_layer=24, n_embd=1024, n_head=16)  # BASELINE configs[3]: GPT-2 medium
+MED_M = O.MapperCfg(embed_dim=768, gpt_dim=1024)     # mapper over CLIP-L/14 (768-d), head dim 128
+L14 = O.ClipCfg(hidden=1024, layers=24, heads=16, patch=14, image=224, inter=4096, proj=768)
+
+
+def test_medium_forward_greedy_train():
+    """configs[3] geometry pinned to the reference (tools/make_goldens.py golden_medium)."""
+    g = load("medium")
+    gsd, msd = O.gpt2_state_dict(MED_G, 0), O.mapper_state_dict(MED_M, 0)
+    ids, mask, labels, emb = inputs(g)
+    prefix = O.mapper_forward(msd, MED_M, emb)
+    assert rel(prefix, g["prefix"]) < 1e-5
+    loss, logits = O.caption_forward(gsd, MED_G, prefix, ids, mask, labels)
+    assert abs(loss.item() - g["loss"][0]) < 1e-5
+    assert rel(logits[:2][:, g["logit_rows"]], g["logits_sel"]) < 1e-5
+    gen = O.greedy_generate(gsd, MED_G, prefix[: g["greedy"].shape[0]], max_length=g["greedy"].shape[1])
+    assert np.array_equal(gen.numpy(), g["greedy"])
+    n = len(g["train_losses"])
+    losses, _, new_m, _ = O.train_steps(gsd, MED_G, msd, MED_M, [inputs(g)] * n, total_steps=n)
+    assert rel(losses, g["train_losses"]) < 1e-5
+    for k, v in new_m.items():
+        t = v.double()
+        assert rel([t.sum().item(), t.abs().sum().item()], g["trained_ck." + k][:2]) < 1e-4, k
+
+
+def test_clip_l14():
+    g = load("clip_l14")
+    sd = O.clip_vision_state_dict(L14, 0)
+    px = torch.randn((2, 3, 224, 224), generator=torch.Generator().manual_seed(int(g["pixels_seed"][0])))
+    assert rel(O.clip_image_features(sd, L14, px), g["features"]) < 1e-5
+    assert rel(O.clip_embed_normalized(sd, L14, px), g["embeddings"]) < 1e-5
+
+
+def test_small_train_three_steps_and_unfrozen(small_weights):
+    """3 frozen reference train() steps (whole / sampled trained tensors) and 2 unfrozen ones (every GPT-2 tensor)."""
+    g = load("small_train")
+    gsd, msd = small_weights
+    batch = inputs(g)
+    losses, _, new_m, _ = O.train_steps(gsd, O.GPT2Cfg(), msd, O.MapperCfg(), [batch] * 3, total_steps=3)
+    assert rel(losses, g["train_losses"]) < 1e-5
+    for k, v in new_m.items():
+        if "trained." + k in g:
+            ref, got, init = g["trained." + k], v.numpy(), msd[k].numpy()
+        elif "trained_sample." + k in g:
+            ref = g["trained_sample." + k]
+            got, init = v.numpy().reshape(-1)[::97], msd[k].numpy().reshape(-1)[::97]
+        else:
+            continue
+        assert np.abs(got - ref).max() <= 0.03 * np.abs(ref - init).max() + 1e-9, k
+    losses2, _, _, g2 = O.train_steps(gsd, O.GPT2Cfg(), msd, O.MapperCfg(), [batch] * 2, total_steps=2,
+                                      freeze_gpt=False)
+    assert rel(losses2, g["unfrozen_losses"]) < 1e-5
+    for k, v in g2.items():
+        t = v.double()
+        assert rel([t.sum().item(), t.abs().sum().item()], g["unfrozen_ck.gpt." + k][:2]) < 1e-5, k
+
+
+def test_topp_filter_matches_reference():
+    """The reference's own top-p filter output (src/models.py:400-449 as it ran: probs > 0 after filtering) equals
+    the oracle's restatement on the same logits, at every recorded step and row."""
+    g = load("topp_filter")
+    T, p = float(g["temperature"][0]), float(g["top_p"][0])
+    for step in range(g["probs"].shape[0]):
+        kept_ref = g["probs"][step] > 0
+        kept = O.topp_filter_reference(torch.from_numpy(g["logits"][step]), T, p).numpy()
+        assert np.array_equal(kept, kept_ref), step
+        # and the kernel's fixed-point restatement keeps the same set
+        _, kept_fixed = O.topp_sample_fixed(g["logits"][step], T, p, seed=3, step=step, eos=511)
+        assert np.array_equal(kept_fixed, kept_ref), step

@@ -1,0 +1,239 @@
+"""Round-2 parity of the HIP path against goldens produced by the reference itself (tools/make_goldens.py):
+
+* BASELINE configs[3] geometry — GPT-2 medium + transformer mapper at gpt_dim 1024 (head dim 128) + CLIP ViT-L/14;
+* the ViT-B/16 tower;
+* the benchmarked precision (bf16) against the reference's fp32 train() and greedy decode, with stated bounds;
+* greedy decode at the benchmarked decode shape (128 captions x 50 tokens) in fp32 parity mode;
+* the top-p sampler against the reference's own filter output.
+
+Tolerances are written per test (fp32 parity mode: loss |d| <= 2e-5 (3e-5 at 24 layers), logits max-rel <= 1e-4,
+greedy ids exact; bf16: stated per test)."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from icap import ops
+from icap.clip import CLIPVisionConfig, CLIPVisionTower
+from icap.vit import ViTImageTower
+from oracle import icap_oracle as O
+from test_model_gpu import _trainer_steps, build, inputs, load, rel
+
+pytestmark = pytest.mark.gpu
+
+MED_G = O.GPT2Cfg(n_layer=24, n_embd=1024, n_head=16)
+MED_M = O.MapperCfg(embed_dim=768, gpt_dim=1024)
+L14 = O.ClipCfg(hidden=1024, layers=24, heads=16, patch=14, image=224, inter=4096, proj=768)
+
+
+# ------------------------------------------------------------------------------------------ configs[3] (medium)
+
+
+@pytest.fixture(scope="module")
+def medium_f32(dev):
+    return build(MED_G, MED_M, torch.float32, dev)
+
+
+def test_medium_forward_f32(dev, medium_f32):
+    g = load("medium")
+    ids, mask, labels, emb = inputs(g, dev)
+    model = medium_f32.eval()
+    with torch.no_grad():
+        out = model(ids, emb, mask, labels)
+        prefix = model.mapping_network(emb)
+    assert rel(prefix, g["prefix"]) < 1e-4
+    assert abs(out.loss.item() - g["loss"][0]) < 3e-5
+    rows = torch.from_numpy(g["logit_rows"])
+    assert rel(out.logits[:2][:, rows], g["logits_sel"]) < 1e-4
+    lse = torch.logsumexp(out.logits.double(), -1).cpu().numpy()
+    assert np.abs(lse - g["lse"]).max() < 1e-4
+
+
+def test_medium_greedy_exact_f32(dev, medium_f32):
+    g = load("medium")
+    emb = torch.from_numpy(g["emb"]).to(dev)[: g["greedy"].shape[0]]
+    gen = medium_f32.generate(emb, max_length=g["greedy"].shape[1], temperature=0.0)
+    assert np.array_equal(gen.cpu().numpy(), g["greedy"])
+
+
+def test_medium_fused_train_f32(dev):
+    g = load("medium")
+    model = build(MED_G, MED_M, torch.float32, dev)
+    n = len(g["train_losses"])
+    losses, _ = _trainer_steps(model, inputs(g, dev), n)
+    assert rel(losses, g["train_losses"]) < 1e-5
+    for k, v in model.mapping_network.state_dict().items():
+        t = v.detach().double()
+        assert rel(torch.tensor([t.sum().item(), t.abs().sum().item()]), torch.tensor(g["trained_ck." + k][:2])) < 1e-4, k
+
+
+def test_medium_forward_bf16(dev):
+    """bf16 perf mode at configs[3]: loss |d| <= 5e-2, selected logits max-rel <= 6e-2, argmax agreement >= 85 %
+    (24 layers of bf16 rounding: looser than GPT-2 small's 3e-2 / 5e-2 / 90 %)."""
+    g = load("medium")
+    ids, mask, labels, emb = inputs(g, dev)
+    model = build(MED_G, MED_M, torch.bfloat16, dev).eval()
+    with torch.no_grad():
+        out = model(ids, emb, mask, labels)
+    assert abs(out.loss.item() - g["loss"][0]) < 5e-2
+    rows = torch.from_numpy(g["logit_rows"])
+    assert rel(out.logits[:2][:, rows], g["logits_sel"]) < 6e-2
+    assert (out.logits.argmax(-1).cpu().numpy() == g["argmax"]).mean() >= 0.85
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_clip_l14(dev, dtype):
+    g = load("clip_l14")
+    tower = CLIPVisionTower(CLIPVisionConfig.vit_l14())
+    tower.load_state_dict(O.clip_vision_state_dict(L14, 0))
+    tower = tower.to(dev)
+    px = torch.randn((2, 3, 224, 224), generator=torch.Generator().manual_seed(int(g["pixels_seed"][0]))).to(dev)
+    f = tower.get_image_features(px, compute_dtype=dtype)
+    e = tower.embed(px, compute_dtype=dtype)
+    if dtype == torch.float32:
+        assert rel(f, g["features"]) < 1e-4 and rel(e, g["embeddings"]) < 1e-4
+    else:
+        cos = torch.nn.functional.cosine_similarity(e.cpu().double(), torch.from_numpy(g["embeddings"]).double())
+        assert cos.min() > 0.99
+
+
+# ------------------------------------------------------------------------------------------------ ViT-B/16 (a16)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_vit_b16(dev, dtype):
+    """src/embeddings/vit.py:63-72 pooler_output (and its L2 normalisation) vs HF ViTModel."""
+    g = load("vit_b16")
+    tower = ViTImageTower.random_init(seed=0).to(dev)
+    px = torch.randn((2, 3, 224, 224), generator=torch.Generator().manual_seed(int(g["pixels_seed"][0]))).to(dev)
+    pooled = tower.pooler_output(px, compute_dtype=dtype)
+    e = tower.embed(px, compute_dtype=dtype)
+    if dtype == torch.float32:
+        assert rel(pooled, g["pooler"]) < 1e-4 and rel(e, g["embeddings"]) < 1e-4
+    else:
+        cos = torch.nn.functional.cosine_similarity(e.cpu().double(), torch.from_numpy(g["embeddings"]).double())
+        assert cos.min() > 0.995
+
+
+def test_vit_extract_directory_end_to_end(dev, tmp_path):
+    """extract_vit_embeddings (vit.py:80-137): decode in 2 workers, device tower, the reference's .pt format; rows
+    equal the single-image path in fp32 (same kernels, another batch size) to 1e-4."""
+    from PIL import Image
+
+    from icap.vit import ViTImageProcessor, extract_vit_embedding_from_image, extract_vit_embeddings
+
+    rng = np.random.default_rng(2)
+    for i in range(5):
+        Image.fromarray(rng.integers(0, 256, (200 + 10 * i, 260, 3), dtype=np.uint8)).save(tmp_path / f"img_{i}.png")
+    tower = ViTImageTower.random_init(seed=0).to(dev)
+    tower.embed = lambda px, compute_dtype=torch.float32, _e=tower.embed: _e(px, compute_dtype)  # fp32 for the check
+    out = tmp_path / "vit.pt"
+    extract_vit_embeddings(str(tmp_path), str(out), tower, ViTImageProcessor(), batch_size=2, num_workers=2)
+    d = torch.load(str(out), weights_only=True)
+    assert len(d["filenames"]) == 5 and d["embeddings"].shape == (5, 768)
+    for name, row in zip(d["filenames"], d["embeddings"]):
+        one = extract_vit_embedding_from_image(str(tmp_path / name), tower, ViTImageProcessor()).cpu()
+        assert rel(row, one) < 1e-4
+
+
+# ---------------------------------------------------------------------------- the benchmarked precision (bf16)
+
+
+def test_small_bf16_train_tracks_reference(dev):
+    """bf16 fused trainer vs the reference's fp32 train() over 3 AdamW steps at GPT-2 small (frozen):
+    loss |d| <= 3e-2 per step; the update direction (param - init) over all recorded tensors together has cosine
+    >= 0.85 with the reference's, and every single tensor >= 0.7 (AdamW normalises the step per element, so bf16
+    gradient noise flips the sign of elements whose true gradient is ~0: small bias vectors and the layers whose
+    gradient is smallest move least reliably -- r02 measured per-tensor cosines down to 0.74)."""
+    g = load("small_train")
+    model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
+    losses, _ = _trainer_steps(model, inputs(g, dev), 3)
+    d = np.abs(np.array(losses) - g["train_losses"])
+    assert d.max() < 3e-2, (losses, g["train_losses"])
+    init = O.mapper_state_dict(O.MapperCfg(), 0)
+    cosines, dg, dr = {}, [], []
+    for k, v in model.mapping_network.state_dict().items():
+        got = v.detach().cpu().double()
+        if "trained." + k in g:
+            ref, ini = torch.from_numpy(g["trained." + k]).double(), init[k].double()
+        elif "trained_sample." + k in g:
+            ref = torch.from_numpy(g["trained_sample." + k]).double()
+            got, ini = got.reshape(-1)[::97], init[k].double().reshape(-1)[::97]
+        else:
+            continue
+        cosines[k] = torch.nn.functional.cosine_similarity((got - ini).reshape(1, -1), (ref - ini).reshape(1, -1)).item()
+        dg.append((got - ini).reshape(-1))
+        dr.append((ref - ini).reshape(-1))
+    assert len(cosines) >= 10
+    whole = torch.nn.functional.cosine_similarity(torch.cat(dg)[None], torch.cat(dr)[None]).item()
+    print(f"bf16 update cosine: all tensors {whole:.4f}, min tensor {min(cosines.values()):.4f}")
+    assert whole >= 0.85, (whole, cosines)
+    assert min(cosines.values()) >= 0.7, cosines
+
+
+def test_small_bf16_greedy_agreement(dev):
+    """bf16 greedy decode vs the reference's fp32 greedy ids at the benchmarked decode shape (128 x 50): the first
+    token agrees for >= 90 % of captions and the first 5 for >= 70 % (random-init logits have top-1/top-2 margins
+    down to ~1e-2, inside bf16 noise; fp32 parity mode is token-exact: next test)."""
+    g = load("small_greedy128")
+    e = torch.randn((128, 512), generator=torch.Generator().manual_seed(int(g["emb_seed"][0])))
+    e = (e / e.norm(dim=-1, keepdim=True)).to(dev)
+    model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
+    gen = model.generate(e, max_length=50, temperature=0.0).cpu().numpy()
+    ref = g["greedy"]
+    assert gen.shape[0] == 128
+    first = (gen[:, 0] == ref[:, 0]).mean()
+    five = (gen[:, :5] == ref[:, :5]).all(1).mean()
+    print(f"bf16 greedy vs reference: first token {first:.3f}, first five {five:.3f}, "
+          f"whole caption {(gen[:, :ref.shape[1]] == ref[:, :gen.shape[1]]).all(1).mean():.3f}")
+    assert first >= 0.9 and five >= 0.7
+
+
+def test_small_greedy128_exact_f32(dev):
+    """fp32 parity mode: every one of the 128 captions x 50 tokens equals the reference's generate() ids."""
+    g = load("small_greedy128")
+    e = torch.randn((128, 512), generator=torch.Generator().manual_seed(int(g["emb_seed"][0])))
+    e = (e / e.norm(dim=-1, keepdim=True)).to(dev)
+    model = build(O.GPT2Cfg(), O.MapperCfg(), torch.float32, dev)
+    gen = model.generate(e, max_length=50, temperature=0.0).cpu().numpy()
+    ref = g["greedy"]
+    assert gen.shape == ref.shape, (gen.shape, ref.shape)
+    bad = np.nonzero((gen != ref).any(1))[0]
+    assert bad.size == 0, f"{bad.size} captions differ: {bad[:8]}"
+
+
+# ---------------------------------------------------------------------------------------------------- top-p (a14)
+
+
+def test_topp_kernel_keeps_reference_filter_set(dev):
+    """icap_topp_sample on the logits the reference filtered (src/models.py:400-449): over 300 seeds every draw lies
+    in the reference's kept set (its post-filter probs > 0), and the draw frequencies follow the reference's
+    post-filter distribution (chi-square over the kept tokens, p > 1e-4)."""
+    from scipy.stats import chisquare
+
+    g = load("topp_filter")
+    T, p = float(g["temperature"][0]), float(g["top_p"][0])
+    step = 0
+    logits = torch.from_numpy(g["logits"][step]).to(dev)
+    probs = g["probs"][step]
+    B = logits.shape[0]
+    out = torch.empty(B, dtype=torch.int64, device=dev)
+    draws = []
+    for seed in range(300):
+        ops.topp_sample(logits, logits.shape[1], T, p, None, seed, step, 511, out)
+        draws.append(out.cpu().numpy().copy())
+    draws = np.stack(draws)  # [seeds, B]
+    for b in range(B):
+        assert (probs[b][draws[:, b]] > 0).all(), b
+    counts = np.bincount(draws[:, 0], minlength=probs.shape[1])
+    kept = probs[0] > 0
+    exp = probs[0][kept] / probs[0][kept].sum() * draws.shape[0]
+    # pool the (many, small-probability) tokens into 8 probability-ordered bins for a valid chi-square
+    order = np.argsort(-probs[0][kept])
+    bins = np.array_split(order, 8)
+    obs_b = np.array([counts[kept][ix].sum() for ix in bins])
+    exp_b = np.array([exp[ix].sum() for ix in bins])
+    exp_b *= obs_b.sum() / exp_b.sum()  # chisquare wants equal totals to ~1e-8; the float sums differ by rounding
+    assert chisquare(obs_b, exp_b).pvalue > 1e-4

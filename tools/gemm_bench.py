@@ -1,7 +1,7 @@
 """GEMM microbenchmark over the shapes/epilogues of one training step (random bf16 operands; HIP-event timing).
 
-Usage: ICAP_GEMM_VARIANT=<n> [ICAP_LIB=path/to/other/libicap_hip.so] python tools/gemm_bench.py
-       (variant: see gemm_kernel in csrc/gemm.hip)
+Usage: [ICAP_LIB=path/to/other/libicap_hip.so] python tools/gemm_bench.py
+       (per shape: the automatic plan and the tile-kernel-only path, interleaved in one process)
 """
 
 import os
@@ -50,10 +50,11 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     reps = int(os.environ.get("REPS", "20"))
-    tot_ms = 0.0
+    tot_ms = tot_tile = 0.0
     for M, N, K, epi, cdt in SHAPES:
-        A = (torch.rand((M, K), generator=g) * 2 - 1).to(dev, torch.bfloat16)
-        B = (torch.rand((N, K), generator=g) * 2 - 1).to(dev, torch.bfloat16)
+        pad = int(os.environ.get("PAD", "0"))  # row padding (elements) of A and B: L2 channel-stride experiments
+        A = (torch.rand((M, K + pad), generator=g) * 2 - 1).to(dev, torch.bfloat16)[:, :K]
+        B = (torch.rand((N, K + pad), generator=g) * 2 - 1).to(dev, torch.bfloat16)[:, :K]
         C = torch.zeros((M, N), device=dev, dtype=cdt)
         kw = {}
         if epi == "gelu_aux":
@@ -70,19 +71,24 @@ def main():
             kw = dict(bias=torch.zeros(N, device=dev), resid=torch.empty_like(C))
         elif epi == "beta":
             kw = dict(beta=1.0)
-        for _ in range(3):
-            ops.gemm(A, B, C, **kw)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            ops.gemm(A, B, C, **kw)
-        e1.record()
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / reps
+        res = []
+        for tile in (False, True):  # automatic plan (ring kernel where eligible) vs the 128-row tile kernels
+            for _ in range(3):
+                ops.gemm(A, B, C, tile_only=tile, **kw)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                ops.gemm(A, B, C, tile_only=tile, **kw)
+            e1.record()
+            torch.cuda.synchronize()
+            res.append(e0.elapsed_time(e1) * 1e3 / reps)
+        us = res[0]
         tot_ms += us / 1e3
-        print(f"{M:6d}x{N:6d}x{K:6d} {epi:10s} {str(cdt)[6:]:9s} {us:9.1f} us {2 * M * N * K / us / 1e6:8.1f} TF/s",
-              flush=True)
-    print(f"variant {os.environ.get('ICAP_GEMM_VARIANT', 'default')}: sum {tot_ms:.3f} ms")
+        tot_tile += res[1] / 1e3
+        fl = 2 * M * N * K
+        print(f"{M:6d}x{N:6d}x{K:6d} {epi:10s} {str(cdt)[6:]:9s} auto {us:8.1f} us {fl / us / 1e6:7.1f} TF/s | "
+              f"tile {res[1]:8.1f} us {fl / res[1] / 1e6:7.1f} TF/s", flush=True)
+    print(f"sum: auto {tot_ms:.3f} ms, tile kernels {tot_tile:.3f} ms")
 
 
 if __name__ == "__main__":

@@ -9,7 +9,7 @@ outputs. Dropout is disabled (GPT2Config *_pdrop=0 and the mapper's dropout
 modules set to p=0) so outputs are deterministic. Only inputs + outputs are
 written: no reference source travels.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/make_goldens.py
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/make_goldens.py [tiny small clip vit clip_l14 topp small_train medium]
 """
 
 from __future__ import annotations
@@ -190,6 +190,149 @@ def golden_clip():
     print("clip", normed[0, :5])
 
 
+def vit_keys_to_installed(sd):
+    """transformers 4.57 ViT names (oracle.vit_state_dict; the reference's pin) -> the installed 5.x layout."""
+    out = {}
+    for k, v in sd.items():
+        n = k
+        if k.startswith("encoder.layer."):
+            i, rest = k[len("encoder.layer."):].split(".", 1)
+            rest = (rest.replace("attention.attention.query", "attention.q_proj")
+                    .replace("attention.attention.key", "attention.k_proj")
+                    .replace("attention.attention.value", "attention.v_proj")
+                    .replace("attention.output.dense", "attention.o_proj")
+                    .replace("intermediate.dense", "mlp.fc1").replace("output.dense", "mlp.fc2"))
+            n = f"layers.{i}.{rest}"
+        out[n] = v
+    return out
+
+
+def golden_vit_b16():
+    """ViT-B/16 pooler embedding (src/embeddings/vit.py:63-72): HF ViTModel(ViTConfig()) = google/vit-base-patch16-224
+    geometry, deterministic weights, 2 seeded images."""
+    from transformers import ViTConfig, ViTModel
+
+    cfg = O.ViTCfg()
+    hf = ViTModel(ViTConfig())
+    missing, unexpected = hf.load_state_dict(vit_keys_to_installed(O.vit_state_dict(cfg, 0)), strict=False)
+    assert not missing and not unexpected, (missing, unexpected)
+    hf.eval()
+    px = torch.randn((2, 3, 224, 224), generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        out = hf(pixel_values=px)
+        pooled = out.pooler_output
+        normed = pooled / pooled.norm(p=2, dim=-1, keepdim=True)  # vit.py:71
+    np.savez_compressed(os.path.join(OUT, "vit_b16.npz"), pixels_seed=np.array([4]), pooler=pooled.numpy(),
+                        embeddings=normed.numpy())
+    print("vit_b16", normed[0, :5])
+
+
+def golden_clip_l14():
+    """CLIP ViT-L/14 image features (BASELINE configs[3]: load_clip_model("openai/clip-vit-large-patch14"),
+    src/embeddings/clip.py:10-12): HF CLIPModel with that vision geometry, deterministic weights, 2 images."""
+    from transformers import CLIPConfig, CLIPModel
+
+    cfg = O.ClipCfg(hidden=1024, layers=24, heads=16, patch=14, image=224, inter=4096, proj=768)
+    hf = CLIPModel(CLIPConfig(vision_config=dict(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16,
+                                                 intermediate_size=4096, patch_size=14, image_size=224),
+                              projection_dim=768))
+    missing, unexpected = hf.load_state_dict(O.clip_vision_state_dict(cfg, seed=0), strict=False)
+    assert not unexpected
+    assert all(not k.startswith("vision_model.") and k != "visual_projection.weight" for k in missing)
+    hf.eval()
+    px = torch.randn((2, 3, 224, 224), generator=torch.Generator().manual_seed(5))
+    with torch.no_grad():
+        feats = hf.get_image_features(pixel_values=px)
+        feats = getattr(feats, "pooler_output", feats)
+        normed = feats / feats.norm(p=2, dim=-1, keepdim=True)
+    np.savez_compressed(os.path.join(OUT, "clip_l14.npz"), pixels_seed=np.array([5]), features=feats.numpy(),
+                        embeddings=normed.numpy())
+    print("clip_l14", normed[0, :5])
+
+
+def golden_topp():
+    """The reference's top-p filter (src/models.py:400-449) as the reference runs it: generate(temperature 0.8,
+    top_p 0.9) at the tiny config with torch.multinomial replaced by a recorder that returns the most probable kept
+    token (so the path is deterministic); records the filter's input logits (recomputed by the reference forward)
+    and its output distribution (probs > 0 = the kept set) for every step."""
+    import src.models as RM
+
+    gcfg = O.GPT2Cfg(n_layer=2, n_embd=128, n_head=2, vocab_size=512, n_positions=128, eos=511)
+    mcfg = O.MapperCfg(embed_dim=64, gpt_dim=128, prefix_length=5, hidden_length=4, num_layers=2)
+    model, _, _ = build_ref(gcfg, mcfg, 0)
+    model.eval()
+    _, _, _, emb = O.synthetic_batch(4, 12, 7, 512, 511, 64, seed=7)
+    probs_log, logits_log = [], []
+    real_softmax = torch.nn.functional.softmax
+
+    def multinomial(probs, num_samples=1):
+        probs_log.append(probs.detach().clone())
+        return probs.argmax(-1, keepdim=True)
+
+    orig_forward = model.gpt.forward
+
+    def forward(*a, **k):
+        out = orig_forward(*a, **k)
+        logits_log.append(out.logits[:, -1, :].detach().clone())
+        return out
+
+    model.gpt.forward = forward
+    with mock.patch.object(RM.torch, "multinomial", multinomial):
+        with torch.no_grad():
+            ids = model.generate(emb, max_length=6, temperature=0.8, top_p=0.9)
+    del real_softmax
+    np.savez_compressed(os.path.join(OUT, "topp_filter.npz"), emb=emb.numpy(), ids=ids.numpy(),
+                        logits=torch.stack(logits_log[: len(probs_log)]).numpy(),
+                        probs=torch.stack(probs_log).numpy(), temperature=np.array([0.8]), top_p=np.array([0.9]))
+    print("topp steps", len(probs_log), "kept per row", (torch.stack(probs_log) > 0).sum(-1)[0].tolist())
+
+
+def golden_small_train(workdir):
+    """GPT-2 small + transformer mapper: 3 frozen train() steps with the trained mapper tensors kept whole (bf16
+    update-direction tests), 2 unfrozen steps (every GPT-2 tensor's checksum), and greedy decode at the
+    benchmarked decode shape (128 captions x 50 tokens, the reference's full-recompute loop)."""
+    gcfg, mcfg = O.GPT2Cfg(), O.MapperCfg()
+    torch.manual_seed(0)
+    model, _, _ = build_ref(gcfg, mcfg, seed=0)
+    ids, mask, labels, emb = O.synthetic_batch(4, 50, 13, gcfg.vocab_size, gcfg.eos, mcfg.embed_dim, seed=1)
+    out = {"ids": ids.numpy(), "mask": mask.numpy(), "labels": labels.numpy(), "emb": emb.numpy()}
+    losses = run_ref_train(model, (ids, mask, labels, emb), 3, 1e-4, True, workdir)
+    out["train_losses"] = np.array(losses)
+    for k, v in model.mapping_network.state_dict().items():
+        out["trained_ck." + k] = checksum(v)
+        if not k.startswith("transformer.layers.") or k.startswith("transformer.layers.0."):
+            a = v.numpy()  # whole (small tensors) or every 97th element (matrices): a fixture of ~0.6 MB
+            if a.size > 20000:
+                out["trained_sample." + k] = a.reshape(-1)[::97].copy()
+            else:
+                out["trained." + k] = a
+    model2, _, _ = build_ref(gcfg, mcfg, seed=0)
+    losses2 = run_ref_train(model2, (ids, mask, labels, emb), 2, 1e-4, False, workdir)
+    out["unfrozen_losses"] = np.array(losses2)
+    for k, v in model2.state_dict().items():
+        if k != "gpt.lm_head.weight":
+            out["unfrozen_ck." + k] = checksum(v)
+    np.savez_compressed(os.path.join(OUT, "small_train.npz"), **out)
+    print("small_train", losses, losses2)
+    model3, _, _ = build_ref(gcfg, mcfg, seed=0)
+    model3.eval()
+    g = torch.Generator().manual_seed(5)
+    e = torch.randn((128, mcfg.embed_dim), generator=g)
+    e = e / e.norm(dim=-1, keepdim=True)
+    with torch.no_grad():
+        gen = model3.generate(e, max_length=50, temperature=0.0)
+    np.savez_compressed(os.path.join(OUT, "small_greedy128.npz"), emb_seed=np.array([5]), greedy=gen.numpy())
+    print("small_greedy128", tuple(gen.shape))
+
+
+def golden_medium(workdir):
+    """BASELINE configs[3] geometry: GPT-2 medium (24 layers, d 1024, 16 heads) + transformer mapper at gpt_dim 1024
+    (head dim 128) over 768-d CLIP-L/14 embeddings."""
+    golden_config("medium", O.GPT2Cfg(n_layer=24, n_embd=1024, n_head=16),
+                  O.MapperCfg(embed_dim=768, gpt_dim=1024), B=2, L=12, real=7, gen_B=2, gen_len=8,
+                  logit_rows=[14, 17, 26], train_steps=2, unfrozen_steps=0, workdir=workdir, full_logits=False)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     stub_modules()
@@ -200,12 +343,26 @@ def main():
     try:
         tiny_g = O.GPT2Cfg(n_layer=2, n_embd=128, n_head=2, vocab_size=512, n_positions=128, eos=511)
         tiny_m = O.MapperCfg(embed_dim=64, gpt_dim=128, prefix_length=5, hidden_length=4, num_layers=2)
-        golden_config("tiny", tiny_g, tiny_m, B=3, L=12, real=7, gen_B=3, gen_len=20, logit_rows=[4, 10, 16],
-                      train_steps=3, unfrozen_steps=2, workdir=work, full_logits=True)
-        golden_mlp(work)
-        golden_config("small", O.GPT2Cfg(), O.MapperCfg(), B=4, L=50, real=13, gen_B=2, gen_len=12,
-                      logit_rows=[14, 27, 64], train_steps=2, unfrozen_steps=0, workdir=work, full_logits=False)
-        golden_clip()
+        only = set(sys.argv[1:])  # optional subset: tiny small clip vit clip_l14 topp small_train medium
+        if not only or "tiny" in only:
+            golden_config("tiny", tiny_g, tiny_m, B=3, L=12, real=7, gen_B=3, gen_len=20, logit_rows=[4, 10, 16],
+                          train_steps=3, unfrozen_steps=2, workdir=work, full_logits=True)
+            golden_mlp(work)
+        if not only or "small" in only:
+            golden_config("small", O.GPT2Cfg(), O.MapperCfg(), B=4, L=50, real=13, gen_B=2, gen_len=12,
+                          logit_rows=[14, 27, 64], train_steps=2, unfrozen_steps=0, workdir=work, full_logits=False)
+        if not only or "clip" in only:
+            golden_clip()
+        if not only or "vit" in only:
+            golden_vit_b16()
+        if not only or "clip_l14" in only:
+            golden_clip_l14()
+        if not only or "topp" in only:
+            golden_topp()
+        if not only or "small_train" in only:
+            golden_small_train(work)
+        if not only or "medium" in only:
+            golden_medium(work)
     finally:
         os.chdir(cwd)
 
