@@ -252,6 +252,99 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(int B, int H, int hd, i
   }
 }
 
+// bf16, hd = 64 (every GPT-2 size): one wave per (b, h). The V rows of the first 8*TV keys go into registers
+// before any score is computed (they do not depend on the scores), so the K and V reads of a short cache share
+// one memory round trip; lane = key for the QK^T dots (8 x 16-byte loads per K row), lane = (key group kg = lane/8,
+// 16-byte column chunk dc = lane%8) for P.V, the 8 key groups summed with cross-lane adds at the end.
+template <int TV>
+__global__ __launch_bounds__(64) void attn_decode64_kernel(int B, int H, int pos, const bf16_t* __restrict__ cache,
+                                                          int64_t ld, bf16_t* __restrict__ out, int64_t ld_out,
+                                                          float scale) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* q = sm;         // 64
+  float* sc = sm + 64;   // pos + 1 scores
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - b * H;
+  const int D = H * 64;
+  const int lane = threadIdx.x, kg = lane >> 3, dc = lane & 7;
+  const int n = pos + 1;
+  const int64_t rs = (int64_t)B * ld;  // elements from one position's row to the next
+  const bf16_t* base = cache + (int64_t)b * ld + h * 64;
+  uint4 vr[TV];
+#pragma unroll
+  for (int t = 0; t < TV; ++t) {
+    const int j = kg + 8 * t;
+    vr[t] = j < n ? *reinterpret_cast<const uint4*>(base + j * rs + 2 * D + dc * 8) : make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (lane < 8) {
+    float v[8];
+    io<bf16_t>::ld8(base + (int64_t)pos * rs + lane * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[lane * 8 + e] = v[e] * scale;
+  }
+  __syncthreads();
+  float m = -INFINITY;
+  for (int j = lane; j < n; j += 64) {
+    const bf16_t* kr = base + j * rs + D;
+    uint4 kk[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) kk[c] = *reinterpret_cast<const uint4*>(kr + 8 * c);
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const uint32_t w[4] = {kk[c].x, kk[c].y, kk[c].z, kk[c].w};
+      const float4 q0 = *reinterpret_cast<const float4*>(q + 8 * c);
+      const float4 q1 = *reinterpret_cast<const float4*>(q + 8 * c + 4);
+      a0 = fmaf(q0.x, __uint_as_float(w[0] << 16), a0);
+      a1 = fmaf(q0.y, __uint_as_float(w[0] & 0xffff0000u), a1);
+      a0 = fmaf(q0.z, __uint_as_float(w[1] << 16), a0);
+      a1 = fmaf(q0.w, __uint_as_float(w[1] & 0xffff0000u), a1);
+      a0 = fmaf(q1.x, __uint_as_float(w[2] << 16), a0);
+      a1 = fmaf(q1.y, __uint_as_float(w[2] & 0xffff0000u), a1);
+      a0 = fmaf(q1.z, __uint_as_float(w[3] << 16), a0);
+      a1 = fmaf(q1.w, __uint_as_float(w[3] & 0xffff0000u), a1);
+    }
+    const float s = a0 + a1;
+    sc[j] = s;
+    m = fmaxf(m, s);
+  }
+  m = wave_max(m);
+  float l = 0.f;
+  for (int j = lane; j < n; j += 64) {
+    const float e = __expf(sc[j] - m);
+    sc[j] = e;
+    l += e;
+  }
+  l = wave_sum(l);
+  __syncthreads();
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto add_row = [&](const uint4 v, float p) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc[2 * e] = fmaf(p, __uint_as_float(w[e] << 16), acc[2 * e]);
+      acc[2 * e + 1] = fmaf(p, __uint_as_float(w[e] & 0xffff0000u), acc[2 * e + 1]);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < TV; ++t) {
+    const int j = kg + 8 * t;
+    if (j < n) add_row(vr[t], sc[j]);
+  }
+  for (int j = 8 * TV + kg; j < n; j += 8)  // keys past the prefetched ones (caches longer than 8*TV)
+    add_row(*reinterpret_cast<const uint4*>(base + j * rs + 2 * D + dc * 8), sc[j]);
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += __shfl_xor(acc[e], o, 64);
+  if (kg == 0) {
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    io<bf16_t>::st8(out + (int64_t)b * ld_out + h * 64 + dc * 8, acc);
+  }
+}
+
 // bf16 MFMA kernels (attention_mfma.hip); the fp32 parity mode and shapes they do not cover use the
 // LDS/VALU kernels of this file. ICAP_ATTN_VALU=1 forces the VALU kernels (A/B testing).
 bool mfma_attention_ok(const icap_attn_args* a, bool bwd);
@@ -351,9 +444,16 @@ extern "C" int icap_attention_decode(int32_t dtype, int32_t B, int32_t H, int32_
   ICAP_REQUIRE(pos >= 0 && pos < 4096, "icap_attention_decode: pos out of range");
   ICAP_REQUIRE(cache && out, "icap_attention_decode: null pointer");
   if (B == 0) return ICAP_OK;
-  const size_t lds = sizeof(float) * (128 + (size_t)pos + 1);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   dim3 grid((unsigned)(B * H)), block(64);
+  const bool al = ((reinterpret_cast<uintptr_t>(cache) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+  if (dtype == ICAP_BF16 && hd == 64 && al && ld_cache % 8 == 0 && ld_out % 8 == 0) {
+    const size_t lds = sizeof(float) * (64 + (size_t)pos + 1);
+    hipLaunchKernelGGL(attn_decode64_kernel<16>, grid, block, lds, s, B, H, pos, (const bf16_t*)cache, ld_cache,
+                       (bf16_t*)out, ld_out, scale);
+    return check_launch("icap_attention_decode");
+  }
+  const size_t lds = sizeof(float) * (128 + (size_t)pos + 1);
   if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(attn_decode_kernel<bf16_t>, grid, block, lds, s, B, H, hd, pos, (const bf16_t*)cache, ld_cache,
                        (bf16_t*)out, ld_out, scale);

@@ -566,7 +566,51 @@ __global__ __launch_bounds__(1024) void greedy_next_kernel(int64_t V, const T* _
     if (argmax_better(v, j, best, bi)) { best = v; bi = j; }
   };
   int64_t j0 = 0;
-  if (vec) {
+  if constexpr (sizeof(T) == 2) {
+    if (vec == 2) {
+      // 16-byte loads, eight per thread in flight at once (a 50,304-logit row is one pass). Each thread visits its
+      // logits in increasing index order, so a strict `>` keeps its first maximum (3 VALU ops per logit instead
+      // of the NaN-aware 64-bit compare); a NaN anywhere in the row sends the block to the exact loop below.
+      const int64_t V8 = V >> 3;
+      float fb = -INFINITY;
+      int fi = (int)V;
+      bool nan = false;
+      for (int64_t q0 = threadIdx.x; q0 < V8; q0 += 8 * NT) {
+        uint4 w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int64_t q = q0 + (int64_t)u * NT;
+          w[u] = q < V8 ? *reinterpret_cast<const uint4*>(row + 8 * q) : make_uint4(0xff80ff80u, 0xff80ff80u,
+                                                                                  0xff80ff80u, 0xff80ff80u);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int jb = (int)(8 * (q0 + (int64_t)u * NT));
+          const uint32_t h[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v0 = __uint_as_float(h[e] << 16), v1 = __uint_as_float(h[e] & 0xffff0000u);
+            nan |= (v0 != v0) | (v1 != v1);
+            if (v0 > fb) { fb = v0; fi = jb + 2 * e; }
+            if (v1 > fb) { fb = v1; fi = jb + 2 * e + 1; }
+          }
+        }
+      }
+      if (__syncthreads_or(nan)) {
+        for (int64_t q = threadIdx.x; q < V8; q += NT) {
+          float v[8];
+          io<T>::ld8(row + 8 * q, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) consider(v[e], 8 * q + e);
+        }
+      } else {
+        best = fb;
+        bi = fi < V ? fi : V;
+      }
+      j0 = V8 << 3;
+    }
+  }
+  if (vec == 1) {
     const int64_t V4 = V >> 2;
 #pragma unroll 4
     for (int64_t q = threadIdx.x; q < V4; q += NT) {
@@ -1068,7 +1112,8 @@ extern "C" int icap_greedy_next(int32_t dtype, int32_t B, int64_t V, const void*
   ICAP_REQUIRE(x == nullptr || (wte && wpe), "icap_greedy_next: x requires wte/wpe");
   if (B == 0) return ICAP_OK;
   const int es = dtype == ICAP_BF16 ? 2 : 4;
-  const int vec = (ld % 4 == 0) && (reinterpret_cast<uintptr_t>(logits) % (4 * es) == 0);
+  const uintptr_t lp = reinterpret_cast<uintptr_t>(logits);
+  const int vec = (es == 2 && ld % 8 == 0 && lp % 16 == 0) ? 2 : (ld % 4 == 0 && lp % (4 * es) == 0) ? 1 : 0;
   DISPATCH_T(dtype, hipLaunchKernelGGL(greedy_next_kernel<T>, dim3((unsigned)B), dim3(1024), 0, S_(stream), V,
                                        CTP(logits), ld, eos, forced, finished, tokens, ld_tokens, step, CTP(wte), CTP(wpe),
                                        pos, D, TP(x), vec));

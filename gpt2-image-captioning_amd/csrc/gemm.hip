@@ -618,7 +618,12 @@ __device__ __forceinline__ uint4 ln_chunk<float>(const uint4 a, float mean, floa
 }
 
 constexpr int SK_WAVES = 8;
-template <typename TI, typename TC, int NT, int MT>
+constexpr int SK_LNK = 1280;  // LN-fused launches up to this K stage gamma / beta in LDS
+// NT: 16-column slabs per block (the host picks the fewest that fit the grid in one pass over the CUs);
+// SKU: k-steps in flight per wave (the host picks enough for one memory round trip over all of K where the
+// registers allow). Neither changes the arithmetic: every wave accumulates its steps in step order and the waves
+// are summed in a fixed order, so all (NT, SKU) instantiations store bitwise-identical outputs.
+template <typename TI, typename TC, int NT, int MT, int SKU>
 __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_args p, uint32_t drop_thresh,
                                                                   float inv_keep) {
   constexpr int ES = sizeof(TI);
@@ -628,8 +633,10 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   constexpr int RLD = BN + 4;         // fp32 stride of the LDS partial tiles
   constexpr int HALF = SK_WAVES / 2;
   constexpr int BM = 16 * MT;
-  constexpr int SK_U = 16 / (MT + NT) < 2 ? 2 : 16 / (MT + NT);  // k-steps in flight per wave
+  constexpr int QPR = BN / 4;         // 4-column epilogue quads per row
+  static_assert(BM * QPR <= 64 * SK_WAVES, "one epilogue quad per thread");
   __shared__ __attribute__((aligned(16))) float red[HALF][BM * RLD];
+  __shared__ __attribute__((aligned(16))) float lngb[2 * SK_LNK];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int64_t N = p.N, K = p.K;
@@ -647,12 +654,143 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   for (int i = 0; i < MT; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  // LayerNorm-fused A (icap_gemm_args.ln_gamma): mean / rstd of the block's rows over all K, 16 threads per row,
-  // two passes (the formula and rounding of ln_fwd8_kernel: (x - mean) * rstd * gamma + beta -> input dtype)
-  // (computed after the first k-steps' operand loads are issued, so their latency overlaps it)
-  __shared__ float ln_mr[BM][2];
+  // rows past M / N lie beyond the descriptor range (zero-filled); K-tail chunks and steps past the end are
+  // redirected out of range (zero fragments: the MFMAs on them add nothing)
+  uint32_t aoff[MT], boff[NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) aoff[i] = (uint32_t)(((i * 16 + fr) * p.lda + fg * EPC) * ES);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) boff[j] = (uint32_t)(((j * 16 + fr) * p.ldb + fg * EPC) * ES);
+  const int64_t nks = (K + KSTEP - 1) / KSTEP;
+  uint4 af[SKU][MT], bfr[SKU][NT];
+  auto load_steps = [&](int64_t base) {  // steps past the end load zero fragments (the MFMAs add nothing)
+#pragma unroll
+    for (int u = 0; u < SKU; ++u) {
+      const int64_t k0 = (base + (int64_t)u * SK_WAVES) * KSTEP;
+      const bool kin = k0 + fg * EPC < K;
+      const uint32_t kb = (uint32_t)(k0 * ES);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bfr[u][j] = bload(rb, kin ? boff[j] + kb : OOB);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[u][i] = bload(ra, kin ? aoff[i] + kb : OOB);
+    }
+  };
+  // LN gamma / beta (K <= SK_LNK) are loaded first, so storing them to LDS waits for these loads only, not for
+  // the fragment loads behind them
   const bool fuse_ln = p.ln_gamma != nullptr;
-  auto ln_stats = [&]() {
+  const bool ln_lds = fuse_ln && K <= SK_LNK;
+  constexpr int LNS = (SK_LNK + 64 * SK_WAVES - 1) / (64 * SK_WAVES);  // gamma (and beta) values per thread
+  float lg[LNS], lb[LNS];
+  if (ln_lds) {
+#pragma unroll
+    for (int q = 0; q < LNS; ++q) {
+      const int k = threadIdx.x + q * 64 * SK_WAVES;
+      lg[q] = k < K ? p.ln_gamma[k] : 0.f;
+      lb[q] = k < K ? p.ln_beta[k] : 0.f;
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // every wave runs at least one (possibly all-zero) pass, so the LN-stats barrier below is block-uniform
+  load_steps(wave);
+  __builtin_amdgcn_sched_barrier(0);
+  if (ln_lds) {
+#pragma unroll
+    for (int q = 0; q < LNS; ++q) {
+      const int k = threadIdx.x + q * 64 * SK_WAVES;
+      if (k < K) {
+        lngb[k] = lg[q];
+        lngb[SK_LNK + k] = lb[q];
+      }
+    }
+  }
+
+  // Epilogue operands, fetched now so their latency hides under the main loop's: one 4-column quad per thread
+  // (bias; the bf16 residual, or dact_src in the backward form, for full quads).
+  const int er = threadIdx.x / QPR, ec = (threadIdx.x - er * QPR) * 4;
+  const int64_t erow = m0 + er, ecol = n0 + ec;
+  const bool eact = threadIdx.x < BM * QPR && erow < M && ecol < N;
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  uint2 pre = make_uint2(0u, 0u);
+  bool use_pre = false;
+  if (eact) {
+    if (p.bias && p.dact == ICAP_ACT_NONE) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bias4[e] = (ecol + e < N) ? p.bias[ecol + e] : 0.f;
+    }
+    if constexpr (sizeof(TC) == 2) {
+      const bf16_t* src = reinterpret_cast<const bf16_t*>(p.dact != ICAP_ACT_NONE ? p.dact_src : p.resid);
+      const int64_t lds_ = p.dact != ICAP_ACT_NONE ? p.ld_dact : p.ldr;
+      if (src && ecol + 4 <= N && (lds_ & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 7) == 0) {
+        pre = *reinterpret_cast<const uint2*>(src + erow * lds_ + ecol);
+        use_pre = true;
+      }
+    }
+  }
+
+  // LayerNorm-fused A (icap_gemm_args.ln_gamma): mean / rstd of the block's rows over all K (two passes: mean,
+  // then the centred sum of squares), then (x - mean) * rstd * gamma + beta -> input dtype per fragment.
+  // bf16 with every k-step in registers (nks <= 8 SKU, the decode launches): the statistics come from the
+  // fragments themselves (lane sums -> the 4 lane groups -> the 8 waves through LDS, fixed order), so LN costs no
+  // extra global reads; otherwise the loop form (16 threads per row, the order and rounding of ln_fwd8_kernel).
+  // gamma / beta are staged in LDS when K <= SK_LNK (above); the barriers below publish them.
+  __shared__ float ln_mr[BM][2];
+  __shared__ float lnp[SK_WAVES][BM];
+  // (instantiations with few fragment registers only: the others would spill; LN-fused launches have K = D)
+  constexpr bool LN_FRAG = ES == 2 && SKU * (MT + NT) <= 24;
+  const bool ln_frag = LN_FRAG && fuse_ln && nks <= (int64_t)SK_WAVES * SKU;
+  float ln_mean[MT], ln_rs[MT];
+  if (LN_FRAG && ln_frag) {
+    auto chunk_in = [&](int u) { return (int64_t)(wave + u * SK_WAVES) * KSTEP + fg * EPC < K; };
+    auto reduce_rows = [&](float part[MT], float out[MT]) {  // lane partials -> row totals (every lane of the row)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        part[i] += __shfl_xor(part[i], 16, 64);
+        part[i] += __shfl_xor(part[i], 32, 64);
+        if (fg == 0) lnp[wave][i * 16 + fr] = part[i];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < SK_WAVES; ++w) t += lnp[w][i * 16 + fr];
+        out[i] = t;
+      }
+      __syncthreads();
+    };
+    float part[MT], tot[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      part[i] = 0.f;
+#pragma unroll
+      for (int u = 0; u < SKU; ++u) {
+        if (chunk_in(u)) {
+          float v[8];
+          unpack_bf16(af[u][i], v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) part[i] += v[e];
+        }
+      }
+    }
+    reduce_rows(part, tot);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      ln_mean[i] = tot[i] / (float)K;
+      part[i] = 0.f;
+#pragma unroll
+      for (int u = 0; u < SKU; ++u) {
+        if (chunk_in(u)) {
+          float v[8];
+          unpack_bf16(af[u][i], v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) part[i] += (v[e] - ln_mean[i]) * (v[e] - ln_mean[i]);
+        }
+      }
+    }
+    reduce_rows(part, tot);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) ln_rs[i] = 1.f / sqrtf(tot[i] / (float)K + p.ln_eps);
+  } else if (fuse_ln) {
     const int t = threadIdx.x & 15;
     for (int rr = threadIdx.x >> 4; rr < BM; rr += 64 * SK_WAVES / 16) {
       const int64_t row = m0 + rr < M ? m0 + rr : M - 1;
@@ -682,58 +820,47 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
       }
     }
     __syncthreads();
-  };
-  // rows past M / N lie beyond the descriptor range (zero-filled); K-tail chunks and steps past the end are
-  // redirected out of range (zero fragments: the MFMAs on them add nothing)
-  uint32_t aoff[MT], boff[NT];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) aoff[i] = (uint32_t)(((i * 16 + fr) * p.lda + fg * EPC) * ES);
-#pragma unroll
-  for (int j = 0; j < NT; ++j) boff[j] = (uint32_t)(((j * 16 + fr) * p.ldb + fg * EPC) * ES);
-  const int64_t nks = (K + KSTEP - 1) / KSTEP;
-  uint4 af[SK_U][MT], bfr[SK_U][NT];
-  auto load_steps = [&](int64_t base) {  // steps past the end load zero fragments (the MFMAs add nothing)
-#pragma unroll
-    for (int u = 0; u < SK_U; ++u) {
-      const int64_t k0 = (base + (int64_t)u * SK_WAVES) * KSTEP;
-      const bool kin = k0 + fg * EPC < K;
-      const uint32_t kb = (uint32_t)(k0 * ES);
-#pragma unroll
-      for (int j = 0; j < NT; ++j) bfr[u][j] = bload(rb, kin ? boff[j] + kb : OOB);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) af[u][i] = bload(ra, kin ? aoff[i] + kb : OOB);
+    for (int i = 0; i < MT; ++i) {
+      ln_mean[i] = ln_mr[i * 16 + fr][0];
+      ln_rs[i] = ln_mr[i * 16 + fr][1];
     }
-  };
-  // every wave runs at least one (possibly all-zero) pass, so the LN-stats barrier below is block-uniform
-  load_steps(wave);
-  if (fuse_ln) ln_stats();
+  }
   for (int64_t base = wave;;) {
-    // all SK_U steps' loads are issued before the first MFMA waits (without this fence hipcc sinks each load
+    // all SKU steps' loads are issued before the first MFMA waits (without this fence hipcc sinks each load
     // to its use and every MFMA waits out a full memory latency)
     __builtin_amdgcn_sched_barrier(0);
     if (fuse_ln) {
 #pragma unroll
-      for (int u = 0; u < SK_U; ++u) {
+      for (int u = 0; u < SKU; ++u) {
         const int64_t k0 = (base + (int64_t)u * SK_WAVES) * KSTEP + fg * EPC;
         if (k0 < K) {  // K-tail / past-the-end chunks stay zero
           float g[EPC], bt[EPC];
-          if constexpr (EPC == 8) { io<float>::ld8(p.ln_gamma + k0, g); io<float>::ld8(p.ln_beta + k0, bt); }
-          else { io<float>::ld4(p.ln_gamma + k0, g); io<float>::ld4(p.ln_beta + k0, bt); }
+          if (ln_lds) {
 #pragma unroll
-          for (int i = 0; i < MT; ++i) {
-            const float mean = ln_mr[i * 16 + fr][0], rs = ln_mr[i * 16 + fr][1];
-            af[u][i] = ln_chunk<TI>(af[u][i], mean, rs, g, bt);
+            for (int e = 0; e < EPC; e += 4) {
+              const float4 gv = *reinterpret_cast<const float4*>(&lngb[k0 + e]);
+              const float4 bv = *reinterpret_cast<const float4*>(&lngb[SK_LNK + k0 + e]);
+              g[e] = gv.x; g[e + 1] = gv.y; g[e + 2] = gv.z; g[e + 3] = gv.w;
+              bt[e] = bv.x; bt[e + 1] = bv.y; bt[e + 2] = bv.z; bt[e + 3] = bv.w;
+            }
+          } else if constexpr (EPC == 8) {
+            io<float>::ld8(p.ln_gamma + k0, g); io<float>::ld8(p.ln_beta + k0, bt);
+          } else {
+            io<float>::ld4(p.ln_gamma + k0, g); io<float>::ld4(p.ln_beta + k0, bt);
           }
+#pragma unroll
+          for (int i = 0; i < MT; ++i) af[u][i] = ln_chunk<TI>(af[u][i], ln_mean[i], ln_rs[i], g, bt);
         }
       }
     }
 #pragma unroll
-    for (int u = 0; u < SK_U; ++u)
+    for (int u = 0; u < SKU; ++u)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < NT; ++j) mfma_chunk<TI>(acc[i][j], af[u][i], bfr[u][j]);
-    base += SK_WAVES * SK_U;
+    base += SK_WAVES * SKU;
     if (base >= nks) break;
     load_steps(base);
   }
@@ -759,26 +886,18 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
     park(red[wave]);  // same addresses this lane just read: no cross-lane hazard
   }
   __syncthreads();
+  if (!eact) return;
   const uint64_t seed = drop_thresh != 0u ? eff_seed(p.seed, p.seed_ptr) : 0ull;
-  constexpr int QPR = BN / 4;  // 4-column quads per row
-  for (int qd = threadIdx.x; qd < BM * QPR; qd += 64 * SK_WAVES) {
-    const int r = qd / QPR, c = (qd - r * QPR) * 4;
-    const int64_t row = m0 + r, col = n0 + c;
-    if (row >= M || col >= N) continue;
-    float x[4];
-    *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(&red[0][r * RLD + c]);
+  float x[4];
+  *reinterpret_cast<float4*>(x) = *reinterpret_cast<const float4*>(&red[0][er * RLD + ec]);
 #pragma unroll
-    for (int w = 1; w < HALF; ++w) {
-      const float4 v = *reinterpret_cast<const float4*>(&red[w][r * RLD + c]);
-      x[0] += v.x; x[1] += v.y; x[2] += v.z; x[3] += v.w;
-    }
-    float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias && p.dact == ICAP_ACT_NONE) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bias4[e] = (col + e < N) ? p.bias[col + e] : 0.f;
-    }
-    epi4<TC>(p, row, col, x, bias4, col + 4 <= N, seed, drop_thresh, inv_keep);
+  for (int w = 1; w < HALF; ++w) {
+    const float4 v = *reinterpret_cast<const float4*>(&red[w][er * RLD + ec]);
+    x[0] += v.x; x[1] += v.y; x[2] += v.z; x[3] += v.w;
   }
+  // two call sites rather than a selected pointer (a pointer select on a local puts it in scratch)
+  if (use_pre) epiw<TC, 4>(p, erow, ecol, x, bias4, ecol + 4 <= N, seed, drop_thresh, inv_keep, &pre);
+  else epiw<TC, 4>(p, erow, ecol, x, bias4, ecol + 4 <= N, seed, drop_thresh, inv_keep);
 }
 
 // Split-K reduction: sum the fp32 partial slabs of `splits` K-ranges in a fixed order (deterministic) and
@@ -1199,6 +1318,7 @@ namespace {
 struct GemmPlan {
   bool skinny = false;
   int nt = 1;            // skinny: 16-column slabs per block
+  int sku = 3;           // skinny: k-steps in flight per wave
   int ring = 0;          // ring kernel: WM (4 = 256 x 128 tiles, 2 = 128 x 128), 0 = not used
   int variant = 0;       // tile kernel (see ICAP_GEMM_LAUNCH)
   int splits = 1, nk_split = 0, tiles_n = 0, tiles_m = 0, units = 0;
@@ -1261,8 +1381,21 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
                "icap_gemm: ln_gamma needs ln_beta, M <= 128, K <= 4096, no split_k / trans_ab");
   if (p.M <= 128 && p.split_k == 0 && (tiles <= 128 || fuse_ln) && !p.trans_ab) {
     pl.skinny = true;
-    pl.nt = p.N > 1536 ? 2 : 1;  // 32-column slabs once there are enough of them
-    pl.grid = dim3((unsigned)((p.N + 16 * pl.nt - 1) / (16 * pl.nt)), (unsigned)((p.M + 31) / 32));
+    // the fewest 16-column slabs per block that keep the grid within one pass over the CUs (every CU streams one
+    // block's A rows + W slab; a second block on a CU doubles its bytes), then enough k-steps in flight per wave
+    // to cover K in one round trip where the fragment registers allow (SKU in {3, 4, 6}; 12 for one-slab blocks)
+    const int64_t gy = (p.M + 31) / 32;
+    const int cus = device_cus();
+    pl.nt = 4;
+    for (int nt = 1; nt <= 4; ++nt)
+      if ((p.N + 16 * nt - 1) / (16 * nt) * gy <= cus) { pl.nt = nt; break; }
+    if (p.in_dtype == ICAP_BF16) {
+      const int64_t need = ((p.K + 31) / 32 + SK_WAVES - 1) / SK_WAVES;
+      pl.sku = need <= 3 ? 3 : need <= 4 ? 4 : (need <= 6 || pl.nt > 1) ? 6 : 12;
+    } else {
+      pl.sku = 6;
+    }
+    pl.grid = dim3((unsigned)((p.N + 16 * pl.nt - 1) / (16 * pl.nt)), (unsigned)gy);
     pl.block = dim3(64 * SK_WAVES);
     return ICAP_OK;
   }
@@ -1347,7 +1480,7 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
   const char* ti = a->in_dtype == ICAP_BF16 ? "unsigned short" : "float";
   const char* tc = a->c_dtype == ICAP_BF16 ? "unsigned short" : "float";
   char fmt[96];
-  if (pl.skinny) snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2>", pl.nt);
+  if (pl.skinny) snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2, %d>", pl.nt, pl.sku);
   else if (pl.ring) snprintf(fmt, sizeof fmt, "gemm_ring_kernel<%d, %d>", pl.ring, pl.ring == 4 ? 3 : 4);
   else snprintf(fmt, sizeof fmt, "%s", variant_kernel(pl.variant));
   char inner[128];
@@ -1369,15 +1502,38 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const float inv_keep = pl.inv_keep;
   if (pl.skinny) {
     const dim3 sgrid = pl.grid, sblock = pl.block;
-#define ICAP_SKINNY(TI, TC)                                                                                   \
-  if (pl.nt == 2) hipLaunchKernelGGL((gemm_skinny_kernel<TI, TC, 2, 2>), sgrid, sblock, 0, s, p, thr, inv_keep); \
-  else hipLaunchKernelGGL((gemm_skinny_kernel<TI, TC, 1, 2>), sgrid, sblock, 0, s, p, thr, inv_keep);
+#define ICAP_SK(TI, TC, NT, U) hipLaunchKernelGGL((gemm_skinny_kernel<TI, TC, NT, 2, U>), sgrid, sblock, 0, s, p, thr, inv_keep)
+#define ICAP_SKINNY_BF(TC)                                                                 \
+  switch (pl.nt * 100 + pl.sku) {                                                          \
+    case 103: ICAP_SK(bf16_t, TC, 1, 3); break;                                            \
+    case 104: ICAP_SK(bf16_t, TC, 1, 4); break;                                            \
+    case 106: ICAP_SK(bf16_t, TC, 1, 6); break;                                            \
+    case 112: ICAP_SK(bf16_t, TC, 1, 12); break;                                           \
+    case 203: ICAP_SK(bf16_t, TC, 2, 3); break;                                            \
+    case 204: ICAP_SK(bf16_t, TC, 2, 4); break;                                            \
+    case 206: ICAP_SK(bf16_t, TC, 2, 6); break;                                            \
+    case 303: ICAP_SK(bf16_t, TC, 3, 3); break;                                            \
+    case 304: ICAP_SK(bf16_t, TC, 3, 4); break;                                            \
+    case 306: ICAP_SK(bf16_t, TC, 3, 6); break;                                            \
+    case 403: ICAP_SK(bf16_t, TC, 4, 3); break;                                            \
+    case 404: ICAP_SK(bf16_t, TC, 4, 4); break;                                            \
+    default: ICAP_SK(bf16_t, TC, 4, 6); break;                                             \
+  }
+#define ICAP_SKINNY_F32(TC)                                                                \
+  switch (pl.nt) {                                                                         \
+    case 1: ICAP_SK(float, TC, 1, 6); break;                                               \
+    case 2: ICAP_SK(float, TC, 2, 6); break;                                               \
+    case 3: ICAP_SK(float, TC, 3, 6); break;                                               \
+    default: ICAP_SK(float, TC, 4, 6); break;                                              \
+  }
     if (p.in_dtype == ICAP_BF16) {
-      if (p.c_dtype == ICAP_BF16) { ICAP_SKINNY(bf16_t, bf16_t) } else { ICAP_SKINNY(bf16_t, float) }
+      if (p.c_dtype == ICAP_BF16) { ICAP_SKINNY_BF(bf16_t) } else { ICAP_SKINNY_BF(float) }
     } else {
-      if (p.c_dtype == ICAP_BF16) { ICAP_SKINNY(float, bf16_t) } else { ICAP_SKINNY(float, float) }
+      if (p.c_dtype == ICAP_BF16) { ICAP_SKINNY_F32(bf16_t) } else { ICAP_SKINNY_F32(float) }
     }
-#undef ICAP_SKINNY
+#undef ICAP_SKINNY_BF
+#undef ICAP_SKINNY_F32
+#undef ICAP_SK
     return check_launch("icap_gemm(skinny)");
   }
   if (pl.ring) {

@@ -93,7 +93,10 @@ def test_gemm_kernel_name_query_without_gpu():
         tile = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 50304, 768, path=path))).decode()
         assert tile.startswith("icap::gemm_kernel<") and "unsigned short, unsigned short" in tile
     skinny = lib.icap_gemm_kernel_name(C.byref(_gemm_args(128, 2304, 768))).decode()
-    assert skinny.startswith("icap::gemm_skinny_kernel<unsigned short, unsigned short, 2")
+    # 2304 columns over 4 row blocks: 3 slabs per block (192 blocks <= 256 CUs), K = 768 in 3 k-steps per wave
+    assert skinny == "icap::gemm_skinny_kernel<unsigned short, unsigned short, 3, 2, 3>", skinny
+    mp = lib.icap_gemm_kernel_name(C.byref(_gemm_args(128, 768, 3072))).decode()
+    assert mp == "icap::gemm_skinny_kernel<unsigned short, unsigned short, 1, 2, 12>", mp
     f32 = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 768, 768, c_dtype=_lib.F32))).decode()
     assert "unsigned short, float" in f32
     assert lib.icap_gemm_kernel_name(C.byref(_gemm_args(8, 8, 3))) is None  # invalid K
