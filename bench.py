@@ -125,9 +125,52 @@ def cpu_baseline(seconds_budget: float = 20.0):
         el = time.perf_counter() - t0
         if el > seconds_budget or n >= 20:
             break
-    return {"value": round(n * B / el, 3), "unit": "images/s", "cores": cores, "kind": "port",
-            "sample": f"{n} oracle train steps x batch {B} (CLIP-B/32 fwd on 224^2 pixels + mapper + GPT-2 small "
-                      f"fwd/bwd + AdamW, dropout 0.1, fp32, torch CPU {cores} threads) in {el:.1f}s"}
+    res = {"value": round(n * B / el, 3), "unit": "images/s", "cores": cores, "kind": "port",
+           "sample": f"{n} oracle train steps x batch {B} (CLIP-B/32 fwd on 224^2 pixels + mapper + GPT-2 small "
+                     f"fwd/bwd + AdamW, dropout 0.1, fp32, torch CPU {cores} threads) in {el:.1f}s"}
+    res["more"] = cpu_baseline_more(gsd, msd, csd, cores)
+    return res
+
+
+def cpu_baseline_more(gsd, msd, csd, cores):
+    """The other CPU rows of BASELINE.md §3 on bounded samples: the headline batch (128) frozen, GPT-2 unfrozen
+    (batch 8), and greedy captions/s of the reference's decode loop (full recompute each token, no KV cache:
+    src/models.py:389-469) over 50 fixed steps."""
+    from oracle import icap_oracle as O
+
+    out = {}
+    ids, mask, labels, _ = O.synthetic_batch(128, 50, 13, seed=1)
+    px = torch.randn((128, 3, 224, 224), generator=torch.Generator().manual_seed(2))
+    t0 = time.perf_counter()
+    O.train_steps(gsd, O.GPT2Cfg(), msd, O.MapperCfg(), [(ids, mask, labels, px)], total_steps=100, p_drop=0.1,
+                  clip=(csd, O.ClipCfg()))
+    el = time.perf_counter() - t0
+    out["train_b128_frozen"] = {"value": round(128 / el, 3), "unit": "images/s",
+                                "sample": f"1 oracle train step x batch 128 (as the headline, incl. CLIP fwd) in {el:.1f}s"}
+    ids, mask, labels, _ = O.synthetic_batch(8, 50, 13, seed=1)
+    emb = torch.randn((8, 512), generator=torch.Generator().manual_seed(3))
+    b8 = (ids, mask, labels, emb / emb.norm(dim=-1, keepdim=True))
+    O.train_steps(gsd, O.GPT2Cfg(), msd, O.MapperCfg(), [b8], total_steps=100, p_drop=0.1, freeze_gpt=False)
+    t0 = time.perf_counter()
+    O.train_steps(gsd, O.GPT2Cfg(), msd, O.MapperCfg(), [b8, b8], total_steps=100, p_drop=0.1, freeze_gpt=False)
+    el = time.perf_counter() - t0
+    out["train_b8_unfrozen"] = {"value": round(16 / el, 3), "unit": "images/s",
+                                "sample": f"2 oracle train steps x batch 8, GPT-2 unfrozen (AdamW over 124M+ params), "
+                                          f"precomputed embeddings, in {el:.1f}s"}
+    Bg = 4
+    emb = torch.randn((Bg, 512), generator=torch.Generator().manual_seed(5))
+    with torch.no_grad():
+        cur = O.mapper_forward(msd, O.MapperCfg(), emb / emb.norm(dim=-1, keepdim=True))
+        t0 = time.perf_counter()
+        for _ in range(50):  # the reference loop, all 50 steps (no early exit: the GPU figure decodes 50 too)
+            _, logits = O.gpt2_forward(gsd, O.GPT2Cfg(), cur)
+            nxt = torch.argmax(logits[:, -1, :], dim=-1)
+            cur = torch.cat((cur, gsd["transformer.wte.weight"][nxt].unsqueeze(1)), dim=1)
+        el = time.perf_counter() - t0
+    out["greedy"] = {"value": round(Bg / el, 3), "unit": "captions/s",
+                     "sample": f"{Bg} captions x 50 greedy tokens, full recompute per token (the reference's loop, "
+                               f"no KV cache), fp32, {cores} threads, in {el:.1f}s"}
+    return out
 
 
 def greedy_rate(model, Bd, dev, world, edim=512):

@@ -17,6 +17,7 @@ import torch
 
 from . import ops
 from .mapper import DWHelper, MLPMapperCore, TransformerMapperCore
+from .models import _embedding_grads
 
 Tensor = torch.Tensor
 
@@ -42,24 +43,38 @@ class CaptionTrainer:
         flat = model.flat()
         self.flat = flat
         self.mcore = model.mapping_network.core(self.dtype, flat)
-        self.gcore = model.gpt.core(self.dtype)
         self.clip = clip_model.core(self.dtype) if clip_model is not None else None
+        # freeze_gpt_weights=False (src/models.py:216-217, train.py:94-96): every GPT-2 tensor is in the flat
+        # storage, the backward adds its dW / bias / LayerNorm / tied-wte / wpe grads, and the AdamW step is
+        # followed by an in-place refresh of the GPT-2 forward-orientation copies
         self.gpt_trainable = not model.freeze_gpt_weights
         if self.gpt_trainable:
-            raise NotImplementedError("the fused trainer covers the reference default freeze_gpt_weights=True; "
-                                      "use ImageCaptioningModel.forward + autograd for unfrozen GPT-2")
+            model.gpt.invalidate_core()  # a core of its own, bound to the flat storage
+            self.gcore = model.gpt.core(self.dtype)
+            model.gpt.invalidate_core()
+            self.gcore.bind_flat(flat)
+            compact_head = False  # the tied wte gradient reads the LM-head input of every row
+        else:
+            self.gcore = model.gpt.core(self.dtype)
         B, Lc = batch_size, caption_len
         P = model.total_prefix_length
         self.P = P
         self.mws = self.mcore.alloc(B, train=True)
-        self.gws = self.gcore.alloc_train(B, P, Lc, compact_head=compact_head)
+        self.gws = self.gcore.alloc_train(B, P, Lc, keep_for_dw=self.gpt_trainable, compact_head=compact_head)
         D = self.gcore.D
         M2 = self.mws.M
         E = self.mcore.E
+        S = self.gws.S
         max_cols = max(4 * D, 3 * D, E, self.mcore.dw_cols())
+        max_rows, ln_rows, cs_cols = max(M2, B), M2, P * D
+        if self.gpt_trainable:  # + the GPT-2 dW products (the tied wte: [V, D]) and the wpe column sums
+            max_cols = max(max_cols, self.gcore.V)
+            max_rows, ln_rows, cs_cols = max(max_rows, self.gws.M), max(M2, self.gws.M), S * D
         # colsum also reduces the prefix_const / task-prefix grads over the batch: B rows x P*D columns
-        self.dwh = DWHelper(self.dtype, self.dev, max_rows=max(M2, B), max_cols=max_cols, ln_rows=M2, ln_D=D,
-                            colsum_cols=P * D)
+        self.dwh = DWHelper(self.dtype, self.dev, max_rows=max_rows, max_cols=max_cols, ln_rows=ln_rows, ln_D=D,
+                            colsum_cols=cs_cols)
+        self.ggrads = model._gpt_grads(flat) if self.gpt_trainable else None
+        self._gver = flat.flat._version
         self.mgrads = self.mcore.grads(flat)
         if model.task_prefix_embeds is not None:
             self.task_grad = flat.grad(model.task_prefix_embeds)
@@ -136,7 +151,10 @@ class CaptionTrainer:
         gc.forward_train(self.gws, pre, pbs, self.ids, self.mask, self.labels, self.gdr, fuse_dlogits=True,
                          grad_scale=grad_scale)
         S = self.gws.S
-        d_emb = gc.backward(self.gws, self.gdr, self.gws.key_mask, self.gws.logits)
+        d_emb = gc.backward(self.gws, self.gdr, self.gws.key_mask, self.gws.logits, grads=self.ggrads,
+                            dw=self.dwh if self.gpt_trainable else None)
+        if self.gpt_trainable:
+            _embedding_grads(d_emb, self.ids, B, P, self.Lc, D, self.ggrads, self.dwh)
         d_pre = d_emb.view(B, S * D)[:, : P * D]
         Pm = mc.P
         if model.task_prefix_embeds is not None:
@@ -157,6 +175,8 @@ class CaptionTrainer:
                        num_warmup_steps=hp.num_warmup_steps, num_training_steps=hp.num_training_steps,
                        bf16_out=f.flat_c)
         self.mcore.refresh_transposes()
+        if self.gpt_trainable:
+            self.gcore.refresh_from_flat()
 
     def _allreduce(self) -> None:
         if self.world > 1:
@@ -176,6 +196,9 @@ class CaptionTrainer:
         With use_graph the first call runs eagerly (warm-up) and every later call replays a captured HIP graph
         (one per (zero, step) form)."""
         self.model.sync_compute_copies()
+        if self.gpt_trainable and self.flat.flat._version != self._gver:  # masters written outside the optimizer
+            self.gcore.refresh_from_flat()
+            self._gver = self.flat.flat._version
         if zero is None:
             zero = self._micro == 0
         if step is None:

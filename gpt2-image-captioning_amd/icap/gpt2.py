@@ -268,6 +268,37 @@ class GPT2Core:
             ops.convert(t.wpe.weight.data, self.wpe)
         self.eps = self.cfg.layer_norm_epsilon
 
+    @torch.no_grad()
+    def bind_flat(self, flat) -> None:
+        """Trainable GPT-2 in the fused trainer: read every weight from the flat parameter storage (fp32 masters
+        and the compute-dtype copy the AdamW kernel writes), so an optimizer step updates this core in place.
+        The [in,out] (dX) orientation, wpe and the fp32 biases / LayerNorm parameters are views of that storage;
+        the [out,in] (forward) transposes and the padded LM-head table are copies that refresh_from_flat()
+        rewrites in place (HIP-graph capturable) after each step."""
+        t = self.model.transformer
+        for blk, lw in zip(t.h, self.layers):
+            lw.w_attn, lw.w_proj = flat.view_c(blk.attn.c_attn.weight), flat.view_c(blk.attn.c_proj.weight)
+            lw.w_fc, lw.w_mp = flat.view_c(blk.mlp.c_fc.weight), flat.view_c(blk.mlp.c_proj.weight)
+            lw.b_attn, lw.b_proj = blk.attn.c_attn.bias.data, blk.attn.c_proj.bias.data
+            lw.b_fc, lw.b_mp = blk.mlp.c_fc.bias.data, blk.mlp.c_proj.bias.data
+            lw.ln1_g, lw.ln1_b = blk.ln_1.weight.data, blk.ln_1.bias.data
+            lw.ln2_g, lw.ln2_b = blk.ln_2.weight.data, blk.ln_2.bias.data
+        self.lnf_g, self.lnf_b = t.ln_f.weight.data, t.ln_f.bias.data
+        self.wpe = flat.view_c(t.wpe.weight)
+        self._wte_c = flat.view_c(t.wte.weight)
+        self.refresh_from_flat()
+
+    @torch.no_grad()
+    def refresh_from_flat(self) -> None:
+        """Rewrite the forward-orientation transposes and the padded LM-head table from the bound storage."""
+        for lw in self.layers:
+            ops.transpose(lw.w_attn, lw.w_attn_t)
+            ops.transpose(lw.w_proj, lw.w_proj_t)
+            ops.transpose(lw.w_fc, lw.w_fc_t)
+            ops.transpose(lw.w_mp, lw.w_mp_t)
+        ops.convert(self._wte_c, self.wte[: self.V])
+        ops.transpose(self.wte, self.wte_t)
+
     # -- workspaces --------------------------------------------------------------------------------------
     def alloc_train(self, B: int, P: int, Lc: int, keep_for_dw: bool = False,
                     compact_head: bool = False) -> SimpleNamespace:

@@ -57,6 +57,23 @@ def test_trainer_step_in_bounds(mapper, dropout, dtype):
         _assert_clean(rec)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dropout", [False, True])
+def test_trainer_unfrozen_step_in_bounds(dtype, dropout):
+    """freeze_gpt_weights=False in the fused trainer: dW / LN / tied-wte / wpe grads, the optimizer step and the
+    in-place refresh of the GPT-2 copies stay in bounds; the GPT-2 grads land in the flat gradient buffer."""
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model(freeze=False, dtype=dtype)
+        t = CaptionTrainer(model, 3, 12, num_training_steps=3, dropout=dropout)
+        assert t.gpt_trainable and not t.gws.compact
+        t.load_batch(*batch(3, 12))
+        t.micro_step()
+        _assert_clean(rec)
+        names = [c[0] for c in rec.calls]
+        assert "icap_embedding_scatter_add" in names and names.count("icap_transpose") >= 4 * 2 + 1
+
+
 def test_trainer_task_prefix_in_bounds():
     with dry_run() as rec:
         icap.weights.ops.call = rec

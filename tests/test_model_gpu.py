@@ -200,6 +200,35 @@ def test_tiny_autograd_dropin_unfrozen(dev):
         assert rel(torch.tensor([t.sum().item(), t.abs().sum().item()]), torch.tensor(ck[:2])) < 1e-4, k
 
 
+def _check_gpt_checksums(model, g, tol):
+    for k, v in model.gpt.state_dict().items():
+        if k == "lm_head.weight":  # tied to transformer.wte.weight
+            continue
+        t = v.detach().double()
+        ck = g["unfrozen_ck.gpt." + k]
+        assert rel(torch.tensor([t.sum().item(), t.abs().sum().item()]), torch.tensor(ck[:2])) < tol, k
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_tiny_fused_train_unfrozen_matches_reference(dev, graph):
+    """freeze_gpt_weights=False through the fused trainer (src/train.py:94-96,150-153: AdamW over all parameters)
+    vs the reference train() golden: every GPT-2 tensor (tied wte, wpe, LayerNorms, biases) after the steps."""
+    g = load("tiny")
+    model = build(TINY_G, TINY_M, torch.float32, dev, freeze=False)
+    n = len(g["unfrozen_losses"])
+    losses, t = _trainer_steps(model, inputs(g, dev), n, graph=graph)
+    assert t.gpt_trainable
+    assert rel(losses, g["unfrozen_losses"]) < 1e-5
+    _check_gpt_checksums(model, g, 1e-4)
+    # the trainer's refreshed GPT-2 copies and the masters the inference path rebuilds from agree: one more
+    # forward/backward in the trainer gives the model's own forward loss at the trained weights
+    ids, mask, labels, emb = inputs(g, dev)
+    t._fwd_bwd(True, 1.0)
+    with torch.no_grad():
+        out = model.eval()(ids, emb, mask, labels)
+    assert abs(t.last_loss.item() - out.loss.item()) < 1e-5
+
+
 @pytest.fixture(scope="module")
 def small_f32(dev):
     return build(O.GPT2Cfg(), O.MapperCfg(), torch.float32, dev)

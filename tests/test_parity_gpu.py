@@ -19,7 +19,7 @@ from icap import ops
 from icap.clip import CLIPVisionConfig, CLIPVisionTower
 from icap.vit import ViTImageTower
 from oracle import icap_oracle as O
-from test_model_gpu import _trainer_steps, build, inputs, load, rel
+from test_model_gpu import _check_gpt_checksums, _trainer_steps, build, inputs, load, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -171,6 +171,26 @@ def test_small_bf16_train_tracks_reference(dev):
     print(f"bf16 update cosine: all tensors {whole:.4f}, min tensor {min(cosines.values()):.4f}")
     assert whole >= 0.85, (whole, cosines)
     assert min(cosines.values()) >= 0.7, cosines
+
+
+def test_small_fused_train_unfrozen_f32(dev):
+    """GPT-2 small unfrozen (freeze_gpt_weights=False) through the fused trainer: 2 reference train() steps, the
+    losses and every GPT-2 tensor's checksum (tools/make_goldens.py golden_small_train)."""
+    g = load("small_train")
+    model = build(O.GPT2Cfg(), O.MapperCfg(), torch.float32, dev, freeze=False)
+    losses, _ = _trainer_steps(model, inputs(g, dev), len(g["unfrozen_losses"]))
+    assert rel(losses, g["unfrozen_losses"]) < 1e-5
+    _check_gpt_checksums(model, g, 1e-4)
+
+
+def test_small_fused_train_unfrozen_bf16(dev):
+    """The same in the benchmarked precision: losses within 3e-2 of the reference's, checksums within 1e-2 rel
+    (bf16 forward/backward, fp32 masters and AdamW)."""
+    g = load("small_train")
+    model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev, freeze=False)
+    losses, _ = _trainer_steps(model, inputs(g, dev), len(g["unfrozen_losses"]), graph=True)
+    assert np.abs(np.array(losses) - g["unfrozen_losses"]).max() < 3e-2, losses
+    _check_gpt_checksums(model, g, 1e-2)
 
 
 def test_small_bf16_greedy_agreement(dev):
