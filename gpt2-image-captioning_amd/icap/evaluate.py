@@ -60,11 +60,16 @@ def compute_caption_metrics(preds, annotations_path: str) -> Dict[str, float]:
 
 def evaluate_epoch(model, dataset, annotations_path, epoch, split_name, batch_size, num_workers, max_length,
                    temperature, top_p, device, output_dir) -> Dict[str, Any]:
+    """src/eval.py:311-386: predictions -> `epoch_{epoch}_{split}_predictions.json` ([{"image_id", "caption"}],
+    indent 2) and `epoch_{epoch}_{split}_metrics.json` ({"epoch", "split", "num_images", **metrics}), the
+    reference's file names and layouts. Returns the metrics dict (+ num_predictions)."""
     model.eval()
-    preds = generate_predictions(model, dataset, batch_size, max_length, temperature, top_p, device)
     os.makedirs(output_dir, exist_ok=True)
-    with open(os.path.join(output_dir, f"{split_name}_predictions_epoch_{epoch}.json"), "w") as f:
-        json.dump(preds, f)
+    preds = generate_predictions(model, dataset, batch_size, max_length, temperature, top_p, device)
     m = compute_caption_metrics(preds, annotations_path) if annotations_path else {}
+    with open(os.path.join(output_dir, f"epoch_{epoch}_{split_name}_predictions.json"), "w") as f:
+        json.dump(preds, f, indent=2)
+    with open(os.path.join(output_dir, f"epoch_{epoch}_{split_name}_metrics.json"), "w") as f:
+        json.dump({"epoch": epoch, "split": split_name, "num_images": len(preds), **m}, f, indent=2)
     m["num_predictions"] = len(preds)
     return m

@@ -1,0 +1,71 @@
+"""Bitwise determinism of the train step against co-scheduled work.
+
+One fused-trainer forward + backward (GPT-2 small frozen + transformer mapper, bf16, dropout off) runs twice from
+the same state: alone, and with a long chain of unrelated GEMMs running concurrently on a second HIP stream (so
+the step's kernels share CUs, L2 and HBM with foreign workgroups). No kernel of the step uses atomics or
+placement-dependent reductions, so every intermediate and the flat gradient must be bitwise identical. On a
+mismatch the test names the first differing buffer in schedule order."""
+
+import pytest
+import torch
+
+from icap import ops
+from oracle import icap_oracle as O
+from test_model_gpu import build
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(B, dev):
+    ids, mask, labels, _ = O.synthetic_batch(B, 50, 13, seed=3)
+    emb = torch.randn((B, 512), generator=torch.Generator().manual_seed(4))
+    return ids.to(dev), mask.to(dev), labels.to(dev), (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
+
+
+def _snapshot(t):
+    g = t.gws
+    snap = [("mapper prefix", t.mws.out if hasattr(t.mws, "out") else None)]
+    snap += [(f"x[{l}]", g.x[l]) for l in range(len(g.x))]
+    snap += [("logits/dlogits", g.logits), ("dhf", g.dhf), ("loss", g.loss)]
+    snap += [("dx", g.dx), ("dx2", g.dx2), ("dxd", g.dxd), ("dqkv (layer 0)", g.dqkv), ("dff (layer 0)", g.dff)]
+    snap += [("mapper dout", t.mws.dout), ("flat_grad", t.flat.flat_grad)]
+    return [(n, x.detach().clone()) for n, x in snap if x is not None]
+
+
+def _noise(dev, n):
+    s = torch.cuda.Stream(dev)
+    a = torch.randn((4096, 4096), device=dev).to(torch.bfloat16)
+    c = torch.empty((4096, 4096), device=dev, dtype=torch.bfloat16)
+    torch.cuda.synchronize(dev)
+
+    def launch():
+        with torch.cuda.stream(s):
+            for _ in range(n):
+                ops.gemm(a, a, c, split_k=1)  # no split-K: never touches the default workspace
+    return launch, s
+
+
+@pytest.mark.parametrize("B", [32])
+def test_train_step_bitwise_with_concurrent_stream(dev, B):
+    from icap import CaptionTrainer
+
+    model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
+    t = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10, dropout=False)
+    t.load_batch(*_batch(B, dev))
+    t._fwd_bwd(True, 1.0)  # warm-up (first-use initialisation)
+    torch.cuda.synchronize(dev)
+    t._fwd_bwd(True, 1.0)
+    torch.cuda.synchronize(dev)
+    ref = _snapshot(t)
+    launch, s = _noise(dev, 40)
+    for rep in range(3):
+        launch()  # ~40 x 4096^3 GEMMs queued on the side stream, running under the step below
+        t._fwd_bwd(True, 1.0)
+        torch.cuda.synchronize(dev)
+        s.synchronize()
+        got = _snapshot(t)
+        for (name, a), (_, b) in zip(ref, got):
+            if not torch.equal(a, b):
+                d = (a.float() - b.float()).abs()
+                pytest.fail(f"rep {rep}: first differing buffer '{name}': {int((d > 0).sum())} elements, "
+                            f"max |d| {float(d.max()):.3g}")

@@ -9,7 +9,7 @@ outputs. Dropout is disabled (GPT2Config *_pdrop=0 and the mapper's dropout
 modules set to p=0) so outputs are deterministic. Only inputs + outputs are
 written: no reference source travels.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/make_goldens.py [tiny small clip vit clip_l14 topp small_train medium]
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/make_goldens.py [tiny small clip vit clip_l14 topp small_train medium ckpt]
 """
 
 from __future__ import annotations
@@ -333,6 +333,29 @@ def golden_medium(workdir):
                   logit_rows=[14, 17, 26], train_steps=2, unfrozen_steps=0, workdir=workdir, full_logits=False)
 
 
+def golden_ckpt_keys(workdir):
+    """Key sets + shapes of the reference's save_parameters() files (src/models.py:489-519) for the transformer
+    mapper with GPT-2 frozen / unfrozen and the MLP mapper (GPT-2 small geometry), and of its extraction .pt
+    (src/embeddings/clip.py:147-149) -> tests/golden/ckpt_keys.json."""
+    import json
+
+    out = {}
+    for tag, mapper, mcfg, freeze in (("transformer_frozen", "transformer", O.MapperCfg(), True),
+                                      ("transformer_unfrozen", "transformer", O.MapperCfg(), False),
+                                      ("mlp_frozen", "mlp", O.MLPMapperCfg(), True)):
+        model, _, _ = build_ref(O.GPT2Cfg(), mcfg, 0, mapper)
+        if not freeze:
+            for p in model.gpt.parameters():
+                p.requires_grad = True
+        path = os.path.join(workdir, f"{tag}.pt")
+        model.save_parameters(path)
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        out[tag] = {k: list(v.shape) for k, v in sd.items()}
+        print(tag, len(sd), "keys")
+    with open(os.path.join(OUT, "ckpt_keys.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     stub_modules()
@@ -363,6 +386,8 @@ def main():
             golden_small_train(work)
         if not only or "medium" in only:
             golden_medium(work)
+        if not only or "ckpt" in only:
+            golden_ckpt_keys(work)
     finally:
         os.chdir(cwd)
 
