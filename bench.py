@@ -246,6 +246,46 @@ def preprocess_rate(dev):
             "device_includes": "host packing + H2D copy of the uint8 pixels + 2 kernels"}
 
 
+def extraction_rate(tower, dev, n_images: int = 512):
+    """End-to-end CLIP embedding extraction (src/embeddings/clip.py:79-149 -> icap.clip.extract_clip_embeddings):
+    a directory of 640x480 JPEGs -> .pt file, incl. JPEG decode in DataLoader workers, device preprocessing, the
+    ViT-B/32 tower (bf16) and the torch.save. The reference's only published figure is this loop at batch 64 with
+    4 workers: 65 images/s (notebooks/extract_clip_embeddings.ipynb:167,174)."""
+    import shutil
+    import tempfile
+
+    import numpy as np
+    from PIL import Image
+
+    from icap.clip import DeviceCLIPProcessor, extract_clip_embeddings
+
+    d = tempfile.mkdtemp(prefix="icap_extract_")
+    try:
+        rng = np.random.default_rng(7)
+        yy, xx = np.mgrid[0:480, 0:640]
+        for i in range(n_images):  # smooth colour fields + noise: JPEG sizes like photos (~60-90 KB)
+            base = np.stack([(xx * (1 + i % 5) + yy * (i % 3)) % 256, (yy * 2 + i * 7) % 256,
+                             (xx + yy + i * 13) % 256], -1).astype(np.int16)
+            img = np.clip(base + rng.integers(-40, 40, base.shape), 0, 255).astype(np.uint8)
+            Image.fromarray(img).save(os.path.join(d, f"COCO_val2014_{i:012d}.jpg"), quality=90)
+        proc = DeviceCLIPProcessor(device=dev)
+        out = os.path.join(d, "emb.pt")
+        res = {}
+        for workers in (4, 16):
+            extract_clip_embeddings(d, out, tower, proc, batch_size=64, num_workers=workers, device=dev)  # warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            extract_clip_embeddings(d, out, tower, proc, batch_size=64, num_workers=workers, device=dev)
+            torch.cuda.synchronize()
+            res[f"images_per_s_{workers}_workers"] = round(n_images / (time.perf_counter() - t0), 1)
+        res.update({"images": n_images, "image": "640x480 JPEG q90", "batch": 64,
+                    "reference_published_images_per_s": 65.0,
+                    "includes": "JPEG decode (PIL, DataLoader workers) + device preprocess + CLIP-B/32 bf16 + .pt save"})
+        return res
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (tools/pmc_traffic.sh writes
     profiles/*pmc_traffic.json from separate FETCH_SIZE / WRITE_SIZE passes over this bench's train step).
@@ -393,6 +433,7 @@ def main():
     # the committed PMC pass measured the configs[1] step: its per-launch bytes do not describe other configs
     traffic, traffic_src = pmc_traffic(dom) if args.config == "small" else (None, None)
     prep = None if args.no_decode else preprocess_rate(dev)
+    extract = extraction_rate(tower, dev) if (not args.no_decode and args.config == "small" and rank == 0) else None
 
     if rank == 0:
         res = {
@@ -418,6 +459,7 @@ def main():
             "greedy_serving_batch": big,
             "topp_sampling": topp,
             "clip_preprocess": prep,
+            "clip_extraction": extract,
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1),
                          "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
                          "traffic": traffic, "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE)",

@@ -317,6 +317,8 @@ class CLIPProcessor:
             images = [images]
         out = []
         for im in images:
+            if isinstance(im, torch.Tensor):  # decoded RGB uint8 from the extraction workers
+                im = im.numpy()
             im = Image.fromarray(np.asarray(im, dtype=np.uint8)) if isinstance(im, np.ndarray) else im.convert("RGB")
             im = im.resize(resize_shortest_edge(im.size, self.size), Image.BICUBIC)
             w, h = im.size

@@ -2,7 +2,7 @@
 DataLoader loops of src/embeddings/clip.py:79-149 / vit.py:80-137).
 
 The reference decodes JPEGs in `num_workers` DataLoader processes and preprocesses each batch on the host; here the
-workers decode to RGB uint8 arrays (cheap to hand between processes) and the batch goes to the tower's processor
+workers decode to RGB uint8 tensors (handed over through shared memory) and the batch goes to the tower's processor
 (the device one runs resize / crop / normalise as HIP kernels). Filenames come in os.listdir order filtered by
 extension, exactly as the reference lists them, so the saved .pt rows line up with the reference's.
 """
@@ -29,15 +29,17 @@ class ImageDirectoryDataset(Dataset):
     def __len__(self) -> int:
         return len(self.filenames)
 
-    def __getitem__(self, idx: int) -> Tuple[str, np.ndarray]:
+    def __getitem__(self, idx: int) -> Tuple[str, torch.Tensor]:
+        """(filename, RGB uint8 [H, W, 3] tensor): a tensor, not a numpy array, so a DataLoader worker hands the
+        decoded pixels over through shared memory instead of pickling ~1 MB per image through a pipe."""
         from PIL import Image
 
         name = self.filenames[idx]
         with Image.open(os.path.join(self.directory, name)) as im:
-            return name, np.asarray(im.convert("RGB"))
+            return name, torch.from_numpy(np.asarray(im.convert("RGB")).copy())
 
     @staticmethod
-    def collate_fn(batch) -> Tuple[List[str], List[np.ndarray]]:
+    def collate_fn(batch) -> Tuple[List[str], List[torch.Tensor]]:
         names, images = zip(*batch)
         return list(names), list(images)
 

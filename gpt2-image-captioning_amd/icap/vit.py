@@ -309,6 +309,8 @@ class ViTImageProcessor:
             images = [images]
         out = []
         for im in images:
+            if isinstance(im, torch.Tensor):  # decoded RGB uint8 from the extraction workers
+                im = im.numpy()
             im = Image.fromarray(np.asarray(im, dtype=np.uint8)) if isinstance(im, np.ndarray) else im.convert("RGB")
             im = im.resize((self.size, self.size), Image.BILINEAR)
             a = np.asarray(im, dtype=np.float32) * np.float32(1 / 255)
