@@ -28,233 +28,9 @@
 // supplies k = 4g+s in MFMA s for both operands, so the K permutation is
 // identical on A and B and the product is exact.
 // C/D map (both): col = lane&15, row = 4*(lane>>4) + reg.
-#include "common.h"
-
-#include <type_traits>
+#include "gemm_common.h"
 
 namespace icap {
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-
-constexpr int GBM = 128, GBN = 128, GROWB = 128, GNT = 256;  // default 128x128 tile, 128-byte LDS rows
-constexpr uint32_t OOB = 0x80000000u;              // buffer offset beyond any num_records -> loads 0
-
-__device__ __forceinline__ int lds_off(int row, int chunk) {
-  return row * GROWB + ((chunk ^ (row & 7)) << 4);
-}
-
-template <typename TI>
-__device__ __forceinline__ void mfma_chunk(f32x4_t& acc, const uint4& a, const uint4& b);
-
-template <>
-__device__ __forceinline__ void mfma_chunk<bf16_t>(f32x4_t& acc, const uint4& a, const uint4& b) {
-#ifdef ICAP_GEMM_NO_MFMA  // diagnostic build only (tools/ab_gemm.sh): the staging pipeline without the MFMAs
-  acc[0] += __uint_as_float((a.x ^ b.x) & 0x3f800000u);
-#else
-  bf16x8_t av = __builtin_bit_cast(bf16x8_t, a);
-  bf16x8_t bv = __builtin_bit_cast(bf16x8_t, b);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
-#endif
-}
-template <>
-__device__ __forceinline__ void mfma_chunk<float>(f32x4_t& acc, const uint4& a, const uint4& b) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint64_t bytes) {
-  const uint32_t n = bytes > 0x7fffffffull ? 0x7fffffffu : (uint32_t)bytes;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
-}
-
-// same, with the inputs forced into SGPRs (readfirstlane) so hipcc can prove the descriptor wave-uniform and
-// emits no waterfall loop around the buffer ops (cdna_hip_programming.md T20)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc_u(const void* base, uint64_t bytes) {
-  const uint64_t b = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-  const uint32_t n = __builtin_amdgcn_readfirstlane(bytes > 0x7fffffffull ? 0x7fffffffu : (uint32_t)bytes);
-  void* pb = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(pb, (short)0, (int)n, 0x00020000);
-}
-
-// 16-byte LDS-DMA of one wave: lane l's 16 bytes land at lds + 16 l
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t off) {
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(lds), 16, off, 0, 0, 0);
-}
-
-// same with a wave-uniform soffset (row / k offsets in SGPRs, one per-lane VGPR offset)
-__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
-  typedef __attribute__((address_space(3))) void* lds_ptr_t;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(lds), 16, voff, soff, 0, 0);
-}
-
-__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-
-// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N)
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-// W consecutive elements (W = 4 or 8) as fp32, through one 8- or 16-byte access (bf16) or one / two float4 (f32)
-template <typename T, int W> struct vecio;
-template <int W> struct vecio<float, W> {
-  static __device__ __forceinline__ void ld(const float* p, float v[W]) {
-#pragma unroll
-    for (int q = 0; q < W / 4; ++q) io<float>::ld4(p + 4 * q, v + 4 * q);
-  }
-  static __device__ __forceinline__ void st(float* p, const float v[W]) {
-#pragma unroll
-    for (int q = 0; q < W / 4; ++q) io<float>::st4(p + 4 * q, v + 4 * q);
-  }
-};
-template <> struct vecio<bf16_t, 4> {
-  static __device__ __forceinline__ void ld(const bf16_t* p, float v[4]) { io<bf16_t>::ld4(p, v); }
-  static __device__ __forceinline__ void st(bf16_t* p, const float v[4]) { io<bf16_t>::st4(p, v); }
-};
-template <> struct vecio<bf16_t, 8> {
-  static __device__ __forceinline__ void ld(const bf16_t* p, float v[8]) {
-    const uint4 t = *reinterpret_cast<const uint4*>(p);
-    const uint32_t w[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      v[2 * q] = __uint_as_float(w[q] << 16);
-      v[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
-    }
-  }
-  static __device__ __forceinline__ void st(bf16_t* p, const float v[8]) {
-    *reinterpret_cast<uint4*>(p) = make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7]));
-  }
-};
-// raw bf16 vector of W elements (prefetched epilogue operands)
-template <int W> struct rawbf;
-template <> struct rawbf<4> { typedef uint2 T; };
-template <> struct rawbf<8> { typedef uint4 T; };
-__device__ __forceinline__ void unpack_bf16(const uint2 w, float v[4]) {
-  v[0] = __uint_as_float(w.x << 16);
-  v[1] = __uint_as_float(w.x & 0xffff0000u);
-  v[2] = __uint_as_float(w.y << 16);
-  v[3] = __uint_as_float(w.y & 0xffff0000u);
-}
-__device__ __forceinline__ void unpack_bf16(const uint4 w, float v[8]) {
-  unpack_bf16(make_uint2(w.x, w.y), v);
-  unpack_bf16(make_uint2(w.z, w.w), v + 4);
-}
-
-// The epilogue arithmetic, shared by every GEMM kernel (tile, split-K reduce, skinny, ring): one formula with a
-// fixed contraction (explicit fma for alpha*acc + bias, no other fusing), so two kernels that accumulate a product
-// in the same order store bitwise-identical outputs (tests/test_gemm_ring_gpu.py).
-// backward form: x = alpha * acc * dropmask * act'(a)
-template <int W>
-__device__ __forceinline__ void epi_bwd_math(const icap_gemm_args& p, float x[W], const float a[W], uint64_t seed,
-                                             uint64_t didx, uint32_t drop_thresh, float inv_keep) {
-#pragma clang fp contract(off)
-#pragma unroll
-  for (int e = 0; e < W; ++e) {
-    float y = p.alpha * x[e];
-    if (drop_thresh != 0u) y = y * drop_scale(seed, didx + e, drop_thresh, inv_keep);
-    x[e] = y * act_bwd(p.dact, a[e]);
-  }
-}
-// forward form, first half: x = act(alpha * acc + bias); a = the aux value (pre-activation, or tanh output)
-template <int W>
-__device__ __forceinline__ void epi_fwd_act(const icap_gemm_args& p, float x[W], const float biasw[W], float a[W]) {
-#pragma clang fp contract(off)
-#pragma unroll
-  for (int e = 0; e < W; ++e) x[e] = __builtin_fmaf(p.alpha, x[e], biasw[e]);
-  if (p.act != ICAP_ACT_NONE || p.aux) {
-#pragma unroll
-    for (int e = 0; e < W; ++e) {
-      const float y = act_fwd(p.act, x[e]);
-      a[e] = (p.act == ICAP_ACT_TANH) ? y : x[e];
-      x[e] = y;
-    }
-  }
-}
-// forward form, second half: x = x * dropmask (+ r)
-template <int W>
-__device__ __forceinline__ void epi_fwd_tail(float x[W], const float r[W], bool add_r, uint64_t seed, uint64_t didx,
-                                             uint32_t drop_thresh, float inv_keep) {
-#pragma clang fp contract(off)
-  if (drop_thresh != 0u) {
-#pragma unroll
-    for (int e = 0; e < W; ++e) x[e] = x[e] * drop_scale(seed, didx + e, drop_thresh, inv_keep);
-  }
-  if (add_r) {
-#pragma unroll
-    for (int e = 0; e < W; ++e) x[e] = x[e] + r[e];
-  }
-}
-
-// Epilogue of W consecutive columns [col, col+W) of row `row` (the order is the one include/icap.h documents).
-// x: alpha-unscaled fp32 accumulators; biasw: bias[col..col+W-1] (0 past N); fullw: all W columns in range;
-// W-wide vector access is used per operand where its leading dimension and base pointer are W-aligned.
-// pre: optional prefetched raw bf16 vector of the epilogue's input operand at (row, col..) — dact_src in the
-// backward form, resid in the forward form — loaded by the caller ahead of the LDS staging (fullw rows only).
-template <typename TC, int W>
-__device__ __forceinline__ void epiw(const icap_gemm_args& p, int64_t row, int64_t col, float x[W],
-                                     const float biasw[W], bool fullw, uint64_t seed, uint32_t drop_thresh,
-                                     float inv_keep, const typename rawbf<W>::T* pre = nullptr) {
-  const int64_t N = p.N;
-  TC* C = reinterpret_cast<TC*>(p.C);
-  TC* aux = reinterpret_cast<TC*>(p.aux);
-  const TC* resid = reinterpret_cast<const TC*>(p.resid);
-  const TC* dsrc = reinterpret_cast<const TC*>(p.dact_src);
-  const uint64_t didx = p.offset + (uint64_t)(row * N + col);
-  float a[W], r[W], c[W];
-  // W-wide vector access needs the leading dimension AND the base pointer aligned to W elements (16 B suffices
-  // for 8 f32: two float4)
-  constexpr uintptr_t VA = (W * sizeof(TC) > 16 ? 16 : W * sizeof(TC)) - 1;
-  auto vok = [&](int64_t ld, const void* ptr) { return (ld % W) == 0 && (reinterpret_cast<uintptr_t>(ptr) & VA) == 0; };
-  fullw = fullw && vok(p.ldc, C);
-  if (p.dact != ICAP_ACT_NONE) {
-    if (pre) unpack_bf16(*pre, a);
-    else if (fullw && vok(p.ld_dact, dsrc)) vecio<TC, W>::ld(dsrc + row * p.ld_dact + col, a);
-    else for (int e = 0; e < W; ++e) a[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
-    epi_bwd_math<W>(p, x, a, seed, didx, drop_thresh, inv_keep);
-  } else {
-    epi_fwd_act<W>(p, x, biasw, a);
-    if (aux) {
-      if (fullw && vok(p.ldaux, aux)) vecio<TC, W>::st(aux + row * p.ldaux + col, a);
-      else for (int e = 0; e < W; ++e) if (col + e < N) io<TC>::st(aux + row * p.ldaux + col + e, a[e]);
-    }
-    if (resid) {
-      if (pre) unpack_bf16(*pre, r);
-      else if (fullw && vok(p.ldr, resid)) vecio<TC, W>::ld(resid + row * p.ldr + col, r);
-      else for (int e = 0; e < W; ++e) r[e] = (col + e < N) ? io<TC>::ld(resid + row * p.ldr + col + e) : 0.f;
-    }
-    epi_fwd_tail<W>(x, r, resid != nullptr, seed, didx, drop_thresh, inv_keep);
-  }
-  TC* cp = C + row * p.ldc + col;
-  if (fullw) {
-    if (p.beta != 0.f) {
-      vecio<TC, W>::ld(cp, c);
-#pragma unroll
-      for (int e = 0; e < W; ++e) x[e] += p.beta * c[e];
-    }
-    vecio<TC, W>::st(cp, x);
-  } else {
-    for (int e = 0; e < W; ++e)
-      if (col + e < N) io<TC>::st(cp + e, p.beta != 0.f ? x[e] + p.beta * io<TC>::ld(cp + e) : x[e]);
-  }
-}
-
-template <typename TC>
-__device__ __forceinline__ void epi4(const icap_gemm_args& p, int64_t row, int64_t col, float x[4],
-                                     const float bias4[4], bool full4, uint64_t seed, uint32_t drop_thresh,
-                                     float inv_keep) {
-  epiw<TC, 4>(p, row, col, x, bias4, full4, seed, drop_thresh, inv_keep);
-}
 
 // ---- K-outer operand images (trans_ab): [64 k-rows][128 columns] bf16, 256-byte rows, 16-byte chunk ch of row r
 // stored at chunk ch ^ kout_swz(r) (cdna_hip_programming.md T10 layout (b)) so the transposed reads below are
@@ -1313,10 +1089,42 @@ static int device_cus() {
   return cus[dev];
 }
 
+namespace icap {
+int gemm256_launch(const icap_gemm_args& p, uint32_t thr, float inv_keep, hipStream_t s);
+}
+
+// ICAP_GEMM256: 0 = never, 2 = wherever eligible, default = the shape rule below (A/B measurements only)
+static int g256_mode() {
+  static const int m = [] {
+    const char* e = getenv("ICAP_GEMM256");
+    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
+  }();
+  return m;
+}
+
+// The 256 x 256 kernel's preconditions, and when it is the automatic choice. It runs one block per CU, so a
+// tile's prologue (first DMA round trip) and epilogue do not overlap other tiles' MFMAs: it beats the 128-row
+// tile kernels (2-3 blocks per CU) on long K (4096^3: 1.09-1.22 vs 0.95 PF) and on many full tile rounds (LM
+// head 8320 x 50304 x 768: 758 vs 835 us), not on the train step's 2-round K = 768 products (8320 x 3072 x 768:
+// 84 vs 80 us) (profiles/r02_gemm256_bench.txt). path 3 forces it where eligible.
+static bool g256_pick(const icap_gemm_args& p) {
+  if (p.path == 1 || p.path == 2) return false;
+  if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.beta != 0.f || p.m_dev || p.split_k > 1) return false;
+  if (p.M < 256 || p.N < 256 || p.K < 64) return false;
+  if (p.path == 3 || g256_mode() == 2) return true;
+  if (g256_mode() == 0) return false;
+  const int64_t tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  const int64_t cus = device_cus();
+  const int64_t rounds = (tiles + cus - 1) / cus;
+  const bool full = tiles * 10 >= rounds * cus * 7;  // rounds at least 70 % occupied
+  return (p.K >= 2048 && tiles * 4 >= cus * 3 && full) || (rounds >= 4 && tiles * 10 >= rounds * cus * 8);
+}
+
 namespace {
 // What icap_gemm launches for one call (shared by the launcher and icap_gemm_kernel_name).
 struct GemmPlan {
   bool skinny = false;
+  bool g256 = false;     // the 256 x 256 8-phase kernel (gemm256.hip)
   int nt = 1;            // skinny: 16-column slabs per block
   int sku = 3;           // skinny: k-steps in flight per wave
   int ring = 0;          // ring kernel: WM (4 = 256 x 128 tiles, 2 = 128 x 128), 0 = not used
@@ -1397,6 +1205,11 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
     }
     pl.grid = dim3((unsigned)((p.N + 16 * pl.nt - 1) / (16 * pl.nt)), (unsigned)gy);
     pl.block = dim3(64 * SK_WAVES);
+    return ICAP_OK;
+  }
+  // 256 x 256 8-phase kernel (gemm256.hip) for wide products whose 256-tiles fill the chip in few, full rounds
+  if (g256_pick(p)) {
+    pl.g256 = true;
     return ICAP_OK;
   }
   // persistent ring kernel (one workgroup per CU, many output tiles each) for every eligible launch except the
@@ -1480,6 +1293,10 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
   const char* ti = a->in_dtype == ICAP_BF16 ? "unsigned short" : "float";
   const char* tc = a->c_dtype == ICAP_BF16 ? "unsigned short" : "float";
   char fmt[96];
+  if (pl.g256) {
+    snprintf(buf, sizeof buf, "icap::gemm256_kernel<%s>", tc);
+    return buf;
+  }
   if (pl.skinny) snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2, %d>", pl.nt, pl.sku);
   else if (pl.ring) snprintf(fmt, sizeof fmt, "gemm_ring_kernel<%d, %d>", pl.ring, pl.ring == 4 ? 3 : 4);
   else snprintf(fmt, sizeof fmt, "%s", variant_kernel(pl.variant));
@@ -1536,6 +1353,7 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
 #undef ICAP_SK
     return check_launch("icap_gemm(skinny)");
   }
+  if (pl.g256) return gemm256_launch(p, thr, inv_keep, s);
   if (pl.ring) {
     if (pl.ring == 4)
       hipLaunchKernelGGL((gemm_ring_kernel<4, 3>), pl.grid, pl.block, 0, s, p, pl.tiles_m, pl.tiles_n, pl.units, thr,

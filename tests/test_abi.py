@@ -89,9 +89,15 @@ def test_gemm_kernel_name_query_without_gpu():
     assert big == "icap::gemm_ring_kernel<4, 3>", big  # persistent ring kernel (opt-in), 256 x 128 tiles
     mid = lib.icap_gemm_kernel_name(C.byref(_gemm_args(3200, 768, 3072, path=2, split_k=1))).decode()
     assert mid == "icap::gemm_ring_kernel<2, 4>", mid  # too few 256-row tiles to fill the chip: 128 x 128
-    for path in (0, 1):  # the default is the tile kernels
-        tile = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 50304, 768, path=path))).decode()
-        assert tile.startswith("icap::gemm_kernel<") and "unsigned short, unsigned short" in tile
+    tile = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 50304, 768, path=1))).decode()
+    assert tile.startswith("icap::gemm_kernel<") and "unsigned short, unsigned short" in tile
+    # automatic choice: the 256 x 256 kernel on many full tile rounds and on long K, the tile kernels on the train
+    # step's two-round K = 768 products (the rule measured in profiles/r02_gemm256_bench.txt)
+    name = lambda *a, **k: lib.icap_gemm_kernel_name(C.byref(_gemm_args(*a, **k))).decode()  # noqa: E731
+    assert name(8320, 50304, 768) == "icap::gemm256_kernel<unsigned short>"
+    assert name(4096, 4096, 4096) == "icap::gemm256_kernel<unsigned short>"
+    assert name(8320, 3072, 768).startswith("icap::gemm_kernel<")
+    assert name(8320, 3072, 768, path=3) == "icap::gemm256_kernel<unsigned short>"
     skinny = lib.icap_gemm_kernel_name(C.byref(_gemm_args(128, 2304, 768))).decode()
     # 2304 columns over 4 row blocks: 3 slabs per block (192 blocks <= 256 CUs), K = 768 in 3 k-steps per wave
     assert skinny == "icap::gemm_skinny_kernel<unsigned short, unsigned short, 3, 2, 3>", skinny

@@ -72,13 +72,16 @@ def main():
         elif epi == "beta":
             kw = dict(beta=1.0)
         res = []
-        for tile in (False, True):  # automatic plan (ring kernel where eligible) vs the 128-row tile kernels
+        forms = [dict(), dict(tile_only=True)]  # automatic plan vs the 128-row tile kernels
+        if M >= 256 and N >= 256 and epi != "beta":
+            forms.append(dict(g256=True, split_k=1))  # the 256 x 256 8-phase kernel
+        for f in forms:
             for _ in range(3):
-                ops.gemm(A, B, C, tile_only=tile, **kw)
+                ops.gemm(A, B, C, **f, **kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(reps):
-                ops.gemm(A, B, C, tile_only=tile, **kw)
+                ops.gemm(A, B, C, **f, **kw)
             e1.record()
             torch.cuda.synchronize()
             res.append(e0.elapsed_time(e1) * 1e3 / reps)
@@ -86,8 +89,9 @@ def main():
         tot_ms += us / 1e3
         tot_tile += res[1] / 1e3
         fl = 2 * M * N * K
+        g256 = f" | g256 {res[2]:8.1f} us {fl / res[2] / 1e6:7.1f} TF/s" if len(res) > 2 else ""
         print(f"{M:6d}x{N:6d}x{K:6d} {epi:10s} {str(cdt)[6:]:9s} auto {us:8.1f} us {fl / us / 1e6:7.1f} TF/s | "
-              f"tile {res[1]:8.1f} us {fl / res[1] / 1e6:7.1f} TF/s", flush=True)
+              f"tile {res[1]:8.1f} us {fl / res[1] / 1e6:7.1f} TF/s{g256}", flush=True)
     print(f"sum: auto {tot_ms:.3f} ms, tile kernels {tot_tile:.3f} ms")
 
 
