@@ -10,8 +10,9 @@ trainable weights is written by the AdamW kernel itself.
 
 from __future__ import annotations
 
+import os
 from types import SimpleNamespace
-from typing import Optional
+from typing import List, Optional, Tuple
 
 import torch
 
@@ -76,6 +77,19 @@ class CaptionTrainer:
         self.ggrads = model._gpt_grads(flat) if self.gpt_trainable else None
         self._gver = flat.flat._version
         self.mgrads = self.mcore.grads(flat)
+        # data-parallel buckets: the flat-gradient ranges each segment of the step finalises (engine._segments)
+        mapper = model.mapping_network
+        if isinstance(self.mcore, TransformerMapperCore):
+            groups = [list(blk.parameters()) for blk in reversed(list(mapper.transformer.layers))]
+            groups.append([mapper.linear.weight, mapper.linear.bias, mapper.prefix_const])
+        else:
+            groups = [list(mapper.parameters())]
+        self._ranges_mapper = [flat_ranges(flat, ps) for ps in groups]
+        seen = {id(p) for ps in groups for p in ps}
+        self._ranges_front = flat_ranges(flat, [p for p in flat.params if id(p) not in seen])
+        self.dp_overlap = os.environ.get("ICAP_DP_OVERLAP", "1") != "0"
+        self.seg_graphs = {}  # zero -> [HIP graph per segment] (data-parallel overlapped step)
+        self._comm = None
         if model.task_prefix_embeds is not None:
             self.task_grad = flat.grad(model.task_prefix_embeds)
             self.pre = torch.empty((B, P, D), dtype=self.dtype, device=self.dev)
@@ -129,6 +143,45 @@ class CaptionTrainer:
 
     # -- the step ---------------------------------------------------------------------------------------------
     def _fwd_bwd(self, zero: bool, grad_scale: float) -> None:
+        for _, fn in self._segments(zero, grad_scale):
+            fn()
+
+    def _segments(self, zero: bool, grad_scale: float):
+        """The forward + backward as [(flat-gradient ranges finalised, fn)] in schedule order: everything up to the
+        mapper backward (finalises the GPT-2 grads when it is trainable and the task-prefix grad), then one segment
+        per mapper layer (top first) and the mapper's input projection. Run back to back they are the step; the
+        data-parallel step all-reduces each segment's ranges while the next segments compute."""
+        B, P, D = self.B, self.P, self.gcore.D
+        model, mc = self.model, self.mcore
+        st = SimpleNamespace()
+
+        def front():
+            st.d_emb = self._front(zero, grad_scale)
+
+        segs = [(self._ranges_front, front)]
+        if isinstance(mc, TransformerMapperCore):
+            steps = mc.backward_steps(self.mws, self.emb_c, self.mdr, self.mgrads, self.dwh)
+            for (_, _, fn), rng in zip(steps, self._ranges_mapper):
+                segs.append((rng, fn))
+        else:
+            S, Pm = self.gws.S, mc.P
+
+            def mlp():
+                d_pre = st.d_emb.view(B, S * D)[:, : P * D]
+                mc.backward_from(d_pre[:, : Pm * D], S * D, self.mws, self.emb_c, self.mgrads, self.dwh)
+
+            segs.append((self._ranges_mapper[0], mlp))
+        last_rng, last_fn = segs[-1]
+
+        def last():
+            last_fn()
+            self.loss_sum.add_(self.gws.loss)
+
+        segs[-1] = (last_rng, last)
+        return segs
+
+    def _front(self, zero: bool, grad_scale: float):
+        """Forward, LM head + CE, GPT-2 backward and the mapper's output gradient; returns d(inputs_embeds)."""
         B, P, D = self.B, self.P, self.gcore.D
         model = self.model
         if zero:
@@ -163,10 +216,7 @@ class CaptionTrainer:
         if isinstance(mc, TransformerMapperCore):
             Hl, Sm = mc.Hl, mc.S
             ops.convert(d_pre[:, : Pm * D], self.mws.dout.view(B, Sm * D)[:, Hl * D:])
-            mc.backward(self.mws, self.emb_c, self.mdr, self.mgrads, self.dwh)
-        else:
-            mc.backward_from(d_pre[:, : Pm * D], S * D, self.mws, self.emb_c, self.mgrads, self.dwh)
-        self.loss_sum.add_(self.gws.loss)
+        return d_emb
 
     def _optimizer(self) -> None:
         hp, f = self.hp, self.flat
@@ -181,6 +231,60 @@ class CaptionTrainer:
     def _allreduce(self) -> None:
         if self.world > 1:
             torch.distributed.all_reduce(self.flat.flat_grad, group=self.pg)
+
+    def _bucket(self, ranges, works) -> None:
+        """All-reduce these flat-gradient ranges behind the work queued so far on this stream, on a communication
+        stream (RCCL then runs beside the next backward segments); `works` collects the async handles."""
+        g = self.flat.flat_grad
+        if not ranges:
+            return
+        if g.is_cuda:
+            if self._comm is None:
+                self._comm = torch.cuda.Stream(g.device)
+            ev = torch.cuda.Event()
+            ev.record()
+            with torch.cuda.stream(self._comm):
+                self._comm.wait_event(ev)
+                for lo, hi in ranges:
+                    works.append(torch.distributed.all_reduce(g[lo:hi], group=self.pg, async_op=True))
+        else:
+            for lo, hi in ranges:
+                works.append(torch.distributed.all_reduce(g[lo:hi], group=self.pg, async_op=True))
+
+    def _overlapped_step(self, zero: bool, use_graph: bool) -> None:
+        """Data-parallel micro-batch that ends an accumulation cycle: each segment's gradient ranges are
+        all-reduced (RCCL, async) while the later segments of the backward run; the optimizer waits for all."""
+        works = []
+        if use_graph:
+            graphs = self.seg_graphs.get(zero)
+            if graphs is None:
+                graphs = self._capture_segments(zero)
+            for (rng, _), g in zip(self._segments(zero, self.grad_scale()), graphs):
+                g.replay()
+                self._bucket(rng, works)
+        else:
+            for rng, fn in self._segments(zero, self.grad_scale()):
+                fn()
+                self._bucket(rng, works)
+        for w in works:
+            w.wait()
+        if use_graph:
+            if self.graph_opt is None:
+                self.graph_opt = self._capture_opt()
+            self.graph_opt.replay()
+        else:
+            self._optimizer()
+
+    def _capture_segments(self, zero: bool):
+        torch.cuda.synchronize(self.dev)
+        graphs = []
+        for _, fn in self._segments(zero, self.grad_scale()):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            graphs.append(g)
+        self.seg_graphs[zero] = graphs
+        return graphs
 
     def grad_scale(self) -> float:
         return 1.0 / (self.grad_accum_steps * self.world)
@@ -203,7 +307,10 @@ class CaptionTrainer:
             zero = self._micro == 0
         if step is None:
             step = self._micro + 1 >= self.grad_accum_steps
-        if use_graph and self._eager_steps >= 1:
+        if step and self.world > 1 and self.dp_overlap:
+            self._overlapped_step(zero, use_graph and self._eager_steps >= 1)
+            self._eager_steps += 1
+        elif use_graph and self._eager_steps >= 1:
             with_opt = step and self.world == 1
             g = self.graphs.get((zero, with_opt))
             if g is None:
@@ -269,6 +376,21 @@ class CaptionTrainer:
     @property
     def last_loss(self) -> Tensor:
         return self.gws.loss
+
+
+def flat_ranges(flat, params) -> List[Tuple[int, int]]:
+    """[lo, hi) element ranges of the flat gradient buffer that hold `params` (each parameter's segment runs to the
+    next one's start, so the alignment padding is covered), adjacent segments merged."""
+    idx = sorted(flat._index(p) for p in params)
+    out: List[Tuple[int, int]] = []
+    for i in idx:
+        lo = flat.offsets[i]
+        hi = flat.offsets[i + 1] if i + 1 < len(flat.offsets) else flat.n
+        if out and out[-1][1] == lo:
+            out[-1] = (out[-1][0], hi)
+        else:
+            out.append((lo, hi))
+    return out
 
 
 def _rows_view(t: Tensor, B: int, n: int, stride: int) -> Tensor:

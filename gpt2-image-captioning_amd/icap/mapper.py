@@ -364,25 +364,37 @@ class TransformerMapperCore:
     # -- backward --------------------------------------------------------------------------------------------
     def backward(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper) -> None:
         """Consumes ws.dout (d of the forward output, rows t<Hl zero); accumulates every parameter grad."""
+        for _, _, fn in self.backward_steps(ws, emb_c, dr, g, dwh):
+            fn()
+
+    def backward_steps(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper):
+        """The backward as [(name, module, fn)]: one step per layer (the top layer first), then the input
+        projection ("head": linear + prefix_const). Run in order they are backward(); each step finalises the
+        grads of its module's parameters, which is what engine.CaptionTrainer's data-parallel all-reduce buckets
+        key on."""
         B, M, S, D, Hl, P = ws.B, ws.M, self.S, self.D, self.Hl, self.P
         scale = 1.0 / math.sqrt(self.hd)
-        dres = ws.dout
-        top = dr.d2(self.nl - 1)
-        if top.p > 0:
-            ops.dropout_apply(dres, ws.dmask, top)
-        dmask_valid = top.p > 0
+        st = SimpleNamespace()
         bufs = [ws.dres, ws.dnew]
-        bi = 0
-        for l in reversed(range(self.nl)):
+
+        def layer(l):
+            if l == self.nl - 1:  # start of the backward
+                st.dres = ws.dout
+                top = dr.d2(self.nl - 1)
+                if top.p > 0:
+                    ops.dropout_apply(st.dres, ws.dmask, top)
+                st.dmask_valid = top.p > 0
+                st.bi = 0
             w, gl = self.layers[l], g.layers[l]
-            dy = ws.dmask if dmask_valid else dres
+            dres = st.dres
+            dy = ws.dmask if st.dmask_valid else dres
             dwh.dW(dy, ws.f[l], gl.l2_w, M=M)
             dwh.db(dy, gl.l2_b, M=M)
             ops.gemm(dy, w.l2_wt, ws.dz, dact=L.ACT_RELU, dact_src=ws.f[l], drop=dr.dff(l))
             dwh.dW(ws.dz, ws.a2[l], gl.l1_w, M=M)
             dwh.db(ws.dz, gl.l1_b, M=M)
             ops.gemm(ws.dz, w.l1_wt, ws.da)
-            dnew = bufs[bi]; bi ^= 1
+            dnew = bufs[st.bi]; st.bi ^= 1
             d1 = dr.d1(l)
             ops.layernorm_bwd(ws.h1[l], w.n2_g, ws.mean2[l], ws.rstd2[l], ws.da, dnew, dres=dres,
                               dx_drop=ws.dmask if d1.p > 0 else None, drop=d1, dgamma=gl.n2_g, dbeta=gl.n2_b,
@@ -397,19 +409,27 @@ class TransformerMapperCore:
             dwh.dW(ws.dqkv, ws.a1[l], gl.in_w, M=M)
             dwh.db(ws.dqkv, gl.in_b, M=M)
             ops.gemm(ws.dqkv, w.in_wt, ws.da)
-            dnew = bufs[bi]; bi ^= 1
+            dnew = bufs[st.bi]; st.bi ^= 1
             nxt = dr.d2(l - 1) if l > 0 else Dropout()
             ops.layernorm_bwd(ws.x[l], w.n1_g, ws.mean1[l], ws.rstd1[l], ws.da, dnew, dres=dres,
                               dx_drop=ws.dmask if nxt.p > 0 else None, drop=nxt, dgamma=gl.n1_g, dbeta=gl.n1_b,
                               workspace=dwh.ln_ws)
-            dres = dnew
-            dmask_valid = nxt.p > 0
-        # x0 = [linear(emb) ; prefix_const]
-        d_lin = dres.view(B, S * D)[:, : Hl * D]
-        dwh.dW(d_lin, emb_c, g.lin_w, M=B)
-        dwh.db(d_lin, g.lin_b, M=B)
-        d_pc = dres.view(B, S * D)[:, Hl * D:]
-        ops.colsum(d_pc, g.prefix_const.view(-1), dwh.cs_ws, accumulate=True, M=B, N=P * D)
+            st.dres = dnew
+            st.dmask_valid = nxt.p > 0
+
+        def head():
+            # x0 = [linear(emb) ; prefix_const]
+            dres = st.dres
+            d_lin = dres.view(B, S * D)[:, : Hl * D]
+            dwh.dW(d_lin, emb_c, g.lin_w, M=B)
+            dwh.db(d_lin, g.lin_b, M=B)
+            d_pc = dres.view(B, S * D)[:, Hl * D:]
+            ops.colsum(d_pc, g.prefix_const.view(-1), dwh.cs_ws, accumulate=True, M=B, N=P * D)
+
+        m = self.m
+        steps = [(f"layer{l}", m.transformer.layers[l], (lambda l=l: layer(l))) for l in reversed(range(self.nl))]
+        steps.append(("head", None, head))
+        return steps
 
     # -- inference -------------------------------------------------------------------------------------------
     @torch.no_grad()

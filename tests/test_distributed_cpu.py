@@ -82,6 +82,7 @@ def _trainer_allreduce(rank, world, _):
         icap.weights.ops.call = rec
         model = tiny_model()
         t = CaptionTrainer(model, 3, 12, num_training_steps=3)
+        t.dp_overlap = False  # the single whole-buffer all-reduce path (ICAP_DP_OVERLAP=0)
         assert t.world == world and abs(t.grad_scale() - 1.0 / world) < 1e-12
         t.load_batch(*batch(3, 12))
         n = t.flat.flat_grad.numel()
@@ -113,6 +114,62 @@ def test_trainer_gradient_allreduce_world2():
         assert v["took"] and v["adamw"] and not v["bad"], v
         assert v["max_err"] < 1e-3, v
     assert out[0]["sum"] == out[1]["sum"]  # identical reduced gradient on every rank
+
+
+def _trainer_overlap(rank, world, arg):
+    """The overlapped data-parallel step: each segment of the step writes a known per-rank gradient into the flat
+    ranges it finalises, right after its real (recorded) schedule; the bucketed async all-reduces must hand the
+    optimizer the sum over ranks of every element (the 1/world is in the CE scale), and the segments' ranges must
+    tile the buffer exactly."""
+    import icap.weights
+    from dryrun import dry_run
+    from icap import CaptionTrainer
+    from test_dryrun_bounds import batch, tiny_model
+
+    mapper, freeze = arg
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model(mapper, freeze=freeze)
+        t = CaptionTrainer(model, 3, 12, num_training_steps=3)
+        assert t.dp_overlap
+        t.load_batch(*batch(3, 12))
+        n = t.flat.flat_grad.numel()
+        cover = torch.zeros(n, dtype=torch.int32)
+        orig_segments, orig_opt = t._segments, t._optimizer
+        seen = {}
+
+        def segments(zero, scale):
+            out = []
+            for rng, fn in orig_segments(zero, scale):
+                def run(rng=rng, fn=fn):
+                    fn()
+                    for lo, hi in rng:
+                        cover[lo:hi] += 1
+                        t.flat.flat_grad[lo:hi] = (torch.arange(lo, hi, dtype=torch.float32) * (rank + 1) + 7.0 * rank)
+                out.append((rng, run))
+            return out
+
+        def optimizer():
+            seen["grad_at_opt"] = t.flat.flat_grad.clone()
+            orig_opt()
+
+        t._segments, t._optimizer = segments, optimizer
+        took = t.micro_step()
+        bad = rec.check()
+        nseg = len(orig_segments(True, 1.0))
+    exp = sum(torch.arange(n, dtype=torch.float32) * (r + 1) + 7.0 * r for r in range(world))  # SUM all-reduce
+    return {"took": took, "bad": bad[:5], "segments": nseg, "cover_ok": bool((cover == 1).all()),
+            "max_err": float((seen["grad_at_opt"] - exp).abs().max())}
+
+
+@pytest.mark.parametrize("mapper,freeze", [("transformer", True), ("transformer", False), ("mlp", True)])
+def test_trainer_overlapped_bucket_allreduce_world2(mapper, freeze):
+    out = _run("_trainer_overlap", (mapper, freeze))
+    for r in range(WORLD):
+        v = out[r]
+        assert v["took"] and not v["bad"] and v["cover_ok"], v
+        assert v["segments"] == (2 if mapper == "mlp" else 1 + 2 + 1), v  # front + per layer (tiny: 2) + head
+        assert v["max_err"] < 1e-2, v
 
 
 # ---------------------------------------------------------------------------------------- 2. train() shards
