@@ -358,17 +358,23 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
   bf16_t* dOs = Vs + g.Sp16 * LDR;  // V is only read by 16-row tiles below Sp16 (skipped past it in the dQ loop)
   float* lse_s = reinterpret_cast<float*>(dOs + Sp * LDR);
   float* delta_s = lse_s + Sp;
+  uint8_t* kok_s = reinterpret_cast<uint8_t*>(delta_s + Sp);  // key allowed by the padding mask (and < S)
   const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
   const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
   const bf16_t* outp = reinterpret_cast<const bf16_t*>(p.out);
   for (int r = threadIdx.x; r < Sp; r += blockDim.x) {
     lse_s[r] = r < S ? p.lse[(int64_t)bh * S + r] : -INFINITY;
     delta_s[r] = 0.f;
+    kok_s[r] = (r < S && (p.key_mask == nullptr || p.key_mask[(int64_t)b * S + r] != 0)) ? 1 : 0;
   }
   __syncthreads();
+  // CPR a power of two (HD 64 / 128): delta[q] = sum_d dO[q][d] O[q][d] fused into the staging loop, the CPR
+  // chunk partials of a row summed across its CPR consecutive lanes (block size and the loop bound are multiples
+  // of CPR, so a row's lanes are active together); otherwise one thread per query after it. Fixed order either way.
+  constexpr bool FUSED_DELTA = (CPR & (CPR - 1)) == 0 && CPR <= 64;
   for (int idx = threadIdx.x; idx < Sp * CPR; idx += blockDim.x) {
     const int r = idx / CPR, c = idx - r * CPR;
-    uint4 q = make_uint4(0, 0, 0, 0), k = q, v = q, d = q;
+    uint4 q = make_uint4(0, 0, 0, 0), k = q, v = q, d = q, o = q;
     if (r < S) {
       const int64_t row = trow(g, b, r);
       const bf16_t* src = qkv + row * p.ld_qkv + h * HD + 8 * c;
@@ -376,31 +382,45 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
       k = *reinterpret_cast<const uint4*>(src + g.D);
       v = *reinterpret_cast<const uint4*>(src + 2 * g.D);
       d = *reinterpret_cast<const uint4*>(dout + row * p.ld_dout + h * HD + 8 * c);
+      if (FUSED_DELTA) o = *reinterpret_cast<const uint4*>(outp + row * p.ld_out + h * HD + 8 * c);
     }
     *reinterpret_cast<uint4*>(Qs + r * LDR + 8 * c) = q;
     *reinterpret_cast<uint4*>(Ks + r * LDR + 8 * c) = k;
     if (r < g.Sp16) *reinterpret_cast<uint4*>(Vs + r * LDR + 8 * c) = v;
     *reinterpret_cast<uint4*>(dOs + r * LDR + 8 * c) = d;
-  }
-  // delta[q] = sum_d dO[q][d] O[q][d], one thread per query in a fixed order (deterministic)
-  for (int r = threadIdx.x; r < S; r += blockDim.x) {
-    const int64_t row = trow(g, b, r);
-    const bf16_t* orow = outp + row * p.ld_out + h * HD;
-    const bf16_t* drow = dout + row * p.ld_dout + h * HD;
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < CPR; ++c) {
-      const uint4 o = *reinterpret_cast<const uint4*>(orow + 8 * c);
-      const uint4 d = *reinterpret_cast<const uint4*>(drow + 8 * c);
+    if constexpr (FUSED_DELTA) {
       const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, ow[4] = {o.x, o.y, o.z, o.w};
+      float part = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        acc += __uint_as_float(dw[e] << 16) * __uint_as_float(ow[e] << 16) +
-               __uint_as_float(dw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+        part += __uint_as_float(dw[e] << 16) * __uint_as_float(ow[e] << 16) +
+                __uint_as_float(dw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+#pragma unroll
+      for (int off = 1; off < CPR; off <<= 1) part += __shfl_xor(part, off, 64);
+      if (c == 0 && r < S) delta_s[r] = part;
     }
-    delta_s[r] = acc;
+  }
+  if constexpr (!FUSED_DELTA) {
+    for (int r = threadIdx.x; r < S; r += blockDim.x) {
+      const int64_t row = trow(g, b, r);
+      const bf16_t* orow = outp + row * p.ld_out + h * HD;
+      const bf16_t* drow = dout + row * p.ld_dout + h * HD;
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < CPR; ++c) {
+        const uint4 o = *reinterpret_cast<const uint4*>(orow + 8 * c);
+        const uint4 d = *reinterpret_cast<const uint4*>(drow + 8 * c);
+        const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc += __uint_as_float(dw[e] << 16) * __uint_as_float(ow[e] << 16) +
+                 __uint_as_float(dw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+      }
+      delta_s[r] = acc;
+    }
   }
   __syncthreads();
+  auto kok = [&](int q, int key) { return kok_s[key] && !(p.causal && key > q); };
   const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
   const uint64_t dbase = p.offset + (uint64_t)bh * S * S;
   bf16_t* dqkv = reinterpret_cast<bf16_t*>(p.dqkv);
@@ -435,7 +455,7 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
           const int q = qt * 16 + 4 * fg + v;
           const float lse = lse_s[q];
           float pv = 0.f;
-          if (lse != -INFINITY && key_ok(p.causal, p.key_mask, g, b, q, key)) pv = __expf(sc[v] * p.scale - lse);
+          if (lse != -INFINITY && kok(q, key)) pv = __expf(sc[v] * p.scale - lse);
           float ms = 1.f;
           if (thr && q < S && key < S) ms = drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
           pd[sub * 4 + v] = pv * ms;
@@ -497,7 +517,7 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
         for (int v = 0; v < 4; ++v) {
           const int key = kt * 16 + 4 * fg + v;
           float pv = 0.f;
-          if (lse != -INFINITY && key_ok(p.causal, p.key_mask, g, b, q, key)) pv = __expf(st[v] * p.scale - lse);
+          if (lse != -INFINITY && kok(q, key)) pv = __expf(st[v] * p.scale - lse);
           float ms = 1.f;
           if (thr && q < S && key < S) ms = drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
           ds[sub * 4 + v] = pv * (dpt[v] * ms - de);
@@ -764,7 +784,8 @@ static bool mfma_fwd2_ok(const icap_attn_args* a) {
 }
 
 size_t mfma_bwd2_lds(const amfma::Geo& g) {
-  return 2 * (3 * (size_t)g.Sp32 + (size_t)g.Sp16) * (g.hd + 8) + 2 * sizeof(float) * (size_t)g.Sp32;
+  return 2 * (3 * (size_t)g.Sp32 + (size_t)g.Sp16) * (g.hd + 8) + 2 * sizeof(float) * (size_t)g.Sp32 +
+         (size_t)g.Sp32;
 }
 
 // v2 backward: needs O (delta), 16-byte aligned row segments, and 2 * Sp16/16 waves within the launch bound

@@ -108,6 +108,21 @@ def test_inference_and_greedy_in_bounds():
         _assert_clean(rec)
 
 
+def test_negative_temperature_samples_full_softmax():
+    """src/models.py:401-407: temperature < 0 divides the logits by 1.0 and skips the top-p filter (a draw from
+    the full softmax): the decode calls icap_topp_sample with temperature 1.0 and top_p 1.0."""
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model()
+        _, _, _, emb = batch(3, 12)
+        model.generate(emb, max_length=4, temperature=-0.5, top_p=0.3)
+        _assert_clean(rec)
+        topp = [c[1] for c in rec.calls if c[0] == "icap_topp_sample"]
+    assert topp, "no sampling call"
+    for args in topp:  # (dtype, B, V, logits, ld, temperature, top_p, ...)
+        assert args[5] == 1.0 and args[6] == 1.0, args[:8]
+
+
 def test_train_grad_accum_short_last_batch_steps_like_reference(tmp_path):
     """src/train.py:128-159 with grad_accum_steps=4 over 6 batches (11 samples, batch 2: the last batch has 1
     sample and runs on its own trainer): optimizer steps after batches 4 and 6 only — 2 AdamW calls per epoch —
