@@ -66,7 +66,7 @@ class GemmTimer:
         return agg
 
 
-def build(B, dev, dropout=True, config="small"):
+def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16):
     """config "small": BASELINE configs[1] (GPT-2 small + CLIP ViT-B/32); "medium": configs[3] (GPT-2 medium +
     CLIP ViT-L/14 encoder on the device, mapper at gpt_dim 1024 / CLIP-L embed 768)."""
     from types import SimpleNamespace
@@ -84,11 +84,31 @@ def build(B, dev, dropout=True, config="small"):
         mapper = TransformerMappingNetwork.random_init(seed=0)
         tower_cfg = None
     model = ImageCaptioningModel(mapper, tokenizer=SimpleNamespace(eos_token_id=50256), gpt=gpt,
-                                 compute_dtype=torch.bfloat16).to(dev)
+                                 compute_dtype=dtype).to(dev)
     tower = CLIPVisionTower.random_init(tower_cfg, seed=0).to(dev)
     trainer = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10 ** 6, clip_model=tower, dropout=dropout,
                              seed=1234)
     return model, tower, trainer
+
+
+def parity_mode_rate(B, dev, steps=5):
+    """The same train step in the fp32 parity mode (every GEMM an exact-fp32 MFMA chain, fp32 activations: the
+    mode the reference goldens are matched in to 1e-5), images/s over `steps` graph-replayed steps."""
+    model, tower, trainer = build(B, dev, dtype=torch.float32)
+    ids, mask, labels, px = synthetic_batch(B, 1, dev)
+    trainer.load_batch(ids, mask, labels, pixels=px)
+    for _ in range(2):
+        trainer.micro_step(use_graph=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.micro_step(use_graph=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    del model, tower, trainer
+    torch.cuda.empty_cache()
+    return {"images_per_s": round(B * steps / el, 2), "ms_per_step": round(el / steps * 1e3, 3), "steps": steps,
+            "dtype": "fp32 (parity mode: 16x16x4 f32 MFMA)"}
 
 
 def synthetic_batch(B, seed, dev):
@@ -449,6 +469,7 @@ def main():
     traffic, traffic_src = pmc_traffic(dom) if args.config == "small" else (None, None)
     prep = None if args.no_decode else preprocess_rate(dev)
     extract = extraction_child() if (not args.no_decode and args.config == "small" and rank == 0) else None
+    parity = parity_mode_rate(B, dev) if (not args.no_decode and args.config == "small" and world == 1) else None
 
     if rank == 0:
         res = {
@@ -475,6 +496,7 @@ def main():
             "topp_sampling": topp,
             "clip_preprocess": prep,
             "clip_extraction": extract,
+            "fp32_parity_mode": parity,
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1),
                          "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
                          "traffic": traffic, "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE)",

@@ -188,6 +188,102 @@ __global__ __launch_bounds__(256) void ce_kernel(int64_t V, const T* __restrict_
   }
 }
 
+// bf16 logits, V <= 8 * 512 * R: the row is read from HBM ONCE into registers (R 16-byte groups per thread, all in
+// flight together), then the block's online max / sum-exp and the dlogits pass both run from the registers
+// (the two-pass kernel above reads the row twice: r01 PMC 541 MB per launch against 360 MB algorithmic).
+template <int R>
+__global__ __launch_bounds__(512) void ce_bf16_reg_kernel(int64_t V, const bf16_t* __restrict__ logits, int64_t ld,
+                                                         const int32_t* __restrict__ labels,
+                                                         const int32_t* __restrict__ n_valid,
+                                                         float* __restrict__ loss_rows, bf16_t* dlogits,
+                                                         float grad_scale, const int32_t* __restrict__ rows_dev) {
+  constexpr int NT = 512, NW = NT / 64;
+  __shared__ float redm[NW], reds[NW];
+  const int64_t r = blockIdx.x;
+  if (rows_dev && r >= *rows_dev) return;
+  const int y = labels[r];
+  const bf16_t* x = logits + r * ld;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t V8 = V >> 3;
+  if (y < 0) {
+    if (tid == 0) loss_rows[r] = 0.f;
+    if (dlogits) {
+      bf16_t* dx = dlogits + r * ld;
+      for (int64_t g = tid; g < (ld >> 3); g += NT) *reinterpret_cast<uint4*>(dx + 8 * g) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    return;
+  }
+  uint4 wv[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int64_t g = tid + (int64_t)i * NT;
+    wv[i] = g < V8 ? *reinterpret_cast<const uint4*>(x + 8 * g) : make_uint4(0xff80ff80u, 0xff80ff80u, 0xff80ff80u,
+                                                                                  0xff80ff80u);  // -inf padding
+  }
+  float m = -INFINITY, s = 0.f;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    float v[8];
+    const uint32_t h[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[2 * e] = __uint_as_float(h[e] << 16);
+      v[2 * e + 1] = __uint_as_float(h[e] & 0xffff0000u);
+    }
+    float mx = v[0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) mx = fmaxf(mx, v[e]);
+    if (mx > m) { s *= __expf(m - mx); m = mx; }
+    if (m != -INFINITY) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += __expf(v[e] - m);
+    }
+  }
+  for (int64_t j = 8 * V8 + tid; j < V; j += NT) {  // the last V % 8 logits
+    const float v = bf2f(x[j]);
+    if (v > m) { s *= __expf(m - v); m = v; }
+    s += __expf(v - m);
+  }
+  const float bm = wave_max(m);
+  s = (m == -INFINITY) ? 0.f : s * __expf(m - bm);
+  s = wave_sum(s);
+  if (lane == 0) { redm[w] = bm; reds[w] = s; }
+  __syncthreads();
+  float M = redm[0];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) M = fmaxf(M, redm[k]);
+  float Ssum = 0.f;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) Ssum += reds[k] * __expf(redm[k] - M);
+  const float lse = M + logf(Ssum);
+  if (tid == 0) loss_rows[r] = lse - bf2f(x[y]);
+  if (dlogits) {
+    const float sc = grad_scale / (float)(*n_valid);
+    bf16_t* dx = dlogits + r * ld;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int64_t g = tid + (int64_t)i * NT;
+      if (g < V8) {
+        const uint32_t h[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
+        uint32_t o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t j = 8 * g + 2 * e;
+          const float a = (__expf(__uint_as_float(h[e] << 16) - lse) - (j == y ? 1.f : 0.f)) * sc;
+          const float b2 = (__expf(__uint_as_float(h[e] & 0xffff0000u) - lse) - (j + 1 == y ? 1.f : 0.f)) * sc;
+          o[e] = f2bf2(a, b2);
+        }
+        *reinterpret_cast<uint4*>(dx + 8 * g) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+    for (int64_t j = 8 * V8 + tid; j < ld; j += NT) {  // V % 8 tail and the padding columns
+      float v = 0.f;
+      if (j < V) v = (__expf(bf2f(x[j]) - lse) - (j == y ? 1.f : 0.f)) * sc;
+      dx[j] = f2bf(v);
+    }
+  }
+}
+
 __global__ void ce_reduce_kernel(int64_t rows, const float* __restrict__ loss_rows, const int32_t* n_valid,
                                  float* loss, const int32_t* __restrict__ rows_dev) {
   __shared__ double red[256];
@@ -909,8 +1005,17 @@ extern "C" int icap_cross_entropy(int32_t dtype, int64_t rows, int64_t V, const 
   if (rows <= 0) return ICAP_OK;
   ICAP_REQUIRE(rows < (1ll << 31), "icap_cross_entropy: too many rows");
   float* lrows = reinterpret_cast<float*>(workspace);
-  DISPATCH_T(dtype, hipLaunchKernelGGL(ce_kernel<T>, dim3((unsigned)rows), dim3(256), 0, S_(stream), V, CTP(logits),
-                                       ld, labels, n_valid, lrows, TP(dlogits), grad_scale, rows_dev));
+  const bool reg = dtype == ICAP_BF16 && V <= 8 * 512 * 13 && ld % 8 == 0 &&
+                   (reinterpret_cast<uintptr_t>(logits) & 15) == 0 &&
+                   (dlogits == nullptr || (reinterpret_cast<uintptr_t>(dlogits) & 15) == 0);
+  if (reg) {
+    hipLaunchKernelGGL(ce_bf16_reg_kernel<13>, dim3((unsigned)rows), dim3(512), 0, S_(stream), V,
+                       reinterpret_cast<const bf16_t*>(logits), ld, labels, n_valid, lrows,
+                       reinterpret_cast<bf16_t*>(dlogits), grad_scale, rows_dev);
+  } else {
+    DISPATCH_T(dtype, hipLaunchKernelGGL(ce_kernel<T>, dim3((unsigned)rows), dim3(256), 0, S_(stream), V, CTP(logits),
+                                         ld, labels, n_valid, lrows, TP(dlogits), grad_scale, rows_dev));
+  }
   int rc = check_launch("icap_cross_entropy");
   if (rc) return rc;
   hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(256), 0, S_(stream), rows, lrows, n_valid, loss, rows_dev);
