@@ -127,6 +127,19 @@ def test_tiny_mlp_mapper(dev):
     assert rel(out.logits, g["logits"]) < 1e-4
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_tiny_mlp_fused_train_matches_reference(dev, graph):
+    """MLPMappingNetwork trained through the fused trainer (tanh-epilogue forward, dtanh backward, dW / bias grads,
+    AdamW) vs 3 steps of the reference train() with that mapper (src/models.py:14-74, train.py:119-166)."""
+    g = load("tiny_mlp")
+    mc = O.MLPMapperCfg(prefix_length=5, embed_dim=64, gpt_dim=128)
+    model = build(TINY_G, mc, torch.float32, dev, mapper="mlp")
+    init = {k: v.detach().clone().cpu() for k, v in model.mapping_network.state_dict().items()}
+    losses, _ = _trainer_steps(model, inputs(g, dev), len(g["train_losses"]), graph=graph)
+    assert rel(losses, g["train_losses"]) < 1e-5
+    _check_updates(model, g, init)
+
+
 def _trainer_steps(model, batch, n, graph=False):
     ids, mask, labels, emb = batch
     t = CaptionTrainer(model, ids.shape[0], ids.shape[1], lr=1e-4, num_training_steps=n, dropout=False)

@@ -162,10 +162,14 @@ def golden_mlp(workdir):
     with torch.no_grad():
         res = model.forward(caption_token_ids=ids, image_embeddings=emb, attention_mask=mask, labels=labels)
         prefix = model.mapping_network(emb)
+    # 3 reference train() steps through the MLP mapper (GPT-2 frozen): losses + every trained tensor
+    model2, _, msd = build_ref(gcfg, mcfg, 0, mapper="mlp")
+    losses = run_ref_train(model2, (ids, mask, labels, emb), 3, 1e-4, True, workdir)
+    trained = {"trained." + k: v.detach().numpy() for k, v in model2.mapping_network.state_dict().items()}
     np.savez_compressed(os.path.join(OUT, "tiny_mlp.npz"), ids=ids.numpy(), mask=mask.numpy(),
                         labels=labels.numpy(), emb=emb.numpy(), prefix=prefix.numpy(), loss=np.array([res.loss.item()]),
-                        logits=res.logits.numpy())
-    print("tiny_mlp loss", res.loss.item())
+                        logits=res.logits.numpy(), train_losses=np.array(losses), **trained)
+    print("tiny_mlp loss", res.loss.item(), "train", losses)
 
 
 def golden_clip():
@@ -370,6 +374,7 @@ def main():
         if not only or "tiny" in only:
             golden_config("tiny", tiny_g, tiny_m, B=3, L=12, real=7, gen_B=3, gen_len=20, logit_rows=[4, 10, 16],
                           train_steps=3, unfrozen_steps=2, workdir=work, full_logits=True)
+        if not only or "tiny" in only or "mlp" in only:
             golden_mlp(work)
         if not only or "small" in only:
             golden_config("small", O.GPT2Cfg(), O.MapperCfg(), B=4, L=50, real=13, gen_B=2, gen_len=12,
