@@ -757,10 +757,6 @@ __device__ __forceinline__ void ds_w32(uint32_t a, float x) {
 #define ICAP_RING_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
 }  // namespace ring
 
-// ICAP_RING_ABL (diagnostic builds only, tools/ring_ablation.sh): 1 = no MFMA, 2 = no LDS-DMA, 3 = no fragment reads
-#ifndef ICAP_RING_ABL
-#define ICAP_RING_ABL 0
-#endif
 template <int WM, int NSLOT>
 __global__ __launch_bounds__(128 * WM, 1) void gemm_ring_kernel(icap_gemm_args p, int tiles_m, int tiles_n, int nunits,
                                                                  uint32_t drop_thresh, float inv_keep) {
@@ -826,18 +822,16 @@ __global__ __launch_bounds__(128 * WM, 1) void gemm_ring_kernel(icap_gemm_args p
       dma16(brs, smem + NSLOT * SLOT + (pbias * NW + wave) * 1024,
             lane < 16 ? (uint32_t)((pn0 + wn * 64) * 4 + 16 * lane) : OOB);
     }
-    if (ICAP_RING_ABL != 2) {
 #pragma unroll
-      for (int i = 0; i < APW; ++i) {
-        const int pc = wave * APW + i;
-        dma16s(pra, st + pc * 8 * GROWB, va, __builtin_amdgcn_readfirstlane((uint32_t)pc * lda8 + (uint32_t)(k0 * 2)));
-      }
+    for (int i = 0; i < APW; ++i) {
+      const int pc = wave * APW + i;
+      dma16s(pra, st + pc * 8 * GROWB, va, __builtin_amdgcn_readfirstlane((uint32_t)pc * lda8 + (uint32_t)(k0 * 2)));
+    }
 #pragma unroll
-      for (int j = 0; j < BPW; ++j) {
-        const int pc = wave * BPW + j;
-        dma16s(prb, st + BM * GROWB + pc * 8 * GROWB, vb,
-               __builtin_amdgcn_readfirstlane((uint32_t)pc * ldb8 + (uint32_t)(k0 * 2)));
-      }
+    for (int j = 0; j < BPW; ++j) {
+      const int pc = wave * BPW + j;
+      dma16s(prb, st + BM * GROWB + pc * 8 * GROWB, vb,
+             __builtin_amdgcn_readfirstlane((uint32_t)pc * ldb8 + (uint32_t)(k0 * 2)));
     }
     ++prod;
     pslot = pslot + 1 == NSLOT ? 0 : pslot + 1;
@@ -880,7 +874,6 @@ __global__ __launch_bounds__(128 * WM, 1) void gemm_ring_kernel(icap_gemm_args p
   // accumulators through slot g (free then); R0 then already holds the next unit's first half.
   u32x4_t R0[8], R1[8];
   auto read_half = [&](u32x4_t (&R)[8], int slot, int ks) __attribute__((always_inline)) {
-    if (ICAP_RING_ABL == 3) return;
     const uint32_t a = smem_base + (uint32_t)(slot * SLOT) + la[ks], b = smem_base + (uint32_t)(slot * SLOT) + lb[ks];
     asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(R[0]) : "v"(a));
     asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(R[1]) : "v"(a));
@@ -921,8 +914,7 @@ __global__ __launch_bounds__(128 * WM, 1) void gemm_ring_kernel(icap_gemm_args p
     auto mma_half = [&](u32x4_t (&R)[8], int from, int to) __attribute__((always_inline)) {
 #pragma unroll
       for (int q = from; q < to; ++q) {
-        if (ICAP_RING_ABL == 1) asm volatile("" ::"v"(R[q >> 2]), "v"(R[4 + (q & 3)]));
-        else mfma_chunk<bf16_t>(acc[q >> 2][q & 3], __builtin_bit_cast(uint4, R[q >> 2]), __builtin_bit_cast(uint4, R[4 + (q & 3)]));
+        mfma_chunk<bf16_t>(acc[q >> 2][q & 3], __builtin_bit_cast(uint4, R[q >> 2]), __builtin_bit_cast(uint4, R[4 + (q & 3)]));
       }
     };
     for (int kt = 0; kt < nk; ++kt) {

@@ -25,13 +25,9 @@ __device__ __forceinline__ void mfma_chunk(f32x4_t& acc, const uint4& a, const u
 
 template <>
 __device__ __forceinline__ void mfma_chunk<bf16_t>(f32x4_t& acc, const uint4& a, const uint4& b) {
-#ifdef ICAP_GEMM_NO_MFMA  // diagnostic build only (tools/ab_gemm.sh): the staging pipeline without the MFMAs
-  acc[0] += __uint_as_float((a.x ^ b.x) & 0x3f800000u);
-#else
   bf16x8_t av = __builtin_bit_cast(bf16x8_t, a);
   bf16x8_t bv = __builtin_bit_cast(bf16x8_t, b);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
-#endif
 }
 template <>
 __device__ __forceinline__ void mfma_chunk<float>(f32x4_t& acc, const uint4& a, const uint4& b) {

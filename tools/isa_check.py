@@ -4,7 +4,7 @@ import re
 import sys
 
 s = open(sys.argv[1]).read()
-pat = sys.argv[2] if len(sys.argv) > 2 else "gemm8p"
+pat = sys.argv[2] if len(sys.argv) > 2 else "gemm256"
 pw = re.compile(r"vmcnt\(\d+\)")
 for name in re.findall(r"^(_ZN4icap\w+):", s, re.M):
     if pat not in name:
