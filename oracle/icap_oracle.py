@@ -358,6 +358,79 @@ def greedy_generate(gpt_sd, gcfg: GPT2Cfg, prefix: Tensor, max_length: int = 50)
     return torch.cat(out, dim=1)
 
 
+# --------------------------------------------------------------------------- beam search (f4)
+
+
+BEAM_NEG = -1.0e9  # the library's "impossible" score (HF/generation/utils.py:3319-3320,3147)
+
+
+@torch.no_grad()
+def beam_generate(gpt_sd, gcfg: GPT2Cfg, prefix: Tensor, max_length: int, num_beams: int = 4,
+                  length_penalty: float = 1.0) -> Tensor:
+    """Beam search over the caption prefix, as GPT2LMHeadModel.generate(inputs_embeds=prefix, num_beams=W,
+    max_new_tokens=max_length, do_sample=False, early_stopping=False, pad_token_id=eos) runs it
+    (HF/generation/utils.py:3208-3540, helpers :3008-3206; the reference has no beam search, SURVEY.md §8f
+    row f4, so HF's is the pinned definition). Full recompute per step (no KV cache), fp32.
+
+    Per caption and step t (t = tokens generated before this step; the prompt is embeddings only, so the
+    decoder prompt length is 0):
+      - candidates: log_softmax(last logits) of each running beam + its running score, the top 2W over W x V
+        (:3077-3129; ties: lower beam*V + token first);
+      - a candidate "hits" when its token is EOS or t + 1 == max_length (EOS + max-length stopping criteria);
+      - running beams of step t+1: the top W candidates after -1e9 on hitting ones (:3131-3151);
+      - finished: the hitting candidates among the first W, scored score / (t + 1) ** length_penalty, merged
+        with the kept ones (best W), unless the caption is already done (:3153-3206);
+      - done (sticky): all W finished slots are filled and the best running score / (t + 1) ** lp is not above
+        the worst finished score (:3008-3053, early_stopping=False).
+    Stops when every caption is done or at max_length. Returns, per caption, its best finished sequence (EOS
+    included when it ended on one), right-padded with EOS to the longest one in the batch (:3512-3523)."""
+    B, P, D = prefix.shape
+    W, eos, V = num_beams, gcfg.eos, gcfg.vocab_size
+    wte = gpt_sd["transformer.wte.weight"]
+    run_seq = [[[] for _ in range(W)] for _ in range(B)]
+    run_score = [[0.0] + [BEAM_NEG] * (W - 1) for _ in range(B)]
+    fin = [[] for _ in range(B)]  # per caption: [(score, seq)], best first, at most W
+    done = [False] * B
+    for t in range(max_length):
+        rows = []
+        for b in range(B):
+            for i in range(W):
+                toks = torch.tensor(run_seq[b][i], dtype=torch.long)
+                rows.append(torch.cat((prefix[b].float(), wte[toks].float()), dim=0))
+        _, logits = gpt2_forward(gpt_sd, gcfg, torch.stack(rows))
+        logp = F.log_softmax(logits[:, -1, :V].float(), dim=-1).view(B, W, V)
+        for b in range(B):
+            acc = (logp[b] + torch.tensor(run_score[b], dtype=torch.float32)[:, None]).reshape(-1)
+            order = _topk_lowidx(acc, 2 * W)
+            cands = [(float(acc[j]), j // V, j % V) for j in order]
+            hits = [tok == eos or t + 1 == max_length for _, _, tok in cands]
+            keep = sorted(range(2 * W), key=lambda j: (-(cands[j][0] + (BEAM_NEG if hits[j] else 0.0)), j))[:W]
+            if not done[b]:
+                new = [(s / float(t + 1) ** length_penalty, run_seq[b][bm] + [tok])
+                       for j, (s, bm, tok) in enumerate(cands) if j < W and hits[j]]
+                fin[b] = sorted(fin[b] + new, key=lambda e: -e[0])[:W]  # stable: kept entries win ties
+            run_seq[b] = [run_seq[b][cands[j][1]] + [cands[j][2]] for j in keep]
+            run_score[b] = [cands[j][0] + (BEAM_NEG if hits[j] else 0.0) for j in keep]
+            if not done[b] and len(fin[b]) == W and \
+                    run_score[b][0] / float(t + 1) ** length_penalty <= min(s for s, _ in fin[b]):
+                done[b] = True
+        if all(done):
+            break
+    best = [fin[b][0][1] if fin[b] else run_seq[b][0] for b in range(B)]
+    n = max(len(s) for s in best)
+    out = torch.full((B, n), eos, dtype=torch.long)
+    for b, s in enumerate(best):
+        out[b, : len(s)] = torch.tensor(s, dtype=torch.long)
+    return out
+
+
+def _topk_lowidx(x: Tensor, k: int):
+    """Indices of the k largest entries of a 1-D fp32 tensor, ties -> lower index first."""
+    thr = torch.topk(x, min(x.numel(), k)).values[-1]
+    pool = torch.nonzero(x >= thr).flatten().tolist()  # every entry tied with the k-th is a candidate
+    return sorted(pool, key=lambda j: (-float(x[j]), j))[:k]
+
+
 # --------------------------------------------------------------------------- top-p sampling (a14)
 
 

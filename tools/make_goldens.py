@@ -291,6 +291,55 @@ def golden_topp():
     print("topp steps", len(probs_log), "kept per row", (torch.stack(probs_log) > 0).sum(-1)[0].tolist())
 
 
+def hf_beam(gcfg, gsd, prefix, max_new, num_beams=4):
+    """transformers' own beam search (GPT2LMHeadModel.generate, HF/generation/utils.py:3208-3540) on the
+    caption prefix: the definition the device beam search and oracle.beam_generate are pinned to (the reference
+    itself has greedy / top-p only, src/models.py:327-477)."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+
+    hf = GPT2Config(vocab_size=gcfg.vocab_size, n_positions=gcfg.n_positions, n_embd=gcfg.n_embd,
+                    n_layer=gcfg.n_layer, n_head=gcfg.n_head, resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=0.0,
+                    layer_norm_epsilon=gcfg.eps, bos_token_id=gcfg.eos, eos_token_id=gcfg.eos)
+    gpt = GPT2LMHeadModel(hf)
+    gpt.load_state_dict(gsd, strict=False)
+    gpt.tie_weights()
+    gpt.eval()
+    with torch.no_grad():
+        return gpt.generate(inputs_embeds=prefix, attention_mask=torch.ones(prefix.shape[:2], dtype=torch.long),
+                            num_beams=num_beams, max_new_tokens=max_new, do_sample=False, early_stopping=False,
+                            length_penalty=1.0, num_return_sequences=1, pad_token_id=gcfg.eos,
+                            eos_token_id=gcfg.eos)
+
+
+def golden_beam():
+    """Beam-4 ids from transformers' generate on the tiny and small goldens' prefixes.
+    `eos_scale` multiplies wte[eos] (the tied LM-head row) so captions finish at different steps and the
+    finished-hypothesis / early-stop paths are exercised; 1.0 = the plain weights."""
+    out = {}
+    tiny_g = O.GPT2Cfg(n_layer=2, n_embd=128, n_head=2, vocab_size=512, n_positions=128, eos=511)
+    tiny = np.load(os.path.join(OUT, "tiny.npz"))
+    small = np.load(os.path.join(OUT, "small.npz"))
+    # the tiny golden's 3 mapper prefixes + 5 seeded ones of the same scale (more captions, more finishing steps)
+    g = torch.Generator().manual_seed(11)
+    extra = torch.randn((5,) + tiny["prefix"].shape[1:], generator=g) * float(tiny["prefix"].std())
+    tiny_pre = np.concatenate([tiny["prefix"], extra.numpy()]).astype(np.float32)
+    for tag, gcfg, pre, L, scales in (("tiny", tiny_g, tiny_pre, 20, (1.0, 4.0, 5.0, 6.0)),
+                                      ("small", O.GPT2Cfg(), small["prefix"][:2], 12, (1.0, 3.0, 4.0))):
+        for s in scales:
+            gsd = O.gpt2_state_dict(gcfg, 0)
+            gsd["transformer.wte.weight"] = gsd["transformer.wte.weight"].clone()
+            gsd["transformer.wte.weight"][gcfg.eos] *= s
+            ids = hf_beam(gcfg, gsd, torch.from_numpy(pre), L)
+            k = f"{tag}_s{s:g}"
+            out[k + "_ids"] = ids.numpy()
+            out[k + "_scale"] = np.array([s])
+            n_eos = [(int((r == gcfg.eos).nonzero()[0][0]) + 1 if (r == gcfg.eos).any() else -1) for r in ids]
+            print("beam", k, tuple(ids.shape), "eos at", n_eos)
+    out["tiny_prefix"] = tiny_pre
+    out["small_prefix"] = small["prefix"][:2]
+    np.savez_compressed(os.path.join(OUT, "beam4.npz"), **out)
+
+
 def golden_small_train(workdir):
     """GPT-2 small + transformer mapper: 3 frozen train() steps with the trained mapper tensors kept whole (bf16
     update-direction tests), 2 unfrozen steps (every GPT-2 tensor's checksum), and greedy decode at the
@@ -387,6 +436,8 @@ def main():
             golden_clip_l14()
         if not only or "topp" in only:
             golden_topp()
+        if not only or "beam" in only:
+            golden_beam()
         if not only or "small_train" in only:
             golden_small_train(work)
         if not only or "medium" in only:
