@@ -207,8 +207,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(icap_attn_args p, AttnGeo
 // one wave per (b, h); keys 0..pos from the position-major cache
 template <typename T>
 __global__ __launch_bounds__(64) void attn_decode_kernel(int B, int H, int hd, int pos, const T* __restrict__ cache,
-                                                        int64_t ld, T* __restrict__ out, int64_t ld_out,
-                                                        float scale) {
+                                                        int64_t ld, const int32_t* __restrict__ anc,
+                                                        T* __restrict__ out, int64_t ld_out, float scale) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* q = sm;            // hd
   float* sc = sm + 128;     // pos+1 scores
@@ -221,8 +221,10 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(int B, int H, int hd, i
   for (int d = lane; d < hd; d += 64) q[d] = io<T>::ld(qrow + d) * scale;
   __syncthreads();
   float m = -INFINITY;
+  // row of key j: this row's own (b) or, in beam search, the cache row its history holds position j in
+  auto src = [&](int j) -> int64_t { return anc ? (int64_t)anc[(int64_t)j * B + b] : (int64_t)b; };
   for (int j = lane; j < n; j += 64) {
-    const T* krow = cache + ((int64_t)j * B + b) * ld + D + h * hd;
+    const T* krow = cache + ((int64_t)j * B + src(j)) * ld + D + h * hd;
     float a = 0.f;
     for (int d = 0; d < hd; d += 4) {
       float kv[4];
@@ -247,7 +249,7 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(int B, int H, int hd, i
   const float inv = 1.f / l;
   for (int d = lane; d < hd; d += 64) {
     float a = 0.f;
-    for (int j = 0; j < n; ++j) a = fmaf(sc[j], io<T>::ld(cache + ((int64_t)j * B + b) * ld + 2 * D + h * hd + d), a);
+    for (int j = 0; j < n; ++j) a = fmaf(sc[j], io<T>::ld(cache + ((int64_t)j * B + src(j)) * ld + 2 * D + h * hd + d), a);
     io<T>::st(out + (int64_t)b * ld_out + h * hd + d, a * inv);
   }
 }
@@ -258,8 +260,8 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(int B, int H, int hd, i
 // 16-byte column chunk dc = lane%8) for P.V, the 8 key groups summed with cross-lane adds at the end.
 template <int TV>
 __global__ __launch_bounds__(64) void attn_decode64_kernel(int B, int H, int pos, const bf16_t* __restrict__ cache,
-                                                          int64_t ld, bf16_t* __restrict__ out, int64_t ld_out,
-                                                          float scale) {
+                                                          int64_t ld, const int32_t* __restrict__ anc,
+                                                          bf16_t* __restrict__ out, int64_t ld_out, float scale) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* q = sm;         // 64
   float* sc = sm + 64;   // pos + 1 scores
@@ -270,11 +272,13 @@ __global__ __launch_bounds__(64) void attn_decode64_kernel(int B, int H, int pos
   const int n = pos + 1;
   const int64_t rs = (int64_t)B * ld;  // elements from one position's row to the next
   const bf16_t* base = cache + (int64_t)b * ld + h * 64;
+  // key j's row (relative to base): this row's own or, in beam search, the cache row holding its position j
+  auto koff = [&](int j) -> int64_t { return j * rs + (anc ? ((int64_t)anc[(int64_t)j * B + b] - b) * ld : 0); };
   uint4 vr[TV];
 #pragma unroll
   for (int t = 0; t < TV; ++t) {
     const int j = kg + 8 * t;
-    vr[t] = j < n ? *reinterpret_cast<const uint4*>(base + j * rs + 2 * D + dc * 8) : make_uint4(0u, 0u, 0u, 0u);
+    vr[t] = j < n ? *reinterpret_cast<const uint4*>(base + koff(j) + 2 * D + dc * 8) : make_uint4(0u, 0u, 0u, 0u);
   }
   if (lane < 8) {
     float v[8];
@@ -285,7 +289,7 @@ __global__ __launch_bounds__(64) void attn_decode64_kernel(int B, int H, int pos
   __syncthreads();
   float m = -INFINITY;
   for (int j = lane; j < n; j += 64) {
-    const bf16_t* kr = base + j * rs + D;
+    const bf16_t* kr = base + koff(j) + D;
     uint4 kk[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) kk[c] = *reinterpret_cast<const uint4*>(kr + 8 * c);
@@ -332,7 +336,7 @@ __global__ __launch_bounds__(64) void attn_decode64_kernel(int B, int H, int pos
     if (j < n) add_row(vr[t], sc[j]);
   }
   for (int j = 8 * TV + kg; j < n; j += 8)  // keys past the prefetched ones (caches longer than 8*TV)
-    add_row(*reinterpret_cast<const uint4*>(base + j * rs + 2 * D + dc * 8), sc[j]);
+    add_row(*reinterpret_cast<const uint4*>(base + koff(j) + 2 * D + dc * 8), sc[j]);
 #pragma unroll
   for (int o = 8; o < 64; o <<= 1)
 #pragma unroll
@@ -437,9 +441,9 @@ extern "C" int icap_attention_bwd(const icap_attn_args* a, void* stream) {
   return check_launch("icap_attention_bwd");
 }
 
-extern "C" int icap_attention_decode(int32_t dtype, int32_t B, int32_t H, int32_t hd, int32_t pos,
-                                     const void* cache, int64_t ld_cache, void* out, int64_t ld_out,
-                                     float scale, void* stream) {
+extern "C" int icap_attention_decode_anc(int32_t dtype, int32_t B, int32_t H, int32_t hd, int32_t pos,
+                                         const void* cache, int64_t ld_cache, const int32_t* anc, void* out,
+                                         int64_t ld_out, float scale, void* stream) {
   ICAP_REQUIRE(hd > 0 && hd <= 128 && hd % 4 == 0, "icap_attention_decode: hd must be <= 128, multiple of 4");
   ICAP_REQUIRE(pos >= 0 && pos < 4096, "icap_attention_decode: pos out of range");
   ICAP_REQUIRE(cache && out, "icap_attention_decode: null pointer");
@@ -450,15 +454,21 @@ extern "C" int icap_attention_decode(int32_t dtype, int32_t B, int32_t H, int32_
   if (dtype == ICAP_BF16 && hd == 64 && al && ld_cache % 8 == 0 && ld_out % 8 == 0) {
     const size_t lds = sizeof(float) * (64 + (size_t)pos + 1);
     hipLaunchKernelGGL(attn_decode64_kernel<16>, grid, block, lds, s, B, H, pos, (const bf16_t*)cache, ld_cache,
-                       (bf16_t*)out, ld_out, scale);
+                       anc, (bf16_t*)out, ld_out, scale);
     return check_launch("icap_attention_decode");
   }
   const size_t lds = sizeof(float) * (128 + (size_t)pos + 1);
   if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(attn_decode_kernel<bf16_t>, grid, block, lds, s, B, H, hd, pos, (const bf16_t*)cache, ld_cache,
-                       (bf16_t*)out, ld_out, scale);
+                       anc, (bf16_t*)out, ld_out, scale);
   else
     hipLaunchKernelGGL(attn_decode_kernel<float>, grid, block, lds, s, B, H, hd, pos, (const float*)cache, ld_cache,
-                       (float*)out, ld_out, scale);
+                       anc, (float*)out, ld_out, scale);
   return check_launch("icap_attention_decode");
+}
+
+extern "C" int icap_attention_decode(int32_t dtype, int32_t B, int32_t H, int32_t hd, int32_t pos,
+                                     const void* cache, int64_t ld_cache, void* out, int64_t ld_out,
+                                     float scale, void* stream) {
+  return icap_attention_decode_anc(dtype, B, H, hd, pos, cache, ld_cache, nullptr, out, ld_out, scale, stream);
 }

@@ -78,6 +78,19 @@ class AdamWArgs(C.Structure):
     ]
 
 
+class BeamArgs(C.Structure):
+    _fields_ = [
+        ("B", i32), ("W", i32), ("V", i32), ("max_len", i32),
+        ("eos", i32), ("length_penalty", f32),
+        ("K", i32),
+        ("T", i32),
+        ("top_val", vp), ("top_idx", vp), ("top_m", vp), ("top_ls", vp),
+        ("ws", vp),
+        ("dtype", i32), ("D", i32), ("n_positions", i32),
+        ("wte", vp), ("wpe", vp), ("x", vp),
+    ]
+
+
 # name -> (restype, argtypes); must mirror include/icap.h exactly
 SIGNATURES = {
     "icap_last_error": (C.c_char_p, []),
@@ -92,6 +105,12 @@ SIGNATURES = {
     "icap_attention_fwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_bwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_decode": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, i64, f32, vp]),
+    "icap_attention_decode_anc": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, vp, i64, f32, vp]),
+    "icap_beam_workspace_bytes": (C.c_size_t, [i32, i32, i32, i32]),
+    "icap_beam_init": (C.c_int, [C.POINTER(BeamArgs), i32, vp]),
+    "icap_beam_rowtop": (C.c_int, [i32, i64, i64, vp, i64, i32, vp, vp, vp, vp, vp]),
+    "icap_beam_update": (C.c_int, [C.POINTER(BeamArgs), i32, i32, vp]),
+    "icap_beam_finalize": (C.c_int, [C.POINTER(BeamArgs), vp, vp, vp]),
     "icap_gpt2_embed": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, vp, f32, u64, u64, vp, vp]),
     "icap_embedding_scatter_add": (C.c_int, [i32, i32, i32, i32, i32, vp, vp, vp, vp]),
     "icap_caption_prep": (C.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),

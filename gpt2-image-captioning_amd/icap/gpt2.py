@@ -534,7 +534,8 @@ class GPT2Core:
             if prefill:
                 ops.attention_fwd(ds.cache[l], o, B=B, S=npos, H=H, hd=hd, scale=scale, causal=True, rsb=1, rss=B)
             else:
-                ops.attention_decode(ds.cache[l], o, B=B, H=H, hd=hd, pos=pos0, scale=scale)
+                ops.attention_decode(ds.cache[l], o, B=B, H=H, hd=hd, pos=pos0, scale=scale,
+                                     anc=getattr(ds, "anc", None))
             ops.gemm(o, lw.w_proj_t, h1, bias=lw.b_proj, resid=x, M=rows)
             if fuse_ln:
                 ops.gemm(h1, lw.w_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows, ln=(lw.ln2_g, lw.ln2_b, self.eps))
@@ -638,6 +639,122 @@ class GPT2Core:
             self._decode_head(ds, ds.x[:B], s, pos + 1, samp)
             steps = s + 1
         return self._truncate(ds.tokens[:, :steps], steps)
+
+
+    # -- beam search (transformers' generate(num_beams=W), HF/generation/utils.py:3208-3540)
+    def alloc_beam(self, B: int, W: int, P: int, max_length: int, length_penalty: float = 1.0) -> SimpleNamespace:
+        """Decode buffers for R = B*W rows (row b*W + i = beam i of caption b) + the beam state; the KV cache
+        is read through the state's ancestry table."""
+        ds = self.alloc_decode(B * W, P, max_length)
+        ds.beam = ops.BeamState(B, W, self.V, max_length, ds.T, self.cfg.eos_token_id, length_penalty, self.dev)
+        ds.beam.set_embedding(self.dtype, self.D, self.cfg.n_positions, self.wte, self.wpe, None)
+        ds.anc = ds.beam.anc
+        ds.W = W
+        return ds
+
+    def _beam_head(self, ds, x_last: Tensor, step: int, pos: int) -> None:
+        """ln_f + LM head on every row's last position, then one beam step (icap_beam_rowtop + icap_beam_update:
+        candidates, running / finished beams, ancestry, next input rows)."""
+        R = ds.B
+        a = ds.a[:R]
+        ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=R)
+        ops.gemm(a, self.wte, ds.logits, M=R, alg_flops=2.0 * R * self.V * self.D)
+        nxt_x = ds.x[:R] if pos + 1 < ds.T else None
+        ds.beam.step(ds.logits, step, pos, nxt_x)
+
+    def _beam_prefill(self, ds, prefix_rows: Tensor) -> None:
+        """prefix_rows [R, P, D]: each caption's prefix once per beam."""
+        R, P, D = prefix_rows.shape
+        ops.add_position(prefix_rows, prefix_rows.stride(0), prefix_rows.stride(1), self.wpe, ds.x, B=R, npos=P,
+                         D=D, pos0=0)
+        ds.beam.init(P)
+        self._decode_block(ds, P * R, ds.x, 0, P, prefill=True)
+        self._beam_head(ds, ds.x[(P - 1) * R: P * R], 0, P - 1)
+
+    def _beam_result(self, ds) -> Tensor:
+        out, n = ds.beam.finalize()
+        m = int(n.max().item()) if n.numel() else 0
+        return out[:, :m].clone()
+
+    @torch.no_grad()
+    def beam_decode(self, prefix: Tensor, max_length: int, num_beams: int = 4, length_penalty: float = 1.0,
+                    check_every: int = 8) -> Tensor:
+        """prefix [B,P,D] -> ids [B, <= max_length]: each caption's best finished hypothesis (EOS included when it
+        ended on one), EOS-padded to the longest (HF/generation/utils.py:3512-3523). Stops early once every
+        caption is done (the early-stop heuristic, :3008-3053)."""
+        B, P, D = prefix.shape
+        if max_length <= 0:
+            return torch.empty((B, 0), dtype=torch.long, device=prefix.device)
+        if prefix.is_cuda and self.graph_decode:
+            return self._beam_runner(B, num_beams, P, max_length, length_penalty).run(prefix, check_every)
+        ds = self.alloc_beam(B, num_beams, P, max_length, length_penalty)
+        rows = prefix.to(self.dtype).repeat_interleave(num_beams, dim=0).contiguous()
+        self._beam_prefill(ds, rows)
+        for s in range(1, max_length):
+            if s % check_every == 0 and bool(ds.beam.done.bool().all()):
+                break
+            pos = P + s - 1
+            self._decode_block(ds, ds.B, ds.x[:ds.B], pos, 1, prefill=False)
+            self._beam_head(ds, ds.x[:ds.B], s, pos)
+        return self._beam_result(ds)
+
+    def _beam_runner(self, B: int, W: int, P: int, max_length: int, length_penalty: float) -> "BeamRunner":
+        if not hasattr(self, "_beam_runners"):
+            self._beam_runners = {}
+        key = (B, W, P, max_length, float(length_penalty))
+        if key not in self._beam_runners:
+            if len(self._beam_runners) >= 2:
+                self._beam_runners.pop(next(iter(self._beam_runners)))
+            self._beam_runners[key] = BeamRunner(self, B, W, P, max_length, length_penalty)
+        return self._beam_runners[key]
+
+
+class BeamRunner:
+    """Beam search of one (B, W, P, max_length) shape as HIP-graph chunks (like DecodeRunner): chunk 0 = state
+    init + prefill + step 0, chunk c = steps [c*C, (c+1)*C). Between chunks the host reads the per-caption done
+    flags once; finished captions are frozen on the device, so extra steps never change the result."""
+
+    def __init__(self, core: "GPT2Core", B: int, W: int, P: int, max_length: int, length_penalty: float,
+                 chunk: int = 8):
+        self.core, self.B, self.W, self.P, self.T = core, B, W, P, max_length
+        self.ds = core.alloc_beam(B, W, P, max_length, length_penalty)
+        self.rows = torch.zeros((B * W, P, core.D), dtype=core.dtype, device=core.dev)
+        self.bounds = [(0, min(chunk, max_length))]
+        s = chunk
+        while s < max_length:
+            self.bounds.append((s, min(s + chunk, max_length)))
+            s += chunk
+        self.graphs = None
+
+    def _chunk(self, c: int) -> None:
+        core, ds, P = self.core, self.ds, self.P
+        s0, s1 = self.bounds[c]
+        if c == 0:
+            core._beam_prefill(ds, self.rows)
+            s0 = 1
+        for s in range(s0, s1):
+            pos = P + s - 1
+            core._decode_block(ds, ds.B, ds.x[:ds.B], pos, 1, prefill=False)
+            core._beam_head(ds, ds.x[:ds.B], s, pos)
+
+    @torch.no_grad()
+    def run(self, prefix: Tensor, check_every: int = 8) -> Tensor:
+        self.rows.copy_(prefix.to(self.core.dtype).repeat_interleave(self.W, dim=0))
+        if self.graphs is None:
+            for c in range(len(self.bounds)):  # eager warm-up pass (initialises every kernel once)
+                self._chunk(c)
+            torch.cuda.synchronize(self.core.dev)
+            self.graphs = []
+            for c in range(len(self.bounds)):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._chunk(c)
+                self.graphs.append(g)
+        for c, g in enumerate(self.graphs):
+            g.replay()
+            if c + 1 < len(self.graphs) and bool(self.ds.beam.done.bool().all()):
+                break
+        return self.core._beam_result(self.ds)
 
 
 class DecodeRunner:

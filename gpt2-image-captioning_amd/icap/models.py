@@ -205,9 +205,13 @@ class ImageCaptioningModel(nn.Module):
     # -- decode -------------------------------------------------------------------------------------------------
     @torch.no_grad()
     def generate(self, image_embeddings: Tensor, max_length: int = 50, temperature: float = 1.0,
-                 top_p: float = 0.9, early_exit: bool = True) -> Tensor:
+                 top_p: float = 0.9, early_exit: bool = True, num_beams: int = 1,
+                 length_penalty: float = 1.0) -> Tensor:
         """src/models.py:327-477: greedy (temperature == 0) or top-p sampling, KV-cached. early_exit=False keeps
-        decoding all max_length steps on the device (output identical; used to time fixed-length captions)."""
+        decoding all max_length steps on the device (output identical; used to time fixed-length captions).
+        num_beams > 1 (an extension; the reference has no beam search): transformers' beam search over the
+        caption prefix (GPT2LMHeadModel.generate(num_beams=..., do_sample=False), HF/generation/utils.py:
+        3208-3540; temperature / top_p are ignored), SURVEY.md §8f row f4."""
         self.eval()
         self.sync_compute_copies()
         B = image_embeddings.shape[0]
@@ -218,6 +222,8 @@ class ImageCaptioningModel(nn.Module):
         pre, pbs = self._prefix(mc, mws, B)
         P, D = self.total_prefix_length, self.gpt_embedding_size
         prefix = pre.as_strided((B, P, D), (pbs, D, 1))
+        if num_beams > 1:
+            return gc.beam_decode(prefix, max_length, num_beams=num_beams, length_penalty=length_penalty)
         if temperature == 0:
             return gc.greedy_decode(prefix, max_length, early_exit=early_exit)
         if temperature < 0:  # src/models.py:401-407: divide by 1.0 and skip the top-p filter (full softmax draw)

@@ -8,7 +8,7 @@ arithmetic itself and none falls back to PyTorch or the CPU.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -215,10 +215,74 @@ def attention_bwd(qkv: Tensor, dout: Tensor, lse: Tensor, dqkv: Tensor, *, B: in
     return dqkv
 
 
-def attention_decode(cache: Tensor, out: Tensor, *, B: int, H: int, hd: int, pos: int, scale: float) -> Tensor:
-    call("icap_attention_decode", dtype_code(cache.dtype), B, H, hd, pos, cache.data_ptr(), _ld(cache),
-         out.data_ptr(), _ld(out), scale, _stream())
+def attention_decode(cache: Tensor, out: Tensor, *, B: int, H: int, hd: int, pos: int, scale: float,
+                     anc: Optional[Tensor] = None) -> Tensor:
+    """anc: int32 [>= pos+1, B] KV ancestry (beam search; include/icap.h icap_attention_decode_anc)."""
+    if anc is None:
+        call("icap_attention_decode", dtype_code(cache.dtype), B, H, hd, pos, cache.data_ptr(), _ld(cache),
+             out.data_ptr(), _ld(out), scale, _stream())
+    else:
+        if anc.dtype != torch.int32 or anc.numel() < (pos + 1) * B:
+            raise L.IcapError("attention_decode: anc must be int32 with >= (pos+1)*B entries")
+        call("icap_attention_decode_anc", dtype_code(cache.dtype), B, H, hd, pos, cache.data_ptr(), _ld(cache),
+             anc.data_ptr(), out.data_ptr(), _ld(out), scale, _stream())
     return out
+
+
+# ---------------------------------------------------------------------------------------------- beam search
+class BeamState:
+    """Device state of one beam search (include/icap.h icap_beam_*): B captions x W beams, token budget
+    max_len, T = P + max_len cache positions. Owns the workspace and the per-row candidate buffers."""
+
+    def __init__(self, B: int, W: int, V: int, max_len: int, T: int, eos: int, length_penalty: float,
+                 dev: torch.device):
+        self.B, self.W, self.V, self.max_len, self.T = B, W, V, max_len, T
+        self.K = 8 if W <= 4 else 16
+        R = B * W
+        nbytes = int(L.load().icap_beam_workspace_bytes(B, W, T, max_len))
+        if nbytes == 0:
+            raise L.IcapError("beam: bad sizes")
+        self.ws = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
+        self.top_val = torch.empty((R, self.K), dtype=torch.float32, device=dev)
+        self.top_idx = torch.empty((R, self.K), dtype=torch.int32, device=dev)
+        self.top_m = torch.empty(R, dtype=torch.float32, device=dev)
+        self.top_ls = torch.empty(R, dtype=torch.float32, device=dev)
+        self.out = torch.empty((B, max_len), dtype=torch.int64, device=dev)
+        self.out_len = torch.empty(B, dtype=torch.int32, device=dev)
+        self.args = L.BeamArgs()
+        a = self.args
+        a.B, a.W, a.V, a.max_len, a.eos, a.length_penalty, a.K, a.T = B, W, V, max_len, eos, float(length_penalty), \
+            self.K, T
+        a.top_val, a.top_idx = self.top_val.data_ptr(), self.top_idx.data_ptr()
+        a.top_m, a.top_ls = self.top_m.data_ptr(), self.top_ls.data_ptr()
+        a.ws = self.ws.data_ptr()
+        # word offsets of the ancestry table and the per-caption done flags (beam.hip layout())
+        up4 = lambda n: (n + 3) & ~3  # noqa: E731
+        o = up4(R) + up4(R * max_len) + up4(R) + up4(R) + up4(R * max_len) + up4(B)
+        self.done = self.ws[o: o + B]
+        o += up4(B)
+        self.anc = self.ws[o: o + T * R]
+
+    def set_embedding(self, dtype: torch.dtype, D: int, n_positions: int, wte: Tensor, wpe: Tensor,
+                      x: Optional[Tensor]) -> None:
+        a = self.args
+        a.dtype, a.D, a.n_positions = dtype_code(dtype), D, n_positions
+        a.wte, a.wpe, a.x = wte.data_ptr(), wpe.data_ptr(), _p(x)
+
+    def init(self, P: int) -> None:
+        call("icap_beam_init", C.byref(self.args), P, _stream())
+
+    def step(self, logits: Tensor, step: int, pos: int, x: Optional[Tensor]) -> None:
+        R = self.B * self.W
+        call("icap_beam_rowtop", dtype_code(logits.dtype), R, self.V, logits.data_ptr(), _ld(logits), self.K,
+             self.top_val.data_ptr(), self.top_idx.data_ptr(), self.top_m.data_ptr(), self.top_ls.data_ptr(),
+             _stream())
+        self.args.x = _p(x)
+        call("icap_beam_update", C.byref(self.args), step, pos, _stream())
+
+    def finalize(self) -> Tuple[Tensor, Tensor]:
+        call("icap_beam_finalize", C.byref(self.args), self.out.data_ptr(), self.out_len.data_ptr(), _stream())
+        return self.out, self.out_len
 
 
 def gpt2_embed(prefix: Optional[Tensor], prefix_bstride: int, wte: Tensor, wpe: Tensor, ids: Optional[Tensor],

@@ -179,6 +179,12 @@ int icap_attention_bwd(const icap_attn_args* a, void* stream);
 int icap_attention_decode(int32_t dtype, int32_t B, int32_t H, int32_t hd, int32_t pos,
                           const void* cache, int64_t ld_cache, void* out, int64_t ld_out,
                           float scale, void* stream);
+/* Same with KV ancestry (beam search): key t of row b is cache row t*B + anc[t*B + b]       */
+/* (anc int32 [pos+1][B]; NULL = the row's own). Replaces the KV-cache reorder of           */
+/* HF/generation/utils.py:3476-3488 (Cache.reorder_cache) without moving cache bytes.        */
+int icap_attention_decode_anc(int32_t dtype, int32_t B, int32_t H, int32_t hd, int32_t pos,
+                              const void* cache, int64_t ld_cache, const int32_t* anc, void* out,
+                              int64_t ld_out, float scale, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Caption/prefix assembly for the GPT-2 input (src/models.py:261,283-317,    */
@@ -307,6 +313,41 @@ int icap_greedy_next(int32_t dtype, int32_t B, int64_t V, const void* logits, in
 int icap_topp_sample(int32_t dtype, int32_t B, int64_t V, const void* logits, int64_t ld, float temperature,
                      float top_p, const int32_t* finished, uint64_t seed, const uint64_t* seed_ptr,
                      int32_t step, int64_t eos, int64_t* out, void* stream);
+/* ------------------------------------------------------------------------- */
+/* Beam search. The reference decodes greedy / top-p  */
+/* only (src/models.py:327-477); the definition is transformers' beam search */
+/* (GPT2LMHeadModel.generate(num_beams=W, do_sample=False, early_stopping=   */
+/* False), HF/generation/utils.py:3208-3540). Decode rows r = b*W + i.        */
+/* Per step: icap_beam_rowtop over the R = B*W logits rows, then             */
+/* icap_beam_update. icap_beam_init before the first step (after prefill of  */
+/* P positions for all R rows), icap_beam_finalize after the last.           */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  int32_t B, W, V, max_len;          /* captions, beams per caption (<= 8), vocab, token budget     */
+  int32_t eos; float length_penalty;
+  int32_t K;                         /* row candidates from icap_beam_rowtop: 8 (W <= 4), 16 (W <= 8)*/
+  int32_t T;                         /* KV-cache positions (prefix + max_len), <= 1024               */
+  const float* top_val; const int32_t* top_idx; const float* top_m; const float* top_ls;
+  void* ws;                          /* icap_beam_workspace_bytes(B, W, T, max_len), 16-byte aligned */
+  int32_t dtype, D, n_positions;     /* next-step input embedding x[r] = wte[tok] + wpe[pos+1]      */
+  const void* wte; const void* wpe; void* x;  /* x [R, D] may be NULL (no next step)             */
+} icap_beam_args;
+size_t icap_beam_workspace_bytes(int32_t B, int32_t W, int32_t T, int32_t max_len);
+/* running scores (0 for beam 0, -1e9 for the others, :3318-3320), no finished hypotheses, and   */
+/* the KV ancestry of the P prefix positions (every row its own).                               */
+int icap_beam_init(const icap_beam_args* a, int32_t P, void* stream);
+/* per row: top K logits (descending, ties -> lower id) into top_val/top_idx [R, K], the row max */
+/* top_m [R] and log(sum(exp(logit - max))) top_ls [R] (log_softmax = (x - m) - ls).             */
+int icap_beam_rowtop(int32_t dtype, int64_t R, int64_t V, const void* logits, int64_t ld, int32_t K,
+                     float* top_val, int32_t* top_idx, float* top_m, float* top_ls, void* stream);
+/* one beam step after the logits of generated-token count `step` (the rows' last computed     */
+/* position is `pos`): top 2W candidates of each caption, the next running beams, the finished */
+/* merge (score / (step+1)^length_penalty), the early-stop heuristic, histories, the KV        */
+/* ancestry and the next input embeddings (HF/generation/utils.py:3077-3206,3008-3053).         */
+int icap_beam_update(const icap_beam_args* a, int32_t step, int32_t pos, void* stream);
+/* out int64 [B, max_len]: each caption's best finished hypothesis, EOS-padded; out_len [B].    */
+int icap_beam_finalize(const icap_beam_args* a, int64_t* out, int32_t* out_len, void* stream);
+
 /* x[(t*B + b)*D + d] = src[b*src_bstride + t*src_tstride + d] + wpe[(pos0+t)*D + d], t < npos */
 /* (prefix rows into the position-major decode input, modeling_gpt2.py:571-577).            */
 int icap_add_position(int32_t dtype, int32_t B, int32_t npos, int32_t D, const void* src,
