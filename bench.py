@@ -75,6 +75,17 @@ def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16):
     from icap.clip import CLIPVisionConfig, CLIPVisionTower
     from icap.gpt2 import GPT2Config
 
+    if config == "large":  # configs[4]: DINOv3 ViT-L/16 (1024-d) -> mapper at gpt_dim 1280 -> GPT-2 large
+        from icap.dino import DINOv3ImageTower
+
+        gpt = GPT2LMHeadModel.random_init(GPT2Config.large(), seed=0)
+        mapper = TransformerMappingNetwork.random_init(embed_dim=1024, gpt_dim=1280, seed=0)
+        model = ImageCaptioningModel(mapper, tokenizer=SimpleNamespace(eos_token_id=50256), gpt=gpt,
+                                     compute_dtype=dtype).to(dev)
+        tower = DINOv3ImageTower.random_init(seed=0).to(dev)
+        trainer = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10 ** 6, clip_model=tower,
+                                 dropout=dropout, seed=1234)
+        return model, tower, trainer
     if config == "medium":
         gpt = GPT2LMHeadModel.random_init(GPT2Config.medium(), seed=0)
         mapper = TransformerMappingNetwork.random_init(embed_dim=768, gpt_dim=1024, seed=0)
@@ -213,6 +224,24 @@ def greedy_rate(model, Bd, dev, world, edim=512):
     caps_per_s = world * Bd * nd / dt
 
     return caps_per_s, dt, nd, lens
+
+
+def beam_rate(model, Bd, dev, world, edim=512, num_beams=4):
+    """50-token KV-cached beam-4 captions/s (BASELINE configs[4] decode; transformers' beam search semantics,
+    tests/test_beam.py): Bd images x num_beams hypotheses decoded on the device, all 50 steps."""
+    g = torch.Generator().manual_seed(7)
+    emb = torch.randn((Bd, edim), generator=g)
+    emb = (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
+    model.generate(emb, max_length=50, temperature=0.0, num_beams=num_beams)  # warm-up (+ graph capture)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nd, lens = 2, []
+    for _ in range(nd):
+        lens.append(model.generate(emb, max_length=50, temperature=0.0, num_beams=num_beams).shape[1])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"captions_per_s": round(world * Bd * nd / dt, 1), "batch_per_gpu": Bd, "num_beams": num_beams,
+            "returned_len": lens[-1], "ms_per_batch": round(dt / nd * 1e3, 3)}
 
 
 def topp_rate(model, Bd, dev, world, edim=512, temperature=1.0, top_p=0.9):
@@ -375,6 +404,9 @@ def launcher_probe():
         torch.distributed.destroy_process_group()
 
 
+EDIM = {"small": 512, "medium": 768, "large": 1024}  # image-embedding width per config (CLIP-B/32, CLIP-L/14, DINOv3-L)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -386,8 +418,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the greedy-decode measurement (PMC passes)")
-    ap.add_argument("--config", default="small", choices=["small", "medium"],
-                    help="small = BASELINE configs[1] (default, the headline); medium = configs[3]")
+    ap.add_argument("--config", default="small", choices=["small", "medium", "large"],
+                    help="small = BASELINE configs[1] (default, the headline); medium = configs[3]; "
+                         "large = configs[4] (DINOv3 ViT-L/16 + GPT-2 large, beam-4 decode; bf16, fp8 not built)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -458,8 +491,10 @@ def main():
     Bd = args.decode_batch
     caps_per_s, dt, nd, lens = None, None, 1, [None]
     if not args.no_decode:
-        caps_per_s, dt, nd, lens = greedy_rate(model, Bd, dev, world, 768 if args.config == "medium" else 512)
-    topp = None if args.no_decode else topp_rate(model, Bd, dev, world, 768 if args.config == "medium" else 512)
+        caps_per_s, dt, nd, lens = greedy_rate(model, Bd, dev, world, EDIM[args.config])
+    topp = None if args.no_decode or args.config == "large" else topp_rate(model, Bd, dev, world, EDIM[args.config])
+    beam = beam_rate(model, Bd, dev, world, EDIM[args.config]) if (not args.no_decode and args.config == "large") \
+        else None
     # the same decode at a serving batch (4 x the headline's): the per-token kernels are latency-bound at 128 rows
     big = None
     if not args.no_decode and args.config == "small":
@@ -482,6 +517,11 @@ def main():
                                     "(8 layers, prefix 15, trained) -> GPT-2 small (frozen) fwd + dX bwd, LM head on "
                                     "the target rows + CE, dropout 0.1, clip_grad_norm 1.0 + AdamW + linear LR")
                        if args.config == "small" else
+                       ("BASELINE configs[4] train step (bf16; the fp8 MFMA path is not built): DINOv3 ViT-L/16 fwd "
+                        "(frozen, 4 registers + RoPE, 201 tokens) on 224x224 pixels -> transformer mapper (8 layers, "
+                        "gpt_dim 1280, trained) -> GPT-2 large (36 layers, d 1280, frozen) fwd + dX bwd, LM head on "
+                        "the target rows + CE, dropout 0.1, clip 1.0 + AdamW; decode: beam-4")
+                       if args.config == "large" else
                        ("BASELINE configs[3] train step: CLIP ViT-L/14 fwd (frozen, 257 tokens) on 224x224 pixels -> "
                         "transformer mapper (8 layers, gpt_dim 1024, trained) -> GPT-2 medium (24 layers, d 1024, "
                         "frozen) fwd + dX bwd, LM head on the target rows + CE, dropout 0.1, clip 1.0 + AdamW"),
@@ -494,6 +534,7 @@ def main():
                        "ms_per_batch": round(dt / nd * 1e3, 3) if dt else None},
             "greedy_serving_batch": big,
             "topp_sampling": topp,
+            "beam4": beam,
             "clip_preprocess": prep,
             "clip_extraction": extract,
             "fp32_parity_mode": parity,

@@ -604,16 +604,43 @@ __global__ void im2col_any_kernel(int B, int C, int HW, int p, int Kp, const flo
 }
 
 template <typename T>
-__global__ void vit_embed_kernel(int B, int G2, int D, const T* __restrict__ pe, const float* __restrict__ cls,
+__global__ void vit_embed_kernel(int B, int G2, int NP, int D, const T* __restrict__ pe, const float* __restrict__ pfx,
                                  const float* __restrict__ pos, T* __restrict__ x) {
-  const int S = G2 + 1;
+  const int S = G2 + NP;
   const int64_t total = (int64_t)B * S * D;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t row = i / D;
     const int d = (int)(i - row * D);
     const int b = (int)(row / S), t = (int)(row - (int64_t)b * S);
-    const float v = (t == 0) ? cls[d] : io<T>::ld(pe + ((int64_t)b * G2 + t - 1) * D + d);
-    io<T>::st(x + i, v + pos[(int64_t)t * D + d]);
+    const float v = (t < NP) ? pfx[(int64_t)t * D + d] : io<T>::ld(pe + ((int64_t)b * G2 + t - NP) * D + d);
+    io<T>::st(x + i, pos ? v + pos[(int64_t)t * D + d] : v);
+  }
+}
+
+// Rotary position embedding of the patch tokens (HF/models/dinov3_vit/modeling_dinov3_vit.py:203-268): for rows
+// t >= NP of every image and every head, q and k (columns [0, H hd) and [H hd, 2 H hd) of the fused QKV row) become
+// x * cos + rotate_half(x) * sin with rotate_half(x) = (-x[hd/2:], x[:hd/2]); cos / sin: fp32 [S - NP, hd]. One
+// thread per (row, q|k, head, i < hd/2) pair updates elements i and i + hd/2 in place.
+template <typename T>
+__global__ void rope_patches_kernel(int B, int S, int NP, int H, int hd, T* __restrict__ qkv, int64_t ld,
+                                    const float* __restrict__ cs, const float* __restrict__ sn) {
+#pragma clang fp contract(off)
+  const int half = hd >> 1;
+  const int P = S - NP;
+  const int64_t total = (int64_t)B * P * 2 * H * half;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(i % half);
+    int64_t r = i / half;
+    const int hq = (int)(r % (2 * H));  // q heads 0..H-1, then k heads
+    r /= (2 * H);
+    const int p = (int)(r % P);
+    const int b = (int)(r / P);
+    T* v = qkv + ((int64_t)b * S + NP + p) * ld + (int64_t)hq * hd;
+    const float x1 = io<T>::ld(v + j), x2 = io<T>::ld(v + j + half);
+    const float* c = cs + (int64_t)p * hd;
+    const float* s = sn + (int64_t)p * hd;
+    io<T>::st(v + j, x1 * c[j] + (-x2) * s[j]);
+    io<T>::st(v + j + half, x2 * c[j + half] + x1 * s[j + half]);
   }
 }
 
@@ -1197,8 +1224,31 @@ extern "C" int icap_vit_embed(int32_t dtype, int32_t B, int32_t G2, int32_t D, c
   const int64_t n = (int64_t)B * (G2 + 1) * D;
   if (n == 0) return ICAP_OK;
   DISPATCH_T(dtype, hipLaunchKernelGGL(vit_embed_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B, G2,
-                                       D, CTP(patch_emb), cls, pos, TP(x)));
+                                       1, D, CTP(patch_emb), cls, pos, TP(x)));
   return check_launch("icap_vit_embed");
+}
+
+extern "C" int icap_prefix_embed(int32_t dtype, int32_t B, int32_t G2, int32_t NP, int32_t D, const void* patch_emb,
+                                 const float* prefix, const float* pos, void* x, void* stream) {
+  ICAP_REQUIRE(patch_emb && prefix && x, "icap_prefix_embed: null pointer");
+  ICAP_REQUIRE(B >= 0 && G2 >= 0 && NP >= 1 && D > 0, "icap_prefix_embed: bad geometry");
+  const int64_t n = (int64_t)B * (G2 + NP) * D;
+  if (n == 0) return ICAP_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(vit_embed_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B, G2,
+                                       NP, D, CTP(patch_emb), prefix, pos, TP(x)));
+  return check_launch("icap_prefix_embed");
+}
+
+extern "C" int icap_rope_patches(int32_t dtype, int32_t B, int32_t S, int32_t NP, int32_t H, int32_t hd, void* qkv,
+                                 int64_t ld_qkv, const float* cos_t, const float* sin_t, void* stream) {
+  ICAP_REQUIRE(qkv && cos_t && sin_t, "icap_rope_patches: null pointer");
+  ICAP_REQUIRE(B >= 0 && S > NP && NP >= 0 && H > 0 && hd > 0 && hd % 2 == 0 && ld_qkv >= 2ll * H * hd,
+               "icap_rope_patches: bad geometry");
+  const int64_t n = (int64_t)B * (S - NP) * H * hd;
+  if (n == 0) return ICAP_OK;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(rope_patches_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B,
+                                       S, NP, H, hd, TP(qkv), ld_qkv, cos_t, sin_t));
+  return check_launch("icap_rope_patches");
 }
 
 extern "C" int icap_l2norm_rows(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx, float* out,

@@ -44,6 +44,10 @@ class GPT2Config:  # HF/models/gpt2/configuration_gpt2.py:84-103
     def medium(cls):  # BASELINE configs[3]
         return cls(n_embd=1024, n_layer=24, n_head=16)
 
+    @classmethod
+    def large(cls):  # BASELINE configs[4]
+        return cls(n_embd=1280, n_layer=36, n_head=20)
+
 
 def pad_vocab(v: int) -> int:
     return (v + 127) // 128 * 128

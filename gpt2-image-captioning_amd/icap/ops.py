@@ -409,6 +409,21 @@ def vit_embed(patch_emb: Tensor, cls: Tensor, pos: Tensor, x: Tensor, B: int, G2
     return x
 
 
+def prefix_embed(patch_emb: Tensor, prefix: Tensor, x: Tensor, B: int, G2: int, D: int,
+                 pos: Optional[Tensor] = None) -> Tensor:
+    """x[b] = [prefix tokens (fp32 [NP, D]) || patch_emb rows of image b] (+ pos) — icap_prefix_embed."""
+    call("icap_prefix_embed", dtype_code(x.dtype), B, G2, prefix.shape[0], D, patch_emb.data_ptr(),
+         prefix.data_ptr(), _p(pos), x.data_ptr(), _stream())
+    return x
+
+
+def rope_patches(qkv: Tensor, cos: Tensor, sin: Tensor, *, B: int, S: int, NP: int, H: int, hd: int) -> Tensor:
+    """In-place rotary embedding of the patch rows' q and k (icap_rope_patches)."""
+    call("icap_rope_patches", dtype_code(qkv.dtype), B, S, NP, H, hd, qkv.data_ptr(), _ld(qkv), cos.data_ptr(),
+         sin.data_ptr(), _stream())
+    return qkv
+
+
 def l2norm_rows(x: Tensor, out: Tensor, rows: Optional[int] = None) -> Tensor:
     rows = x.shape[0] if rows is None else rows
     call("icap_l2norm_rows", dtype_code(x.dtype), rows, x.shape[-1], x.data_ptr(), _ld(x), out.data_ptr(),

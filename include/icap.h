@@ -287,6 +287,17 @@ int icap_im2col_patches(int32_t dtype, int32_t B, int32_t C, int32_t HW, int32_t
 /* x[b, 0] = cls + pos[0];  x[b, 1+i] = patch_emb[b*G2 + i] + pos[1+i] */
 int icap_vit_embed(int32_t dtype, int32_t B, int32_t G2, int32_t D, const void* patch_emb,
                    const float* cls, const float* pos, void* x, void* stream);
+/* DINOv3 token assembly (HF/models/dinov3_vit/modeling_dinov3_vit.py:75-92; BASELINE configs[4], reference
+ * src/embeddings/dino.py:166): x[b, t] = prefix[t] (t < NP: CLS, then the register tokens) or
+ * patch_emb[b*G2 + t - NP] (t >= NP), plus pos[t] when pos != NULL. prefix fp32 [NP, D], pos fp32 [NP + G2, D]. */
+int icap_prefix_embed(int32_t dtype, int32_t B, int32_t G2, int32_t NP, int32_t D, const void* patch_emb,
+                      const float* prefix, const float* pos, void* x, void* stream);
+/* Rotary position embedding of the patch tokens, in place on the fused QKV activation (DINOv3:
+ * modeling_dinov3_vit.py:203-268): for rows t >= NP of each image, q = cols [0, H hd) and k = [H hd, 2 H hd),
+ * per head x <- x * cos + rotate_half(x) * sin, rotate_half(x) = (-x[hd/2:], x[:hd/2]); cos / sin fp32
+ * [S - NP, hd]. Rows of image b start at b*S; ld_qkv in elements. */
+int icap_rope_patches(int32_t dtype, int32_t B, int32_t S, int32_t NP, int32_t H, int32_t hd, void* qkv,
+                      int64_t ld_qkv, const float* cos_t, const float* sin_t, void* stream);
 /* out[b] = x[b] / ||x[b]||_2 (fp32 out) */
 int icap_l2norm_rows(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
                      float* out, int64_t ldo, void* stream);

@@ -635,6 +635,112 @@ def vit_embed_normalized(sd, cfg: ViTCfg, pixels: Tensor) -> Tensor:
     return f / f.norm(p=2, dim=-1, keepdim=True)
 
 
+@dataclass
+class DinoCfg:  # DINOv3 ViT-L/16 backbone of dino.txt (src/embeddings/dino.py:11-12,72-79; BASELINE configs[4])
+    hidden: int = 1024
+    layers: int = 24
+    heads: int = 16
+    inter: int = 4096
+    patch: int = 16
+    image: int = 224
+    channels: int = 3
+    registers: int = 4
+    eps: float = 1e-5
+    rope_theta: float = 100.0
+
+
+def dinov3_state_dict(cfg: DinoCfg, seed: int = 0) -> Dict[str, Tensor]:
+    """HF DINOv3ViTModel parameter names (transformers 5.15, modeling_dinov3_vit.py:60-548): key_bias=False,
+    LayerScale after attention and MLP. The mask token is unused at inference (zeros)."""
+    d, r = cfg.hidden, cfg.registers
+    sd = {
+        "embeddings.cls_token": gen_tensor(seed, "d.cls", (1, 1, d), 0.5),
+        "embeddings.mask_token": torch.zeros(1, 1, d),
+        "embeddings.register_tokens": gen_tensor(seed, "d.reg", (1, r, d), 0.5),
+        "embeddings.patch_embeddings.weight": gen_tensor(seed, "d.patch.w", (d, cfg.channels, cfg.patch, cfg.patch), 0.02),
+        "embeddings.patch_embeddings.bias": gen_tensor(seed, "d.patch.b", (d,), 0.02),
+        "norm.weight": gen_tensor(seed, "d.ln.w", (d,), 0.05, 1.0),
+        "norm.bias": gen_tensor(seed, "d.ln.b", (d,), 0.02),
+    }
+    for i in range(cfg.layers):
+        p = f"model.layer.{i}."
+        for nm in ("q", "k", "v", "o"):
+            sd[p + f"attention.{nm}_proj.weight"] = gen_tensor(seed, p + nm + ".w", (d, d), 0.02)
+            if nm != "k":
+                sd[p + f"attention.{nm}_proj.bias"] = gen_tensor(seed, p + nm + ".b", (d,), 0.02)
+        sd[p + "mlp.up_proj.weight"] = gen_tensor(seed, p + "up.w", (cfg.inter, d), 0.02)
+        sd[p + "mlp.up_proj.bias"] = gen_tensor(seed, p + "up.b", (cfg.inter,), 0.02)
+        sd[p + "mlp.down_proj.weight"] = gen_tensor(seed, p + "down.w", (d, cfg.inter), 0.02)
+        sd[p + "mlp.down_proj.bias"] = gen_tensor(seed, p + "down.b", (d,), 0.02)
+        for nm in ("norm1", "norm2"):
+            sd[p + nm + ".weight"] = gen_tensor(seed, p + nm + ".w", (d,), 0.05, 1.0)
+            sd[p + nm + ".bias"] = gen_tensor(seed, p + nm + ".b", (d,), 0.02)
+        sd[p + "layer_scale1.lambda1"] = gen_tensor(seed, p + "ls1", (d,), 0.1, 0.5)
+        sd[p + "layer_scale2.lambda1"] = gen_tensor(seed, p + "ls2", (d,), 0.1, 0.5)
+    return sd
+
+
+def dinov3_rope_tables(cfg: DinoCfg, h_patches: int, w_patches: int):
+    """cos / sin [h*w, hd] of the patch tokens (modeling_dinov3_vit.py:96-121,153-200, eval mode: no coordinate
+    augmentation): patch-centre coordinates in [-1, 1], inv_freq = 1 / theta^(arange(0, 1, 4 / hd)), angles
+    2 pi coord inv_freq per axis, (y, x) interleaved by flatten, tiled twice."""
+    hd = cfg.hidden // cfg.heads
+    inv_freq = 1 / cfg.rope_theta ** torch.arange(0, 1, 4 / hd, dtype=torch.float32)
+    ch = torch.arange(0.5, h_patches, dtype=torch.float32) / h_patches
+    cw = torch.arange(0.5, w_patches, dtype=torch.float32) / w_patches
+    coords = torch.stack(torch.meshgrid(ch, cw, indexing="ij"), dim=-1).flatten(0, 1)
+    coords = 2.0 * coords - 1.0
+    angles = (2 * math.pi * coords[:, :, None] * inv_freq[None, None, :]).flatten(1, 2).tile(2)
+    return torch.cos(angles), torch.sin(angles)
+
+
+def dinov3_forward(sd: Dict[str, Tensor], cfg: DinoCfg, pixels: Tensor) -> Tensor:
+    """DINOv3ViTModel(pixel_values).last_hidden_state (modeling_dinov3_vit.py:507-548): patch Conv2d (bias) ->
+    [CLS || registers || patches] (no absolute positions) -> pre-LN layers (norm1, q/k/v (k without bias), RoPE on
+    the patch rows of q and k :238-268, softmax attention, o_proj, LayerScale, +res; norm2, up_proj + erf-GELU,
+    down_proj, LayerScale, +res) -> final norm over every token."""
+    d, H = cfg.hidden, cfg.heads
+    hd = d // H
+    B = pixels.shape[0]
+    g = pixels.shape[-1] // cfg.patch
+    pe = F.conv2d(pixels, sd["embeddings.patch_embeddings.weight"], sd["embeddings.patch_embeddings.bias"],
+                  stride=cfg.patch).flatten(2).transpose(1, 2)
+    x = torch.cat([sd["embeddings.cls_token"].expand(B, -1, -1), sd["embeddings.register_tokens"].expand(B, -1, -1),
+                   pe], dim=1)
+    S, npfx = x.shape[1], 1 + cfg.registers
+    cos, sin = dinov3_rope_tables(cfg, g, g)
+
+    def rope(t):  # t [B, H, S, hd]; patch rows only
+        pre, pat = t[:, :, :npfx], t[:, :, npfx:]
+        rot = torch.cat((-pat[..., hd // 2:], pat[..., :hd // 2]), dim=-1)
+        return torch.cat((pre, pat * cos + rot * sin), dim=2)
+
+    for i in range(cfg.layers):
+        p = f"model.layer.{i}."
+        a = F.layer_norm(x, (d,), sd[p + "norm1.weight"], sd[p + "norm1.bias"], cfg.eps)
+        q = a @ sd[p + "attention.q_proj.weight"].t() + sd[p + "attention.q_proj.bias"]
+        k = a @ sd[p + "attention.k_proj.weight"].t()
+        v = a @ sd[p + "attention.v_proj.weight"].t() + sd[p + "attention.v_proj.bias"]
+        q, k, v = (t.view(B, S, H, hd).transpose(1, 2) for t in (q, k, v))
+        q, k = rope(q), rope(k)
+        w = torch.softmax((q @ k.transpose(-1, -2)) * hd ** -0.5, dim=-1)
+        o = (w @ v).transpose(1, 2).reshape(B, S, d)
+        o = o @ sd[p + "attention.o_proj.weight"].t() + sd[p + "attention.o_proj.bias"]
+        x = o * sd[p + "layer_scale1.lambda1"] + x
+        a = F.layer_norm(x, (d,), sd[p + "norm2.weight"], sd[p + "norm2.bias"], cfg.eps)
+        f = F.gelu(a @ sd[p + "mlp.up_proj.weight"].t() + sd[p + "mlp.up_proj.bias"])
+        f = f @ sd[p + "mlp.down_proj.weight"].t() + sd[p + "mlp.down_proj.bias"]
+        x = f * sd[p + "layer_scale2.lambda1"] + x
+    return F.layer_norm(x, (d,), sd["norm.weight"], sd["norm.bias"], cfg.eps)
+
+
+def dinov3_embed_normalized(sd, cfg: DinoCfg, pixels: Tensor) -> Tensor:
+    """pooler_output (the normed CLS row, modeling_dinov3_vit.py:541) L2-normalised as src/embeddings/dino.py:177-179
+    normalises encode_image's output."""
+    f = dinov3_forward(sd, cfg, pixels)[:, 0]
+    return f / f.norm(p=2, dim=-1, keepdim=True)
+
+
 # --------------------------------------------------------------------------- optimisation
 
 

@@ -125,6 +125,15 @@ def accesses(name, args):
         dt, B, G2, D, pe, cls, pos, x, _s = a
         out += [("pe", pe, B * G2 * D * ES[dt]), ("cls", cls, D * 4), ("pos", pos, (G2 + 1) * D * 4),
                 ("x", x, B * (G2 + 1) * D * ES[dt])]
+    elif name == "icap_prefix_embed":
+        dt, B, G2, NP, D, pe, pf, pos, x, _s = a
+        out += [("pe", pe, B * G2 * D * ES[dt]), ("prefix", pf, NP * D * 4), ("x", x, B * (G2 + NP) * D * ES[dt])]
+        if pos:
+            out.append(("pos", pos, (G2 + NP) * D * 4))
+    elif name == "icap_rope_patches":
+        dt, B, S, NP, H, hd, q, ld, cs, sn, _s = a
+        out += [("qkv", q, _rows(B * S, ld, 2 * H * hd, ES[dt])), ("cos", cs, (S - NP) * hd * 4),
+                ("sin", sn, (S - NP) * hd * 4)]
     elif name == "icap_l2norm_rows":
         dt, rows, D, x, ldx, o, ldo, _s = a
         out += [("x", x, _rows(rows, ldx, D, ES[dt])), ("out", o, _rows(rows, ldo, D, 4))]

@@ -257,3 +257,103 @@ def test_topp_kernel_keeps_reference_filter_set(dev):
     exp_b = np.array([exp[ix].sum() for ix in bins])
     exp_b *= obs_b.sum() / exp_b.sum()  # chisquare wants equal totals to ~1e-8; the float sums differ by rounding
     assert chisquare(obs_b, exp_b).pvalue > 1e-4
+
+
+# --------------------------------------------------------------------------------------- DINOv3 ViT-L/16 (configs[4])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_dinov3_l16(dev, dtype):
+    """DINOv3 backbone pooled CLS (and its L2 normalisation, src/embeddings/dino.py:175-179) vs HF DINOv3ViTModel:
+    register tokens, RoPE on the patch rows (icap_rope_patches), LayerScale folded into o_proj / down_proj."""
+    from icap.dino import DINOv3ImageTower
+
+    g = load("dinov3_l16")
+    tower = DINOv3ImageTower.random_init(seed=0).to(dev)
+    px = torch.randn((2, 3, 224, 224), generator=torch.Generator().manual_seed(int(g["pixels_seed"][0]))).to(dev)
+    pooled = tower.pooler_output(px, compute_dtype=dtype)
+    e = tower.embed(px, compute_dtype=dtype)
+    if dtype == torch.float32:
+        assert rel(pooled, g["pooler"]) < 1e-4 and rel(e, g["embeddings"]) < 1e-4
+    else:
+        cos = torch.nn.functional.cosine_similarity(e.cpu().double(), torch.from_numpy(g["embeddings"]).double())
+        assert cos.min() > 0.99, cos
+
+
+def test_rope_patches_kernel_matches_torch(dev):
+    """icap_rope_patches vs the HF formula (q*cos + rotate_half(q)*sin on the patch rows of q and k only)."""
+    from icap.dino import DinoConfig, rope_tables
+
+    B, NP, G, H, hd = 2, 5, 14, 4, 64
+    S = NP + G * G
+    cos, sin = rope_tables(DinoConfig(hidden_size=H * hd, num_attention_heads=H), G, G)
+    qkv = torch.randn((B * S, 3 * H * hd), generator=torch.Generator().manual_seed(3))
+    ref = qkv.clone().view(B, S, 3, H, hd)
+    pat = ref[:, NP:, :2]
+    rot = torch.cat((-pat[..., hd // 2:], pat[..., :hd // 2]), dim=-1)
+    ref[:, NP:, :2] = pat * cos[None, :, None, None, :] + rot * sin[None, :, None, None, :]
+    d = qkv.to(dev)
+    ops.rope_patches(d, cos.to(dev), sin.to(dev), B=B, S=S, NP=NP, H=H, hd=hd)
+    torch.cuda.synchronize()
+    assert torch.equal(d.cpu(), ref.view(B * S, -1))
+
+
+# ------------------------------------------------------------------------- configs[4] caption model (GPT-2 large)
+
+LRG_G = O.GPT2Cfg(n_layer=36, n_embd=1280, n_head=20)
+LRG_M = O.MapperCfg(embed_dim=1024, gpt_dim=1280)  # mapper heads of 160 (the generic attention kernels)
+
+
+@pytest.fixture(scope="module")
+def large_f32(dev):
+    return build(LRG_G, LRG_M, torch.float32, dev)
+
+
+def test_large_forward_and_greedy_f32(dev, large_f32):
+    """GPT-2 large (36 layers, d 1280, 20 heads) + mapper at gpt_dim 1280 vs the reference's forward / generate."""
+    g = load("large")
+    ids, mask, labels, emb = inputs(g, dev)
+    model = large_f32.eval()
+    with torch.no_grad():
+        out = model(ids, emb, mask, labels)
+        prefix = model.mapping_network(emb)
+    assert rel(prefix, g["prefix"]) < 1e-4
+    assert abs(out.loss.item() - g["loss"][0]) < 3e-5
+    rows = torch.from_numpy(g["logit_rows"])
+    assert rel(out.logits[:2][:, rows], g["logits_sel"]) < 1e-4
+    gen = model.generate(emb[: g["greedy"].shape[0]], max_length=g["greedy"].shape[1], temperature=0.0)
+    assert np.array_equal(gen.cpu().numpy(), g["greedy"])
+
+
+def test_large_beam4_exact_f32(dev, large_f32):
+    """configs[4] decode: the device beam-4 search returns transformers' generate(num_beams=4) ids at the GPT-2
+    large geometry (prefix from the reference's mapper)."""
+    g = load("large_beam4")
+    core = large_f32.gpt.core(torch.float32)
+    ids = core.beam_decode(torch.from_numpy(g["prefix"]).to(dev), g["ids"].shape[1], num_beams=4).cpu().numpy()
+    assert np.array_equal(ids, g["ids"])
+
+
+def test_large_fused_train_f32(dev):
+    g = load("large")
+    model = build(LRG_G, LRG_M, torch.float32, dev)
+    n = len(g["train_losses"])
+    losses, _ = _trainer_steps(model, inputs(g, dev), n)
+    assert rel(losses, g["train_losses"]) < 1e-5
+    for k, v in model.mapping_network.state_dict().items():
+        t = v.detach().double()
+        assert rel(torch.tensor([t.sum().item(), t.abs().sum().item()]), torch.tensor(g["trained_ck." + k][:2])) < 1e-4, k
+
+
+def test_large_forward_bf16(dev):
+    """bf16 perf mode at the configs[4] geometry: loss |d| <= 5e-2, selected logits max-rel <= 8e-2, argmax >= 80 %
+    (36 layers of bf16 rounding)."""
+    g = load("large")
+    ids, mask, labels, emb = inputs(g, dev)
+    model = build(LRG_G, LRG_M, torch.bfloat16, dev).eval()
+    with torch.no_grad():
+        out = model(ids, emb, mask, labels)
+    assert abs(out.loss.item() - g["loss"][0]) < 5e-2
+    rows = torch.from_numpy(g["logit_rows"])
+    assert rel(out.logits[:2][:, rows], g["logits_sel"]) < 8e-2
+    assert (out.logits.argmax(-1).cpu().numpy() == g["argmax"]).mean() >= 0.8

@@ -9,7 +9,7 @@ outputs. Dropout is disabled (GPT2Config *_pdrop=0 and the mapper's dropout
 modules set to p=0) so outputs are deterministic. Only inputs + outputs are
 written: no reference source travels.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/make_goldens.py [tiny small clip vit clip_l14 topp small_train medium ckpt]
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/make_goldens.py [tiny small clip vit clip_l14 dino topp small_train medium ckpt]
 """
 
 from __future__ import annotations
@@ -254,6 +254,34 @@ def golden_clip_l14():
     print("clip_l14", normed[0, :5])
 
 
+def golden_dinov3():
+    """DINOv3 ViT-L/16 backbone (BASELINE configs[4]; src/embeddings/dino.py loads it from torch.hub, which is gated
+    and offline here): HF DINOv3ViTModel (transformers 5.15) at the ViT-L/16 geometry with 4 register tokens,
+    key_bias=False and LayerScale, deterministic weights, 2 seeded images. The dino.txt vision head that
+    encode_image adds on top of the backbone is not available offline (parity unpinned for that head)."""
+    from transformers import DINOv3ViTConfig, DINOv3ViTModel
+
+    cfg = O.DinoCfg()
+    hf = DINOv3ViTModel(DINOv3ViTConfig(hidden_size=cfg.hidden, num_hidden_layers=cfg.layers,
+                                        num_attention_heads=cfg.heads, intermediate_size=cfg.inter,
+                                        num_register_tokens=cfg.registers, key_bias=False, layerscale_value=1.0,
+                                        patch_size=cfg.patch, image_size=cfg.image, rope_theta=cfg.rope_theta,
+                                        layer_norm_eps=cfg.eps))
+    missing, unexpected = hf.load_state_dict(O.dinov3_state_dict(cfg, 0), strict=True)
+    assert not missing and not unexpected, (missing, unexpected)
+    hf.eval()
+    px = torch.randn((2, 3, 224, 224), generator=torch.Generator().manual_seed(6))
+    with torch.no_grad():
+        out = hf(pixel_values=px)
+        pooled = out.pooler_output
+        normed = pooled / pooled.norm(p=2, dim=-1, keepdim=True)
+        patch_mean = out.last_hidden_state[:, 1 + cfg.registers:].mean(dim=1)
+    np.savez_compressed(os.path.join(OUT, "dinov3_l16.npz"), pixels_seed=np.array([6]), pooler=pooled.numpy(),
+                        embeddings=normed.numpy(), patch_mean=patch_mean.numpy(),
+                        registers=out.last_hidden_state[:, 1:1 + cfg.registers].numpy())
+    print("dinov3_l16", normed[0, :5])
+
+
 def golden_topp():
     """The reference's top-p filter (src/models.py:400-449) as the reference runs it: generate(temperature 0.8,
     top_p 0.9) at the tiny config with torch.multinomial replaced by a recorder that returns the most probable kept
@@ -386,6 +414,23 @@ def golden_medium(workdir):
                   logit_rows=[14, 17, 26], train_steps=2, unfrozen_steps=0, workdir=workdir, full_logits=False)
 
 
+def golden_large(workdir):
+    """BASELINE configs[4] caption model: GPT-2 large (36 layers, d 1280, 20 heads) + transformer mapper at
+    gpt_dim 1280 (8 heads of 160) over 1024-d DINOv3 ViT-L/16 embeddings; plus transformers' beam-4 ids on its
+    caption prefix (the configs[4] decode)."""
+    gcfg, mcfg = O.GPT2Cfg(n_layer=36, n_embd=1280, n_head=20), O.MapperCfg(embed_dim=1024, gpt_dim=1280)
+    golden_config("large", gcfg, mcfg, B=2, L=12, real=7, gen_B=2, gen_len=6, logit_rows=[14, 17, 26],
+                  train_steps=2, unfrozen_steps=0, workdir=workdir, full_logits=False)
+    model, gsd, _ = build_ref(gcfg, mcfg, 0)
+    model.eval()
+    _, _, _, emb = O.synthetic_batch(2, 12, 7, gcfg.vocab_size, gcfg.eos, mcfg.embed_dim, seed=1)
+    with torch.no_grad():
+        prefix = model.mapping_network(emb)
+    ids = hf_beam(gcfg, gsd, prefix, 8, num_beams=4)
+    np.savez_compressed(os.path.join(OUT, "large_beam4.npz"), prefix=prefix.numpy(), ids=ids.numpy())
+    print("large beam4", ids.tolist())
+
+
 def golden_ckpt_keys(workdir):
     """Key sets + shapes of the reference's save_parameters() files (src/models.py:489-519) for the transformer
     mapper with GPT-2 frozen / unfrozen and the MLP mapper (GPT-2 small geometry), and of its extraction .pt
@@ -434,6 +479,8 @@ def main():
             golden_vit_b16()
         if not only or "clip_l14" in only:
             golden_clip_l14()
+        if not only or "dino" in only:
+            golden_dinov3()
         if not only or "topp" in only:
             golden_topp()
         if not only or "beam" in only:
@@ -442,6 +489,8 @@ def main():
             golden_small_train(work)
         if not only or "medium" in only:
             golden_medium(work)
+        if not only or "large" in only:
+            golden_large(work)
         if not only or "ckpt" in only:
             golden_ckpt_keys(work)
     finally:
