@@ -232,16 +232,17 @@ def beam_rate(model, Bd, dev, world, edim=512, num_beams=4):
     g = torch.Generator().manual_seed(7)
     emb = torch.randn((Bd, edim), generator=g)
     emb = (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
-    model.generate(emb, max_length=50, temperature=0.0, num_beams=num_beams)  # warm-up (+ graph capture)
+    # all 50 steps (random-init weights finish captions early; finished ones stay frozen): fixed work per caption
+    model.generate(emb, max_length=50, temperature=0.0, num_beams=num_beams, early_exit=False)  # warm-up + capture
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     nd, lens = 2, []
     for _ in range(nd):
-        lens.append(model.generate(emb, max_length=50, temperature=0.0, num_beams=num_beams).shape[1])
+        lens.append(model.generate(emb, max_length=50, temperature=0.0, num_beams=num_beams, early_exit=False).shape[1])
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     return {"captions_per_s": round(world * Bd * nd / dt, 1), "batch_per_gpu": Bd, "num_beams": num_beams,
-            "returned_len": lens[-1], "ms_per_batch": round(dt / nd * 1e3, 3)}
+            "decode_steps": 50, "returned_len": lens[-1], "ms_per_batch": round(dt / nd * 1e3, 3)}
 
 
 def topp_rate(model, Bd, dev, world, edim=512, temperature=1.0, top_p=0.9):

@@ -201,7 +201,9 @@ __global__ __launch_bounds__(1024) void ln_param_reduce(int nblk, int D, const f
 // Half a wave per row: 32 lanes x LN8_MAXC chunks of 8 elements, each one 16-byte access (the 4-wide form moves
 // 8 bytes per lane and access; these kernels are access-issue bound, like the GEMM store tail). 8 rows per
 // 256-thread block; the row reductions stay inside the half-wave (xor shuffles 16..1).
-// LN8_MAXC (template): chunks per lane, 3 for D <= 768, 4 for D <= 1024
+// LN8_MAXC (template): chunks per lane, 3 for D <= 768, 4 for D <= 1024, 5 for D <= 1280 (GPT-2 large), 6 for
+// D <= 1536
+constexpr int LN8_DMAX = 6 * 32 * 8;
 
 __device__ __forceinline__ float half_sum(float v) {
 #pragma unroll
@@ -410,8 +412,10 @@ static int ln_blocks(int64_t rows, int cap) {
 extern "C" int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
                                   const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
                                   float* mean, float* rstd, const int32_t* y_rowmap, void* stream) {
-  ICAP_REQUIRE(D > 0 && D % 4 == 0 && D <= 4 * 64 * LN_MAXV, "icap_layernorm_fwd: D must be a multiple of 4, <= 1024");
   ICAP_REQUIRE(x && y && gamma && beta, "icap_layernorm_fwd: null pointer");
+  ICAP_REQUIRE(D > 0 && D % 4 == 0 && (D <= 4 * 64 * LN_MAXV || (D <= LN8_DMAX && ln8_ok(dtype, D, x, ldx) &&
+                                                               ln8_ok(dtype, D, y, ldy))),
+               "icap_layernorm_fwd: D must be a multiple of 4, <= 1024 (<= 1536 with 16-byte rows)");
   ICAP_REQUIRE(ldx % 4 == 0 && ldy % 4 == 0, "icap_layernorm_fwd: strides must be multiples of 4");
   if (rows == 0) return ICAP_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -421,9 +425,11 @@ extern "C" int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const 
   hipLaunchKernelGGL((ln_fwd8_kernel<T, NC>), dim3(nb8), dim3(256), 0, s, rows, (int)D, (const T*)x, ldx, gamma, \
                      beta, eps, (T*)y, ldy, mean, rstd, y_rowmap)
     if (dtype == ICAP_BF16) {
-      if (D <= 768) ICAP_LN_FWD8(bf16_t, 3); else ICAP_LN_FWD8(bf16_t, 4);
+      if (D <= 768) ICAP_LN_FWD8(bf16_t, 3); else if (D <= 1024) ICAP_LN_FWD8(bf16_t, 4);
+      else if (D <= 1280) ICAP_LN_FWD8(bf16_t, 5); else ICAP_LN_FWD8(bf16_t, 6);
     } else {
-      if (D <= 768) ICAP_LN_FWD8(float, 3); else ICAP_LN_FWD8(float, 4);
+      if (D <= 768) ICAP_LN_FWD8(float, 3); else if (D <= 1024) ICAP_LN_FWD8(float, 4);
+      else if (D <= 1280) ICAP_LN_FWD8(float, 5); else ICAP_LN_FWD8(float, 6);
     }
 #undef ICAP_LN_FWD8
     return check_launch("icap_layernorm_fwd");
@@ -448,8 +454,12 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
                                   void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
                                   uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
                                   void* workspace, const int32_t* dy_rowmap, void* stream) {
-  ICAP_REQUIRE(D > 0 && D % 4 == 0 && D <= 4 * 64 * LN_MAXV, "icap_layernorm_bwd: D must be a multiple of 4, <= 1024");
   ICAP_REQUIRE(x && gamma && mean && rstd && dy && dx, "icap_layernorm_bwd: null pointer");
+  const bool wide8 = ln8_ok(dtype, D, x, ldx) && ln8_ok(dtype, D, dy, lddy) && ln8_ok(dtype, D, dx, lddx) &&
+                     (dres == nullptr || ln8_ok(dtype, D, dres, lddres)) &&
+                     (dx_drop == nullptr || ln8_ok(dtype, D, dx_drop, lddx));
+  ICAP_REQUIRE(D > 0 && D % 4 == 0 && (D <= 4 * 64 * LN_MAXV || (D <= LN8_DMAX && wide8)),
+               "icap_layernorm_bwd: D must be a multiple of 4, <= 1024 (<= 1536 with 16-byte rows)");
   ICAP_REQUIRE((dgamma == nullptr && dbeta == nullptr) || workspace != nullptr,
                "icap_layernorm_bwd: dgamma/dbeta need a workspace");
   ICAP_REQUIRE(drop_p >= 0.f && drop_p < 1.f, "icap_layernorm_bwd: drop_p out of range");
@@ -460,12 +470,12 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
   const uint32_t thr = drop_p > 0.f ? drop_threshold(drop_p) : 0u;
   const float inv_keep = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
   float* partial = want_params ? reinterpret_cast<float*>(workspace) : nullptr;
-  if (ln8_ok(dtype, D, x, ldx) && ln8_ok(dtype, D, dy, lddy) && ln8_ok(dtype, D, dx, lddx) &&
-      (dres == nullptr || ln8_ok(dtype, D, dres, lddres)) && (dx_drop == nullptr || ln8_ok(dtype, D, dx_drop, lddx))) {
+  if (wide8) {
     // same block count as the partial workspace is sized for (8 rows per block here, 4 in the 4-wide form)
     const int nb8 = want_params ? nb : ln_blocks8(rows, 4096);
 #define ICAP_LN_BWD8(T, P)                                                                                      \
-  if (D <= 768) ICAP_LN_BWD8N(T, P, 3); else ICAP_LN_BWD8N(T, P, 4)
+  if (D <= 768) ICAP_LN_BWD8N(T, P, 3); else if (D <= 1024) ICAP_LN_BWD8N(T, P, 4);              \
+  else if (D <= 1280) ICAP_LN_BWD8N(T, P, 5); else ICAP_LN_BWD8N(T, P, 6)
 #define ICAP_LN_BWD8N(T, P, NC)                                                                                 \
   hipLaunchKernelGGL((ln_bwd8_kernel<T, P, NC>), dim3(nb8), dim3(256), 0, s, rows, (int)D, (const T*)x, ldx, gamma, \
                      mean, rstd, (const T*)dy, lddy, (const T*)dres, lddres, (T*)dx, lddx, (T*)dx_drop, thr,     \

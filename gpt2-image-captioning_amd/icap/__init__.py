@@ -16,3 +16,5 @@ from .mapper import MLPMappingNetwork, TransformerMappingNetwork  # noqa: E402,F
 from .models import ImageCaptioningModel, load_gpt2_tokenizer  # noqa: E402,F401
 from .train import train  # noqa: E402,F401
 from .vit import ViTConfig, ViTImageTower, extract_vit_embedding_from_image, extract_vit_embeddings, load_vit_model  # noqa: E402,F401
+from .dino import (DINOv3ImageTower, DinoConfig, extract_dino_embeddings, get_dinov3_preprocessor,  # noqa: E402,F401
+                   load_dinov3_models)

@@ -682,20 +682,21 @@ class GPT2Core:
 
     @torch.no_grad()
     def beam_decode(self, prefix: Tensor, max_length: int, num_beams: int = 4, length_penalty: float = 1.0,
-                    check_every: int = 8) -> Tensor:
+                    check_every: int = 8, early_exit: bool = True) -> Tensor:
         """prefix [B,P,D] -> ids [B, <= max_length]: each caption's best finished hypothesis (EOS included when it
         ended on one), EOS-padded to the longest (HF/generation/utils.py:3512-3523). Stops early once every
-        caption is done (the early-stop heuristic, :3008-3053)."""
+        caption is done (the early-stop heuristic, :3008-3053); early_exit=False runs all max_length steps (finished
+        captions stay frozen, so the ids are the same: a fixed-work throughput measurement)."""
         B, P, D = prefix.shape
         if max_length <= 0:
             return torch.empty((B, 0), dtype=torch.long, device=prefix.device)
         if prefix.is_cuda and self.graph_decode:
-            return self._beam_runner(B, num_beams, P, max_length, length_penalty).run(prefix, check_every)
+            return self._beam_runner(B, num_beams, P, max_length, length_penalty).run(prefix, early_exit)
         ds = self.alloc_beam(B, num_beams, P, max_length, length_penalty)
         rows = prefix.to(self.dtype).repeat_interleave(num_beams, dim=0).contiguous()
         self._beam_prefill(ds, rows)
         for s in range(1, max_length):
-            if s % check_every == 0 and bool(ds.beam.done.bool().all()):
+            if early_exit and s % check_every == 0 and bool(ds.beam.done.bool().all()):
                 break
             pos = P + s - 1
             self._decode_block(ds, ds.B, ds.x[:ds.B], pos, 1, prefill=False)
@@ -742,7 +743,7 @@ class BeamRunner:
             core._beam_head(ds, ds.x[:ds.B], s, pos)
 
     @torch.no_grad()
-    def run(self, prefix: Tensor, check_every: int = 8) -> Tensor:
+    def run(self, prefix: Tensor, early_exit: bool = True) -> Tensor:
         self.rows.copy_(prefix.to(self.core.dtype).repeat_interleave(self.W, dim=0))
         if self.graphs is None:
             for c in range(len(self.bounds)):  # eager warm-up pass (initialises every kernel once)
@@ -756,7 +757,7 @@ class BeamRunner:
                 self.graphs.append(g)
         for c, g in enumerate(self.graphs):
             g.replay()
-            if c + 1 < len(self.graphs) and bool(self.ds.beam.done.bool().all()):
+            if early_exit and c + 1 < len(self.graphs) and bool(self.ds.beam.done.bool().all()):
                 break
         return self.core._beam_result(self.ds)
 

@@ -223,7 +223,8 @@ class ImageCaptioningModel(nn.Module):
         P, D = self.total_prefix_length, self.gpt_embedding_size
         prefix = pre.as_strided((B, P, D), (pbs, D, 1))
         if num_beams > 1:
-            return gc.beam_decode(prefix, max_length, num_beams=num_beams, length_penalty=length_penalty)
+            return gc.beam_decode(prefix, max_length, num_beams=num_beams, length_penalty=length_penalty,
+                                  early_exit=early_exit)
         if temperature == 0:
             return gc.greedy_decode(prefix, max_length, early_exit=early_exit)
         if temperature < 0:  # src/models.py:401-407: divide by 1.0 and skip the top-p filter (full softmax draw)

@@ -330,8 +330,12 @@ def test_large_beam4_exact_f32(dev, large_f32):
     large geometry (prefix from the reference's mapper)."""
     g = load("large_beam4")
     core = large_f32.gpt.core(torch.float32)
-    ids = core.beam_decode(torch.from_numpy(g["prefix"]).to(dev), g["ids"].shape[1], num_beams=4).cpu().numpy()
+    prefix = torch.from_numpy(g["prefix"]).to(dev)
+    ids = core.beam_decode(prefix, g["ids"].shape[1], num_beams=4).cpu().numpy()
     assert np.array_equal(ids, g["ids"])
+    # fixed-work form (bench.py beam_rate): every step decoded, finished captions frozen -> the same ids
+    full = core.beam_decode(prefix, g["ids"].shape[1], num_beams=4, early_exit=False).cpu().numpy()
+    assert np.array_equal(full, g["ids"])
 
 
 def test_large_fused_train_f32(dev):
