@@ -576,8 +576,6 @@ class GPT2Core:
         if max_length <= 0:
             return torch.empty((B, 0), dtype=torch.long, device=prefix.device)
         if prefix.is_cuda and self.graph_decode:
-            if self.decode_streams > 1 and B >= 32 * self.decode_streams:
-                return self._split_runner(B, P, max_length).run(prefix, early_exit)
             return self._runner(B, P, max_length).run(prefix, early_exit, check_every)
         ds = self.alloc_decode(B, P, max_length)
         pre = prefix if (prefix.dtype == self.dtype and prefix.stride(-1) == 1) else prefix.to(self.dtype).contiguous()
@@ -597,9 +595,6 @@ class GPT2Core:
         return self._truncate(toks, steps)
 
     graph_decode = True  # replay captured HIP graphs of the decode chunks (per batch shape)
-    # greedy decode of B >= 32 * decode_streams captions runs as that many independent sub-batches, each a chain of
-    # graph replays on its own HIP stream (SplitDecodeRunner); 1 = one chain
-    decode_streams = 2
 
     def _runner(self, B: int, P: int, max_length: int, sampling=None) -> "DecodeRunner":
         if not hasattr(self, "_runners"):
@@ -610,16 +605,6 @@ class GPT2Core:
                 self._runners.pop(next(iter(self._runners)))
             self._runners[key] = DecodeRunner(self, B, P, max_length, sampling=sampling)
         return self._runners[key]
-
-    def _split_runner(self, B: int, P: int, max_length: int) -> "SplitDecodeRunner":
-        if not hasattr(self, "_split_runners"):
-            self._split_runners = {}
-        key = (B, P, max_length, self.decode_streams)
-        if key not in self._split_runners:
-            if len(self._split_runners) >= 2:
-                self._split_runners.pop(next(iter(self._split_runners)))
-            self._split_runners[key] = SplitDecodeRunner(self, B, P, max_length, self.decode_streams)
-        return self._split_runners[key]
 
     def _truncate(self, toks: Tensor, steps: int) -> Tensor:
         B = toks.shape[0]
@@ -816,17 +801,6 @@ class DecodeRunner:
 
     @torch.no_grad()
     def run(self, prefix: Tensor, early_exit: bool = True, check_every: int = 8, seed: int = 0) -> Tensor:
-        self.prepare(prefix, seed)
-        steps = 0
-        for c, g in enumerate(self.graphs):
-            g.replay()
-            steps = self.bounds[c][1]
-            if early_exit and c + 1 < len(self.graphs) and bool(self.ds.finished.bool().all()):
-                break
-        return self.core._truncate(self.ds.tokens[:, :steps], steps)
-
-    def prepare(self, prefix: Tensor, seed: int = 0) -> None:
-        """Stage the prefix (and seed) on the current stream; capture the chunk graphs on first use."""
         self.prefix.copy_(prefix)
         if self.samp is not None:
             self.seed_dev.fill_(seed)
@@ -840,48 +814,10 @@ class DecodeRunner:
                 with torch.cuda.graph(g):
                     self._chunk(c)
                 self.graphs.append(g)
-
-
-class SplitDecodeRunner:
-    """Greedy decode of B captions as `parts` independent sub-batches (rows are independent: the ids equal the
-    one-batch decode's), each a DecodeRunner whose chunk graphs replay on a HIP stream of its own with split-K
-    scratch of its own. A token of one sub-batch is a chain of ~63 dependent, latency-bound launches that leaves
-    CUs idle between and inside them; the other chains fill those gaps. After each chunk round the host joins the
-    streams and reads every sub-batch's EOS latch (early exit, src/models.py:390-391)."""
-
-    def __init__(self, core: GPT2Core, B: int, P: int, max_length: int, parts: int):
-        base, extra = divmod(B, parts)
-        self.sizes = [base + (1 if i < extra else 0) for i in range(parts)]
-        self.core = core
-        self.runners = [DecodeRunner(core, b, P, max_length) for b in self.sizes]
-        self.streams = [torch.cuda.Stream(core.dev) for _ in self.sizes]
-        self.ws = [torch.empty(SPLIT_DECODE_WS_BYTES // 4, dtype=torch.float32, device=core.dev) for _ in self.sizes]
-
-    @torch.no_grad()
-    def run(self, prefix: Tensor, early_exit: bool = True) -> Tensor:
-        cur = torch.cuda.current_stream(self.core.dev)
-        r0 = 0
-        for r, st, ws, b in zip(self.runners, self.streams, self.ws, self.sizes):
-            st.wait_stream(cur)
-            with torch.cuda.stream(st), ops.workspace_scope(ws):
-                r.prepare(prefix[r0:r0 + b])
-            r0 += b
-        bounds = self.runners[0].bounds
         steps = 0
-        for c in range(len(bounds)):
-            for r, st in zip(self.runners, self.streams):
-                with torch.cuda.stream(st):
-                    r.graphs[c].replay()
-            steps = bounds[c][1]
-            if early_exit and c + 1 < len(bounds):
-                for st in self.streams:
-                    cur.wait_stream(st)
-                if all(bool(r.ds.finished.bool().all()) for r in self.runners):
-                    break
-        for st in self.streams:
-            cur.wait_stream(st)
-        toks = torch.cat([r.ds.tokens[:, :steps] for r in self.runners], 0)
-        return self.core._truncate(toks, steps)
-
-
-SPLIT_DECODE_WS_BYTES = 64 << 20  # per sub-batch split-K scratch (prefill of <= 64 captions: <= 18 MB)
+        for c, g in enumerate(self.graphs):
+            g.replay()
+            steps = self.bounds[c][1]
+            if early_exit and c + 1 < len(self.graphs) and bool(self.ds.finished.bool().all()):
+                break
+        return self.core._truncate(self.ds.tokens[:, :steps], steps)

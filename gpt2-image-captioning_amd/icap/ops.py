@@ -112,7 +112,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     if resid is not None:
         a.resid, a.ldr = resid.data_ptr(), _ld(resid)
     a.drop_p, a.seed, a.offset, a.seed_ptr = drop.p, drop.seed, drop.offset, drop.ptr
-    ws = (_ws_override if _ws_override is not None else gemm_workspace(A.device)) if workspace is None else workspace
+    ws = gemm_workspace(A.device) if workspace is None else workspace
     a.workspace, a.workspace_bytes, a.split_k = ws.data_ptr(), ws.numel() * 4, split_k
     a.m_dev = _p(m_dev)
     a.path = 1 if tile_only else (2 if ring else (3 if g256 else 0))
@@ -144,27 +144,6 @@ def gemm_workspace(device) -> Tensor:
         ws = torch.empty(GEMM_WORKSPACE_BYTES // 4, dtype=torch.float32, device=device)
         _gemm_ws[key] = ws
     return ws
-
-
-_ws_override = None
-
-
-class workspace_scope:
-    """GEMMs issued inside use `ws` as their split-K scratch instead of the per-device default (work captured
-    for another stream, e.g. one decode sub-batch of GPT2Core's split greedy decode, needs scratch of its own)."""
-
-    def __init__(self, ws: Optional[Tensor]):
-        self.ws, self.prev = ws, None
-
-    def __enter__(self):
-        global _ws_override
-        self.prev, _ws_override = _ws_override, self.ws
-        return self
-
-    def __exit__(self, *exc):
-        global _ws_override
-        _ws_override = self.prev
-        return False
 
 
 GEMM_TIMER = None  # set to an object with .launch(key, flops, fn) to time every GEMM launch

@@ -222,15 +222,6 @@ def test_small_greedy128_exact_f32(dev):
     assert gen.shape == ref.shape, (gen.shape, ref.shape)
     bad = np.nonzero((gen != ref).any(1))[0]
     assert bad.size == 0, f"{bad.size} captions differ: {bad[:8]}"
-    # the split decode (B >= 64: sub-batches on their own streams, GPT2Core.decode_streams = 2 by default) and the
-    # one-chain decode return the same ids, with and without the per-chunk early exit
-    core = model.gpt.core(torch.float32)
-    assert core.decode_streams >= 2
-    for parts, early in ((1, True), (4, True), (4, False)):
-        core.decode_streams = parts
-        out = model.generate(e, max_length=50, temperature=0.0, early_exit=early).cpu().numpy()
-        assert np.array_equal(out[:, :ref.shape[1]], ref), (parts, early)
-    core.decode_streams = 2
 
 
 # ---------------------------------------------------------------------------------------------------- top-p (a14)
