@@ -705,349 +705,11 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(icap_gemm_args p, int 
 
 
 // ---------------------------------------------------------------------------------------------------------------
-// Persistent ring GEMM (bf16 in, bf16 out, fp32 accumulate) for the mid-sized products of the train step
-// (M = 3200 ... 8320 tokens, N = 768 ... 3072, K = 768 ... 3072: GPT-2 / CLIP / mapper projections and their dX).
-//
-// Why: the 128 x 128 tile kernels above keep ONE 32 KiB stage in flight per block; at 2-3 blocks/CU that is
-// ~64-96 KiB in flight per CU against ~1 us of loaded L2/MALL latency, so they stage at ~50 GB/s per CU and run
-// at ~0.23 of the bf16 peak (profiles/r01_*). Here one workgroup per CU owns the whole LDS:
-//   - tile BM x 128 (BM = 64 WM; WM = 4: 256 x 128, 8 waves as 4 (M) x 2 (N), each wave 64 x 64 = 4 x 4 MFMA
-//     16x16x32 tiles), K advancing 64 per step (128-byte LDS rows, XOR-swizzled 16-byte chunks as lds_off);
-//   - an NSLOT-deep ring of LDS stages filled by LDS-DMA (buffer_load ... lds) with AHEAD = NSLOT - 1 steps in
-//     flight while a step is computed: counted `s_waitcnt vmcnt(N)` + raw s_barrier, never vmcnt(0) in steady
-//     state (cdna_hip_programming.md §5 "Pipelining across barriers");
-//   - persistent: the grid is one block per CU and each block walks its output tiles (units u = wg, wg + G, ...)
-//     as ONE continuous stream of k-steps, so the DMA of the next tile's first stages is already in flight while
-//     the current tile's epilogue runs (short-K products no longer pay a pipeline fill per tile);
-//   - fragment reads, the epilogue's operand prefetch and its LDS staging are inline asm, so hipcc never drains
-//     the DMA queue in front of them (it would wait vmcnt(0) before any LDS read following an LDS-DMA issue);
-//     the epilogue stores are range-checked buffer stores (exact instruction count, no branches).
-// Block -> tile placement is XCD-aware (consecutive units on one XCD share A row panels / B column panels in L2).
-// Constraints (checked by the host plan): bf16 A/B/C, K % 8 == 0, N % 8 == 0, every epilogue operand and its
-// leading dimension 16-byte aligned, beta == 0, one K split.
-namespace ring {
-constexpr int BN = 128;
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-typedef int v4i_t __attribute__((ext_vector_type(4)));
-
-// wave-uniform buffer descriptor as 4 SGPRs for inline asm (same fields as make_rsrc: stride 0, raw buffer)
-__device__ __forceinline__ v4i_t rsrc4(const void* base, uint64_t bytes) {
-  const uint64_t b = reinterpret_cast<uint64_t>(base);
-  const uint32_t n = bytes > 0x7fffffffull ? 0x7fffffffu : (uint32_t)bytes;
-  v4i_t r;
-  r.x = (int)__builtin_amdgcn_readfirstlane((uint32_t)b);
-  r.y = (int)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xffffu);
-  r.z = (int)__builtin_amdgcn_readfirstlane(n);
-  r.w = 0x00020000;
-  return r;
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t as_rsrc(v4i_t r) {
-  return __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(((uint64_t)(uint32_t)r.y << 32) | (uint32_t)r.x), (short)0, r.z, r.w);
-}
-
-// one fp32 to LDS (asm: invisible to hipcc's LDS-DMA alias tracking). FIRST: the value may come straight from an
-// MFMA accumulator, which an asm reader must not touch for 12 wait states (cdna_hip_programming.md §5.7 item 2)
-template <int OFF, bool FIRST>
-__device__ __forceinline__ void ds_w32(uint32_t a, float x) {
-  if constexpr (FIRST) asm volatile("s_nop 7\n\ts_nop 7\n\tds_write_b32 %0, %1 offset:%2" ::"v"(a), "v"(x), "i"(OFF));
-  else asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(a), "v"(x), "i"(OFF));
-}
-
-#define ICAP_RING_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
-}  // namespace ring
-
-template <int WM, int NSLOT>
-__global__ __launch_bounds__(128 * WM, 1) void gemm_ring_kernel(icap_gemm_args p, int tiles_m, int tiles_n, int nunits,
-                                                                 uint32_t drop_thresh, float inv_keep) {
-  using namespace ring;
-  constexpr int NW = 2 * WM;                // waves
-  constexpr int BM = 64 * WM;
-  constexpr int SLOT = (BM + BN) * GROWB;   // bytes per ring slot (one 64-deep k-step of A and B)
-  constexpr int APW = BM / 8 / NW;          // 8-row DMA pieces per wave per step: A
-  constexpr int BPW = BN / 8 / NW;          //                                     B
-  constexpr int D = APW + BPW;              // DMA instructions per wave per step (the vmcnt unit)
-  constexpr int ELD = 68;                   // fp32 row stride of the epilogue staging tile (bank-conflict-free writes)
-  static_assert(NW * 16 * ELD * 4 <= SLOT, "epilogue staging must fit one ring slot");
-  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT + 2 * NW * 1024];  // ring + bias (2 units)
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int G = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int64_t M = p.M, N = p.N, K = p.K;
-  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;
-  const int nk = (int)((K + 63) / 64);
-  const bf16_t* Ag = reinterpret_cast<const bf16_t*>(p.A);
-  const bf16_t* Bg = reinterpret_cast<const bf16_t*>(p.B);
-
-  auto unit_tm = [&](int u) { return p.m_dev ? u % tiles_m : u / tiles_n; };
-  auto unit_tn = [&](int u) { return p.m_dev ? u / tiles_m : u % tiles_n; };
-  auto next_valid = [&](int u) {
-    while (u < nunits && (int64_t)unit_tm(u) * BM >= Mv) u += G;
-    return u;
-  };
-
-  // ---- producer: LDS-DMA of k-step (pu, pk) into ring slot pslot (and, with a unit's first step, its bias) ------
-  const int lrow = lane >> 3;
-  const int lchunk = ((lane & 7) ^ lrow) * 8;  // logical K offset (elements) of this lane's 16 bytes
-  const uint32_t va0 = (uint32_t)((lrow * p.lda + lchunk) * 2), vb0 = (uint32_t)((lrow * p.ldb + lchunk) * 2);
-  const uint32_t lda8 = (uint32_t)(p.lda * 16), ldb8 = (uint32_t)(p.ldb * 16);  // bytes per 8 rows
-  const bool has_bias = p.bias && p.dact == ICAP_ACT_NONE;
-  int pu = next_valid(wg), pk = 0, pslot = 0, prod = 0, pbias = 0;
-  int64_t pn0 = 0;  // first column of the producer's unit
-  __amdgpu_buffer_rsrc_t pra = make_rsrc_u(Ag, 16), prb = make_rsrc_u(Bg, 16);
-  auto set_prod = [&]() {
-    if (pu < nunits) {
-      const int64_t m0 = (int64_t)unit_tm(pu) * BM, n0 = (int64_t)unit_tn(pu) * BN;
-      pn0 = n0;
-      const int64_t mr = Mv - m0 < BM ? Mv - m0 : BM, nr = N - n0 < BN ? N - n0 : BN;
-      pra = make_rsrc_u(Ag + m0 * p.lda, (uint64_t)((mr - 1) * p.lda + K) * 2);
-      prb = make_rsrc_u(Bg + n0 * p.ldb, (uint64_t)((nr - 1) * p.ldb + K) * 2);
-    }
-  };
-  set_prod();
-  // block-uniform: every wave issues the same DMA count (D, + 1 with a unit's first step when there is a bias), or
-  // none once the stream has ended
-  auto produce = [&]() {
-    if (pu >= nunits) return;
-    const int64_t k0 = (int64_t)pk * 64;
-    const bool kin = k0 + lchunk < K;  // K % 8 == 0: a 16-byte chunk is wholly inside or outside
-    const uint32_t va = kin ? va0 : OOB, vb = kin ? vb0 : OOB;
-    char* st = smem + pslot * SLOT;
-    if (pk == 0 && has_bias) {  // this unit's 128 bias values -> the wave's area of bias buffer (unit parity)
-      const __amdgpu_buffer_rsrc_t brs = make_rsrc_u(p.bias, (uint64_t)N * 4);
-      dma16(brs, smem + NSLOT * SLOT + (pbias * NW + wave) * 1024,
-            lane < 16 ? (uint32_t)((pn0 + wn * 64) * 4 + 16 * lane) : OOB);
-    }
-#pragma unroll
-    for (int i = 0; i < APW; ++i) {
-      const int pc = wave * APW + i;
-      dma16s(pra, st + pc * 8 * GROWB, va, __builtin_amdgcn_readfirstlane((uint32_t)pc * lda8 + (uint32_t)(k0 * 2)));
-    }
-#pragma unroll
-    for (int j = 0; j < BPW; ++j) {
-      const int pc = wave * BPW + j;
-      dma16s(prb, st + BM * GROWB + pc * 8 * GROWB, vb,
-             __builtin_amdgcn_readfirstlane((uint32_t)pc * ldb8 + (uint32_t)(k0 * 2)));
-    }
-    ++prod;
-    pslot = pslot + 1 == NSLOT ? 0 : pslot + 1;
-    if (++pk == nk) {
-      pk = 0;
-      pbias ^= 1;
-      pu = next_valid(pu + G);
-      set_prod();
-    }
-  };
-
-  // ---- consumer fragment addressing (lds_off of rows wm*64 + i*16 + fr / BM + wn*64 + j*16 + fr) ----------------
-  const int fr = lane & 15, fg = lane >> 4;
-  const uint32_t smem_base = (uint32_t)reinterpret_cast<uintptr_t>(smem);
-  uint32_t la[2], lb[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    const uint32_t sw = (uint32_t)(((ks * 4 + fg) ^ (fr & 7)) << 4);
-    la[ks] = (uint32_t)((wm * 64 + fr) * GROWB) + sw;
-    lb[ks] = (uint32_t)((BM + wn * 64 + fr) * GROWB) + sw;
-  }
-
-  // ---- epilogue geometry: lane -> 8 consecutive columns of one row, 8 rows per wave instruction ----------------
-  const int er = lane >> 3, ec = (lane & 7) * 8;
-  const bool use_dact = p.dact != ICAP_ACT_NONE;
-  const bf16_t* esrc = use_dact ? reinterpret_cast<const bf16_t*>(p.dact_src) : reinterpret_cast<const bf16_t*>(p.resid);
-  const int64_t eld = use_dact ? p.ld_dact : p.ldr;
-  const bool has_pre = esrc != nullptr;
-  const uint64_t seed = drop_thresh != 0u ? eff_seed(p.seed, p.seed_ptr) : 0ull;
-
-  // ---- main loop ------------------------------------------------------------------------------------------------
-  // A k-step g is two phases, one per 32-deep half (ks) of its 64-deep slot; fragment registers R0 (ks 0) and R1
-  // (ks 1), 8 ds_read_b128 each (A rows, B columns):
-  //   X(g): read R1 <- slot g ks 1;               16 MFMAs on R0 (read during Y(g-1))
-  //   Y(g): R1 reads retired (this wave is done with slot g); wait until step g+1 landed (counted vmcnt: the
-  //         AHEAD-1 younger steps stay in flight); s_barrier (every wave's DMA of g+1 landed, every wave done with
-  //         slot g); DMA step g+NSLOT into slot g; read R0 <- slot g+1 ks 0; 16 MFMAs on R1.
-  // So the LDS reads of one half overlap the MFMAs of the other and the DMA issue sits among MFMAs, with NSLOT - 1
-  // steps in flight. At a unit's last step the DMA of Y(g) is deferred past the epilogue, which stages the
-  // accumulators through slot g (free then); R0 then already holds the next unit's first half.
-  u32x4_t R0[8], R1[8];
-  auto read_half = [&](u32x4_t (&R)[8], int slot, int ks) __attribute__((always_inline)) {
-    const uint32_t a = smem_base + (uint32_t)(slot * SLOT) + la[ks], b = smem_base + (uint32_t)(slot * SLOT) + lb[ks];
-    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(R[0]) : "v"(a));
-    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(R[1]) : "v"(a));
-    asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(R[2]) : "v"(a));
-    asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(R[3]) : "v"(a));
-    asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(R[4]) : "v"(b));
-    asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(R[5]) : "v"(b));
-    asm volatile("ds_read_b128 %0, %1 offset:4096" : "=v"(R[6]) : "v"(b));
-    asm volatile("ds_read_b128 %0, %1 offset:6144" : "=v"(R[7]) : "v"(b));
-  };
-#define ICAP_RING_LGKM(n, R)                                                                                   \
-  asm volatile("s_waitcnt lgkmcnt(" #n ")"                                                                     \
-               : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7])); \
-  __builtin_amdgcn_sched_barrier(0)
-  // wait until step `s` landed in this wave: the steps produced after it may stay in flight
-  auto wait_step = [&](int s) __attribute__((always_inline)) {
-    __builtin_amdgcn_sched_barrier(0);
-    const int younger = prod - 1 - s;
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * D) : "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(D) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  for (int s = 0; s < NSLOT; ++s) produce();  // prologue: NSLOT steps in flight
-  int g = 0, cslot = 0, cbias = 0;
-  wait_step(0);
-  __builtin_amdgcn_s_barrier();
-  read_half(R0, 0, 0);
-
-  for (int cu = next_valid(wg); cu < nunits; cu = next_valid(cu + G)) {
-    const int64_t m0 = (int64_t)unit_tm(cu) * BM, n0 = (int64_t)unit_tn(cu) * BN;
-    f32x4_t acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    auto mma_half = [&](u32x4_t (&R)[8], int from, int to) __attribute__((always_inline)) {
-#pragma unroll
-      for (int q = from; q < to; ++q) {
-        mfma_chunk<bf16_t>(acc[q >> 2][q & 3], __builtin_bit_cast(uint4, R[q >> 2]), __builtin_bit_cast(uint4, R[4 + (q & 3)]));
-      }
-    };
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool last = kt + 1 == nk;
-      const int nslot = cslot + 1 == NSLOT ? 0 : cslot + 1;
-      // X(g)
-      read_half(R1, cslot, 1);
-      ICAP_RING_LGKM(8, R0);
-      mma_half(R0, 0, 16);
-      // Y(g)
-      __builtin_amdgcn_sched_barrier(0);
-      ICAP_RING_LGKM(0, R1);
-      if (prod > g + 1) wait_step(g + 1);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      read_half(R0, nslot, 0);
-      mma_half(R1, 0, 8);
-      __builtin_amdgcn_sched_barrier(0);
-      if (!last) produce();
-      __builtin_amdgcn_sched_barrier(0);
-      mma_half(R1, 8, 16);
-      cslot = nslot;
-      ++g;
-    }
-
-    // ---- epilogue of unit cu, staged through the slot of its last step --------------------------------------------
-    const int eslot = cslot == 0 ? NSLOT - 1 : cslot - 1;
-    const int64_t col_l = wn * 64 + ec;  // tile-relative column of this lane's 8
-    const int64_t mr = Mv - m0 < BM ? Mv - m0 : BM, nr = N - n0 < BN ? N - n0 : BN;
-    const bool cin = n0 + col_l < N;
-    // residual / activation-gradient operand of this lane's rows: plain buffer loads (hipcc waits for them at first
-    // use; no DMA is issued after them before that), overlapped with the first pass's LDS staging
-    uint4 pre[8];
-    {
-      const __amdgpu_buffer_rsrc_t ers =
-          has_pre ? make_rsrc_u(esrc + m0 * eld + n0, (uint64_t)((mr - 1) * eld + nr) * 2) : make_rsrc_u(Ag, 0);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int64_t rl = wm * 64 + (t >> 1) * 16 + (t & 1) * 8 + er;
-        pre[t] = has_pre ? bload(ers, cin ? (uint32_t)((rl * eld + col_l) * 2) : OOB) : make_uint4(0u, 0u, 0u, 0u);
-      }
-    }
-    const uint32_t wst = smem_base + (uint32_t)(eslot * SLOT + wave * 16 * ELD * 4);
-    float bias8[8];
-    {
-      u32x4_t b0 = (u32x4_t){0u, 0u, 0u, 0u}, b1 = b0;
-      if (has_bias) {  // this unit's bias landed with its first step (older than every step waited for since)
-        const uint32_t ba = smem_base + (uint32_t)(NSLOT * SLOT + (cbias * NW + wave) * 1024 + (lane & 7) * 32);
-        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(b0), "=&v"(b1) : "v"(ba));
-      }
-      const uint32_t w[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) bias8[e] = __uint_as_float(w[e]);
-    }
-    cbias ^= 1;
-    const __amdgpu_buffer_rsrc_t crs = make_rsrc_u(reinterpret_cast<bf16_t*>(p.C) + m0 * p.ldc + n0,
-                                                  (uint64_t)((mr - 1) * p.ldc + nr) * 2);
-    __amdgpu_buffer_rsrc_t ars = crs;
-    if (p.aux)
-      ars = make_rsrc_u(reinterpret_cast<bf16_t*>(p.aux) + m0 * p.ldaux + n0, (uint64_t)((mr - 1) * p.ldaux + nr) * 2);
-    // per 16-row pass: raw accumulators -> LDS (per-wave region, fp32 [16][68]) -> 8 columns per lane
-    auto pass = [&](auto ic) __attribute__((always_inline)) {
-      constexpr int i = decltype(ic)::value;
-      const uint32_t wa = wst + (uint32_t)(((fg * 4) * ELD + fr) * 4);
-      static_for<0, 4>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        static_for<0, 4>([&](auto vc) {
-          constexpr int v = decltype(vc)::value;
-          constexpr int off = (v * ELD + j * 16) * 4;
-          const float x = acc[i][j][v];
-          ds_w32<off, i == 0 && j == 0 && v == 0>(wa, x);
-        });
-      });
-      const uint32_t ra = wst + (uint32_t)((er * ELD + ec) * 4);
-      u32x4_t r[2][2];
-      asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(r[0][0]) : "v"(ra));
-      asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(r[0][1]) : "v"(ra));
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[1][0]) : "v"(ra), "i"(8 * ELD * 4));
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[1][1]) : "v"(ra), "i"(8 * ELD * 4 + 16));
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0][0]), "+v"(r[0][1]), "+v"(r[1][0]), "+v"(r[1][1]));
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int64_t rl = wm * 64 + i * 16 + t * 8 + er;  // tile-relative row
-        const int64_t row = m0 + rl;
-        float x[8] = {__uint_as_float(r[t][0].x), __uint_as_float(r[t][0].y), __uint_as_float(r[t][0].z),
-                      __uint_as_float(r[t][0].w), __uint_as_float(r[t][1].x), __uint_as_float(r[t][1].y),
-                      __uint_as_float(r[t][1].z), __uint_as_float(r[t][1].w)};
-        float a[8];
-        const bool keep_row = row < Mv;
-        const uint64_t didx = p.offset + (uint64_t)(row * N + n0 + col_l);
-        if (use_dact) {
-          unpack_bf16(pre[i * 2 + t], a);
-          epi_bwd_math<8>(p, x, a, seed, didx, drop_thresh, inv_keep);
-        } else {
-          epi_fwd_act<8>(p, x, bias8, a);
-          if (p.aux) {
-            const uint4 av = make_uint4(f2bf2(a[0], a[1]), f2bf2(a[2], a[3]), f2bf2(a[4], a[5]), f2bf2(a[6], a[7]));
-            const uint32_t aoff = (cin && keep_row) ? (uint32_t)((rl * p.ldaux + col_l) * 2) : OOB;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, av), ars, aoff, 0, 0);
-          }
-          float rr[8];
-          unpack_bf16(pre[i * 2 + t], rr);
-          epi_fwd_tail<8>(x, rr, has_pre, seed, didx, drop_thresh, inv_keep);
-        }
-        const uint4 cv = make_uint4(f2bf2(x[0], x[1]), f2bf2(x[2], x[3]), f2bf2(x[4], x[5]), f2bf2(x[6], x[7]));
-        const uint32_t coff = (cin && keep_row) ? (uint32_t)((rl * p.ldc + col_l) * 2) : OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, cv), crs, coff, 0, 0);
-      }
-    };
-    pass(std::integral_constant<int, 0>{});
-    pass(std::integral_constant<int, 1>{});
-    pass(std::integral_constant<int, 2>{});
-    pass(std::integral_constant<int, 3>{});
-    // every wave is done with the staging slot before the deferred DMA of the last step's Y phase refills it
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    produce();
-  }
-#undef ICAP_RING_LGKM
-  __builtin_amdgcn_sched_barrier(0);
-  ICAP_RING_VMCNT(0);  // nothing of ours in flight when the wave ends
-}
-#undef ICAP_RING_VMCNT
-
 }  // namespace icap
 
 using namespace icap;
 
-// Tile-kernel variant for the launches the ring kernel does not take (f32 parity mode, K-outer dW products, beta,
-// split-K). Measured on MI355X (tools/gemm_bench.py, profiles/r01_gemm_variants.txt): short K (<= 16 stages) is
+// Tile-kernel variant. Measured on MI355X (tools/gemm_bench.py, profiles/r01_gemm_variants.txt): short K (<= 16 stages) is
 // bound by the per-block prologue/epilogue, which co-resident blocks hide -> single LDS buffer, 3-4 blocks/CU (4
 // when the epilogue moves a second M x N tensor: dact_src read / aux store); long K favours the double-buffered
 // main loop at 2 blocks/CU.
@@ -1057,18 +719,7 @@ static int gemm_variant(const icap_gemm_args& p, int64_t nk_per_block) {
   return heavy ? 5 : 4;
 }
 
-// The ring kernel is opt-in: per call with path == 2, or for every eligible launch with ICAP_GEMM_RING=1. r02
-// measured it bit-identical to the tile kernels but 2-25 % slower on the step's shapes ("ring GEMM"),
-// so the tile kernels stay the default.
-static bool gemm_ring_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("ICAP_GEMM_RING");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// compute units of the current device (the ring kernel's persistent grid: one workgroup per CU)
+// compute units of the current device (the skinny-GEMM grid rule, the 256 x 256 kernel's pick)
 static int device_cus() {
   static int cus[64] = {0};
   int dev = 0;
@@ -1100,7 +751,7 @@ static int g256_mode() {
 // head 8320 x 50304 x 768: 758 vs 835 us), not on the train step's 2-round K = 768 products (8320 x 3072 x 768:
 // 84 vs 80 us) (profiles/r02_gemm256_bench.txt). path 3 forces it where eligible.
 static bool g256_pick(const icap_gemm_args& p) {
-  if (p.path == 1 || p.path == 2) return false;
+  if (p.path == 1) return false;
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.beta != 0.f || p.m_dev || p.split_k > 1) return false;
   if (p.M < 256 || p.N < 256 || p.K < 64) return false;
   if (p.path == 3 || g256_mode() == 2) return true;
@@ -1119,9 +770,8 @@ struct GemmPlan {
   bool g256 = false;     // the 256 x 256 8-phase kernel (gemm256.hip)
   int nt = 1;            // skinny: 16-column slabs per block
   int sku = 3;           // skinny: k-steps in flight per wave
-  int ring = 0;          // ring kernel: WM (4 = 256 x 128 tiles, 2 = 128 x 128), 0 = not used
   int variant = 0;       // tile kernel (see ICAP_GEMM_LAUNCH)
-  int splits = 1, nk_split = 0, tiles_n = 0, tiles_m = 0, units = 0;
+  int splits = 1, nk_split = 0, tiles_n = 0;
   dim3 grid, block;
   uint32_t thr = 0;
   float inv_keep = 1.f;
@@ -1130,21 +780,9 @@ struct GemmPlan {
 
 static bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
-// The ring kernel's preconditions (see gemm_ring_kernel).
-static bool ring_eligible(const icap_gemm_args& p) {
-  if (p.path == 1 || (p.path != 2 && !gemm_ring_enabled())) return false;
-  if (p.in_dtype != ICAP_BF16 || p.c_dtype != ICAP_BF16 || p.trans_ab || p.beta != 0.f || p.ln_gamma) return false;
-  // K > 128: three k-steps per tile at least (a unit's bias buffer is reused two units later; see the kernel)
-  if (p.split_k > 1 || p.M <= 128 || p.K <= 128 || (p.N & 7) || (p.K & 7) || (p.ldc & 7) || !al16(p.C)) return false;
-  if (p.aux && ((p.ldaux & 7) || !al16(p.aux))) return false;
-  if (p.dact != ICAP_ACT_NONE && ((p.ld_dact & 7) || !al16(p.dact_src))) return false;
-  if (p.dact == ICAP_ACT_NONE && p.resid && ((p.ldr & 7) || !al16(p.resid))) return false;
-  if (p.bias && (reinterpret_cast<uintptr_t>(p.bias) & 3)) return false;
-  return true;
-}
-
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
+  ICAP_REQUIRE(p.path == 0 || p.path == 1 || p.path == 3, "icap_gemm: path must be 0, 1 or 3");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16, "icap_gemm: bad in_dtype");
   ICAP_REQUIRE(p.c_dtype == ICAP_F32 || p.c_dtype == ICAP_BF16, "icap_gemm: bad c_dtype");
@@ -1202,21 +840,6 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // 256 x 256 8-phase kernel (gemm256.hip) for wide products whose 256-tiles fill the chip in few, full rounds
   if (g256_pick(p)) {
     pl.g256 = true;
-    return ICAP_OK;
-  }
-  // persistent ring kernel (one workgroup per CU, many output tiles each) for every eligible launch except the
-  // decode-sized ones (<= 64 tiles of 128 x 128), which keep split-K unless the caller asks for one pass:
-  // 256 x 128 tiles when they give every CU work, 128 x 128 otherwise
-  if (ring_eligible(p) && (p.split_k == 1 || tiles > 64)) {
-    const int cus = device_cus();
-    const int64_t tn = (p.N + 127) / 128;
-    const int64_t tm4 = (p.M + 255) / 256, tm2 = (p.M + 127) / 128;
-    pl.ring = tm4 * tn >= cus * 3 / 4 ? 4 : 2;
-    pl.tiles_m = (int)(pl.ring == 4 ? tm4 : tm2);
-    pl.tiles_n = (int)tn;
-    pl.units = pl.tiles_m * pl.tiles_n;
-    pl.grid = dim3((unsigned)(pl.units < cus ? pl.units : cus));
-    pl.block = dim3(128 * pl.ring);
     return ICAP_OK;
   }
   // split-K over K stages for launches that cannot fill the chip (decode-time M = batch, small projections):
@@ -1290,11 +913,9 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
     return buf;
   }
   if (pl.skinny) snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2, %d>", pl.nt, pl.sku);
-  else if (pl.ring) snprintf(fmt, sizeof fmt, "gemm_ring_kernel<%d, %d>", pl.ring, pl.ring == 4 ? 3 : 4);
   else snprintf(fmt, sizeof fmt, "%s", variant_kernel(pl.variant));
   char inner[128];
-  if (pl.ring) snprintf(inner, sizeof inner, "%s", fmt);
-  else snprintf(inner, sizeof inner, fmt, ti, tc);
+  snprintf(inner, sizeof inner, fmt, ti, tc);
   snprintf(buf, sizeof buf, "icap::%s", inner);
   return buf;
 }
@@ -1346,15 +967,6 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     return check_launch("icap_gemm(skinny)");
   }
   if (pl.g256) return gemm256_launch(p, thr, inv_keep, s);
-  if (pl.ring) {
-    if (pl.ring == 4)
-      hipLaunchKernelGGL((gemm_ring_kernel<4, 3>), pl.grid, pl.block, 0, s, p, pl.tiles_m, pl.tiles_n, pl.units, thr,
-                         inv_keep);
-    else
-      hipLaunchKernelGGL((gemm_ring_kernel<2, 4>), pl.grid, pl.block, 0, s, p, pl.tiles_m, pl.tiles_n, pl.units, thr,
-                         inv_keep);
-    return check_launch("icap_gemm(ring)");
-  }
   const dim3 grid = pl.grid, block = pl.block;
   const int sp = pl.splits, nks = pl.nk_split, tn = pl.tiles_n;
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));

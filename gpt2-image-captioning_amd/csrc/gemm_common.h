@@ -1,4 +1,4 @@
-// Shared pieces of the GEMM kernels (gemm.hip: tile / skinny / ring kernels; gemm256.hip: the 256x256 8-phase
+// Shared pieces of the GEMM kernels (gemm.hip: tile / skinny kernels; gemm256.hip: the 256x256 8-phase
 // kernel): MFMA chunk wrappers, buffer descriptors, LDS-DMA and buffer-load helpers, the XOR-swizzled LDS row
 // layout, and the epilogue arithmetic every kernel applies (one formula, fixed contraction: bitwise-equal
 // outputs across kernels that accumulate in the same order).
@@ -123,9 +123,9 @@ __device__ __forceinline__ void unpack_bf16(const uint4 w, float v[8]) {
   unpack_bf16(make_uint2(w.z, w.w), v + 4);
 }
 
-// The epilogue arithmetic, shared by every GEMM kernel (tile, split-K reduce, skinny, ring): one formula with a
+// The epilogue arithmetic, shared by every GEMM kernel (tile, split-K reduce, skinny, 256 x 256): one formula with a
 // fixed contraction (explicit fma for alpha*acc + bias, no other fusing), so two kernels that accumulate a product
-// in the same order store bitwise-identical outputs (tests/test_gemm_ring_gpu.py).
+// in the same order store bitwise-identical outputs (tests/test_gemm256_gpu.py).
 // backward form: x = alpha * acc * dropmask * act'(a)
 template <int W>
 __device__ __forceinline__ void epi_bwd_math(const icap_gemm_args& p, float x[W], const float a[W], uint64_t seed,

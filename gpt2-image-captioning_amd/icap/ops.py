@@ -71,7 +71,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None,
          alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None,
          trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None,
-         tile_only: bool = False, ring: bool = False, g256: bool = False) -> Tensor:
+         tile_only: bool = False, g256: bool = False) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
     workspace: fp32 split-K scratch for launches on a stream other than the package's main one (the per-device
     default serves every GEMM ordered on one stream). The split count depends on the shape alone, so the result
@@ -81,8 +81,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).
     split_k: 0 = automatic split-K for launches of <= 64 output tiles, 1 = never, > 1 = forced.
     m_dev: device int32 row count <= M (rows past it are neither computed nor stored).
-    tile_only: the 128-row tile kernels only; ring: the persistent ring kernel wherever its preconditions hold
-    (it is opt-in: A/B measurements, path-equality tests); g256: the 256 x 256 kernel wherever eligible."""
+    tile_only: the 128-row tile kernels only; g256: the 256 x 256 kernel wherever eligible (A/B measurements,
+    path-equality tests)."""
     if trans_ab:
         M = A.shape[1] if M is None else M
         K = A.shape[0] if K is None else K
@@ -115,7 +115,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     ws = gemm_workspace(A.device) if workspace is None else workspace
     a.workspace, a.workspace_bytes, a.split_k = ws.data_ptr(), ws.numel() * 4, split_k
     a.m_dev = _p(m_dev)
-    a.path = 1 if tile_only else (2 if ring else (3 if g256 else 0))
+    a.path = 1 if tile_only else (3 if g256 else 0)
     if ln is not None:
         a.ln_gamma, a.ln_beta, a.ln_eps = ln[0].data_ptr(), ln[1].data_ptr(), float(ln[2])
     if GEMM_TIMER is None:

@@ -104,9 +104,9 @@ typedef struct {
   /* then * ln_gamma[k] + ln_beta[k], rounded to the input dtype) — the decode step's ln_1 / ln_2 fused    */
   /* into the QKV / c_fc GEMMs (HF/models/gpt2/modeling_gpt2.py:281,301). Only for M <= 128 launches.     */
   const float* ln_gamma; const float* ln_beta; float ln_eps;
-  /* path: 0 = automatic kernel choice (tile kernels; the ring kernel too when ICAP_GEMM_RING=1);             */
-  /* 1 = the 128-row tile kernels only; 2 = the persistent ring kernel wherever its preconditions hold;        */
-  /* 3 = the 256 x 256 8-phase kernel wherever its preconditions hold (bf16 A/B, no trans_ab / ln / beta /     */
+  /* path: 0 = automatic kernel choice; 1 = the 128-row tile kernels only; (2: the round-2 persistent ring    */
+  /* kernel, measured slower and removed: rejected); 3 = the 256 x 256 8-phase kernel wherever its           */
+  /* preconditions hold (bf16 A/B, no trans_ab / ln / beta /                                                   */
   /*     m_dev / split-K, M and N >= 256) —                                                                      */
   /* for A/B measurements and for tests that compare the two paths (identical MFMA chains: bitwise equal).     */
   int32_t path;

@@ -12,7 +12,7 @@ import torch
 
 from icap import _lib as L
 from icap import ops
-from test_gemm_ring_gpu import _assert_same, _run, rnd
+from gemm_helpers import _assert_same, _run, rnd
 
 pytestmark = pytest.mark.gpu
 
