@@ -511,61 +511,55 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   // gamma / beta are staged in LDS when K <= SK_LNK (above); the barriers below publish them.
   __shared__ float ln_mr[BM][2];
   __shared__ float lnp[SK_WAVES][BM];
+  __shared__ float lnp2[SK_WAVES][BM];
   // (instantiations with few fragment registers only: the others would spill; LN-fused launches have K = D)
   constexpr bool LN_FRAG = ES == 2 && SKU * (MT + NT) <= 24;
   const bool ln_frag = LN_FRAG && fuse_ln && nks <= (int64_t)SK_WAVES * SKU;
   float ln_mean[MT], ln_rs[MT];
   if (LN_FRAG && ln_frag) {
+    // one pass over the fragments: per-row sum and sum of squares, reduced together (lane groups by shuffles, the
+    // 8 waves through LDS in a fixed order), var = E[x^2] - mean^2 in fp32 (bf16 inputs: the mean is an exact
+    // rounding away from any catastrophic cancellation that matters at bf16 output precision)
     auto chunk_in = [&](int u) { return (int64_t)(wave + u * SK_WAVES) * KSTEP + fg * EPC < K; };
-    auto reduce_rows = [&](float part[MT], float out[MT]) {  // lane partials -> row totals (every lane of the row)
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        part[i] += __shfl_xor(part[i], 16, 64);
-        part[i] += __shfl_xor(part[i], 32, 64);
-        if (fg == 0) lnp[wave][i * 16 + fr] = part[i];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        float t = 0.f;
-#pragma unroll
-        for (int w = 0; w < SK_WAVES; ++w) t += lnp[w][i * 16 + fr];
-        out[i] = t;
-      }
-      __syncthreads();
-    };
-    float part[MT], tot[MT];
+    float part[MT], part2[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       part[i] = 0.f;
+      part2[i] = 0.f;
 #pragma unroll
       for (int u = 0; u < SKU; ++u) {
         if (chunk_in(u)) {
           float v[8];
           unpack_bf16(af[u][i], v);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) part[i] += v[e];
+          for (int e = 0; e < 8; ++e) {
+            part[i] += v[e];
+            part2[i] += v[e] * v[e];
+          }
         }
       }
+      part[i] += __shfl_xor(part[i], 16, 64);
+      part[i] += __shfl_xor(part[i], 32, 64);
+      part2[i] += __shfl_xor(part2[i], 16, 64);
+      part2[i] += __shfl_xor(part2[i], 32, 64);
+      if (fg == 0) {
+        lnp[wave][i * 16 + fr] = part[i];
+        lnp2[wave][i * 16 + fr] = part2[i];
+      }
     }
-    reduce_rows(part, tot);
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      ln_mean[i] = tot[i] / (float)K;
-      part[i] = 0.f;
+      float t = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int u = 0; u < SKU; ++u) {
-        if (chunk_in(u)) {
-          float v[8];
-          unpack_bf16(af[u][i], v);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) part[i] += (v[e] - ln_mean[i]) * (v[e] - ln_mean[i]);
-        }
+      for (int w = 0; w < SK_WAVES; ++w) {
+        t += lnp[w][i * 16 + fr];
+        t2 += lnp2[w][i * 16 + fr];
       }
+      ln_mean[i] = t / (float)K;
+      const float var = t2 / (float)K - ln_mean[i] * ln_mean[i];
+      ln_rs[i] = 1.f / sqrtf((var > 0.f ? var : 0.f) + p.ln_eps);
     }
-    reduce_rows(part, tot);
-#pragma unroll
-    for (int i = 0; i < MT; ++i) ln_rs[i] = 1.f / sqrtf(tot[i] / (float)K + p.ln_eps);
   } else if (fuse_ln) {
     const int t = threadIdx.x & 15;
     for (int rr = threadIdx.x >> 4; rr < BM; rr += 64 * SK_WAVES / 16) {
