@@ -88,6 +88,10 @@ class CaptionTrainer:
         seen = {id(p) for ps in groups for p in ps}
         self._ranges_front = flat_ranges(flat, [p for p in flat.params if id(p) not in seen])
         self.dp_overlap = os.environ.get("ICAP_DP_OVERLAP", "1") != "0"
+        # opt-in: all-reduce the gradients as bf16 (half the bytes over xGMI; the sum over ranks is rounded to bf16
+        # per element, so it is not the fp32 reduction the reference's single-process step corresponds to)
+        self.dp_bf16 = os.environ.get("ICAP_DP_BF16", "0") == "1"
+        self._g16 = None
         self.seg_graphs = {}  # zero -> [HIP graph per segment] (data-parallel overlapped step)
         self._comm = None
         if model.task_prefix_embeds is not None:
@@ -230,7 +234,29 @@ class CaptionTrainer:
 
     def _allreduce(self) -> None:
         if self.world > 1:
-            torch.distributed.all_reduce(self.flat.flat_grad, group=self.pg)
+            if self.dp_bf16:
+                g = self.flat.flat_grad
+                self._to16(g, 0, g.numel())
+                torch.distributed.all_reduce(self._g16, group=self.pg)
+                self._from16(g, [(0, g.numel())])
+            else:
+                torch.distributed.all_reduce(self.flat.flat_grad, group=self.pg)
+
+    def _to16(self, g, lo: int, hi: int) -> None:
+        """bf16 staging copy of flat_grad[lo:hi] (the dp_bf16 all-reduce), on the current stream."""
+        if self._g16 is None:
+            self._g16 = torch.empty(g.numel(), dtype=torch.bfloat16, device=g.device)
+        if g.is_cuda:
+            ops.convert(g[lo:hi].view(1, -1), self._g16[lo:hi].view(1, -1))
+        else:  # CPU dry runs (gloo tests): no kernels
+            self._g16[lo:hi].copy_(g[lo:hi])
+
+    def _from16(self, g, ranges) -> None:
+        for lo, hi in ranges:
+            if g.is_cuda:
+                ops.convert(self._g16[lo:hi].view(1, -1), g[lo:hi].view(1, -1))
+            else:
+                g[lo:hi].copy_(self._g16[lo:hi])
 
     def _bucket(self, ranges, works) -> None:
         """All-reduce these flat-gradient ranges behind the work queued so far on this stream, on a communication
@@ -238,6 +264,7 @@ class CaptionTrainer:
         g = self.flat.flat_grad
         if not ranges:
             return
+        src = (lambda lo, hi: self._g16[lo:hi]) if self.dp_bf16 else (lambda lo, hi: g[lo:hi])
         if g.is_cuda:
             if self._comm is None:
                 self._comm = torch.cuda.Stream(g.device)
@@ -246,15 +273,22 @@ class CaptionTrainer:
             with torch.cuda.stream(self._comm):
                 self._comm.wait_event(ev)
                 for lo, hi in ranges:
-                    works.append(torch.distributed.all_reduce(g[lo:hi], group=self.pg, async_op=True))
+                    if self.dp_bf16:
+                        self._to16(g, lo, hi)
+                    works.append(torch.distributed.all_reduce(src(lo, hi), group=self.pg, async_op=True))
         else:
             for lo, hi in ranges:
-                works.append(torch.distributed.all_reduce(g[lo:hi], group=self.pg, async_op=True))
+                if self.dp_bf16:
+                    self._to16(g, lo, hi)
+                works.append(torch.distributed.all_reduce(src(lo, hi), group=self.pg, async_op=True))
+        if self.dp_bf16:
+            self._pending16.extend(ranges)
 
     def _overlapped_step(self, zero: bool, use_graph: bool) -> None:
         """Data-parallel micro-batch that ends an accumulation cycle: each segment's gradient ranges are
         all-reduced (RCCL, async) while the later segments of the backward run; the optimizer waits for all."""
         works = []
+        self._pending16 = []
         if use_graph:
             graphs = self.seg_graphs.get(zero)
             if graphs is None:
@@ -268,6 +302,8 @@ class CaptionTrainer:
                 self._bucket(rng, works)
         for w in works:
             w.wait()
+        if self.dp_bf16:  # the reduced bf16 ranges back into the fp32 gradient the optimizer reads
+            self._from16(self.flat.flat_grad, self._pending16)
         if use_graph:
             if self.graph_opt is None:
                 self.graph_opt = self._capture_opt()
