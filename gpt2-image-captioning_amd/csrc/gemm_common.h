@@ -126,16 +126,36 @@ __device__ __forceinline__ void unpack_bf16(const uint4 w, float v[8]) {
 // The epilogue arithmetic, shared by every GEMM kernel (tile, split-K reduce, skinny, 256 x 256): one formula with a
 // fixed contraction (explicit fma for alpha*acc + bias, no other fusing), so two kernels that accumulate a product
 // in the same order store bitwise-identical outputs (tests/test_gemm256_gpu.py).
+// The activation is a runtime argument: it is dispatched ONCE per W-element call, each case a straight run over the
+// W elements. (A switch inside the element loop put every activation's code — libm tanhf / erff included — W times
+// into every unrolled epilogue call site; any activated launch then executed through that code and paid for it in
+// instruction fetch: 8320 x 3072 x 768 with relu 97 us vs 61 plain, tools/act_epilogue_probe.py.) The arithmetic
+// per element is unchanged (act_fwd / act_bwd), so outputs are bitwise the same.
 // backward form: x = alpha * acc * dropmask * act'(a)
 template <int W>
 __device__ __forceinline__ void epi_bwd_math(const icap_gemm_args& p, float x[W], const float a[W], uint64_t seed,
                                              uint64_t didx, uint32_t drop_thresh, float inv_keep) {
 #pragma clang fp contract(off)
+  float y[W];
 #pragma unroll
   for (int e = 0; e < W; ++e) {
-    float y = p.alpha * x[e];
-    if (drop_thresh != 0u) y = y * drop_scale(seed, didx + e, drop_thresh, inv_keep);
-    x[e] = y * act_bwd(p.dact, a[e]);
+    y[e] = p.alpha * x[e];
+    if (drop_thresh != 0u) y[e] = y[e] * drop_scale(seed, didx + e, drop_thresh, inv_keep);
+  }
+  switch (p.dact) {
+#define ICAP_DACT_CASE(A)                                              \
+  case A:                                                              \
+    _Pragma("unroll") for (int e = 0; e < W; ++e) x[e] = y[e] * act_bwd(A, a[e]); \
+    break;
+    ICAP_DACT_CASE(ICAP_ACT_GELU_NEW)
+    ICAP_DACT_CASE(ICAP_ACT_RELU)
+    ICAP_DACT_CASE(ICAP_ACT_QUICK_GELU)
+    ICAP_DACT_CASE(ICAP_ACT_TANH)
+    ICAP_DACT_CASE(ICAP_ACT_GELU_ERF)
+#undef ICAP_DACT_CASE
+    default:
+#pragma unroll
+      for (int e = 0; e < W; ++e) x[e] = y[e] * act_bwd(ICAP_ACT_NONE, a[e]);
   }
 }
 // forward form, first half: x = act(alpha * acc + bias); a = the aux value (pre-activation, or tanh output)
@@ -144,13 +164,26 @@ __device__ __forceinline__ void epi_fwd_act(const icap_gemm_args& p, float x[W],
 #pragma clang fp contract(off)
 #pragma unroll
   for (int e = 0; e < W; ++e) x[e] = __builtin_fmaf(p.alpha, x[e], biasw[e]);
-  if (p.act != ICAP_ACT_NONE || p.aux) {
+  switch (p.act) {
+#define ICAP_ACT_CASE(A)                                              \
+  case A:                                                             \
+    _Pragma("unroll") for (int e = 0; e < W; ++e) {                   \
+      const float y = act_fwd(A, x[e]);                               \
+      a[e] = (A == ICAP_ACT_TANH) ? y : x[e];                         \
+      x[e] = y;                                                       \
+    }                                                                 \
+    break;
+    ICAP_ACT_CASE(ICAP_ACT_GELU_NEW)
+    ICAP_ACT_CASE(ICAP_ACT_RELU)
+    ICAP_ACT_CASE(ICAP_ACT_QUICK_GELU)
+    ICAP_ACT_CASE(ICAP_ACT_TANH)
+    ICAP_ACT_CASE(ICAP_ACT_GELU_ERF)
+#undef ICAP_ACT_CASE
+    default:
+      if (p.aux) {
 #pragma unroll
-    for (int e = 0; e < W; ++e) {
-      const float y = act_fwd(p.act, x[e]);
-      a[e] = (p.act == ICAP_ACT_TANH) ? y : x[e];
-      x[e] = y;
-    }
+        for (int e = 0; e < W; ++e) a[e] = x[e];
+      }
   }
 }
 // forward form, second half: x = x * dropmask (+ r)
