@@ -164,6 +164,13 @@ __device__ __forceinline__ void epi_fwd_act(const icap_gemm_args& p, float x[W],
 #pragma clang fp contract(off)
 #pragma unroll
   for (int e = 0; e < W; ++e) x[e] = __builtin_fmaf(p.alpha, x[e], biasw[e]);
+  if (__builtin_expect(p.act == ICAP_ACT_NONE, 1)) {  // no activation: keep this path short and first
+    if (p.aux) {
+#pragma unroll
+      for (int e = 0; e < W; ++e) a[e] = x[e];
+    }
+    return;
+  }
   switch (p.act) {
 #define ICAP_ACT_CASE(A)                                              \
   case A:                                                             \
@@ -180,10 +187,7 @@ __device__ __forceinline__ void epi_fwd_act(const icap_gemm_args& p, float x[W],
     ICAP_ACT_CASE(ICAP_ACT_GELU_ERF)
 #undef ICAP_ACT_CASE
     default:
-      if (p.aux) {
-#pragma unroll
-        for (int e = 0; e < W; ++e) a[e] = x[e];
-      }
+      break;
   }
 }
 // forward form, second half: x = x * dropmask (+ r)
