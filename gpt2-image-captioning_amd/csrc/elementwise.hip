@@ -1239,6 +1239,41 @@ extern "C" int icap_prefix_embed(int32_t dtype, int32_t B, int32_t G2, int32_t N
   return check_launch("icap_prefix_embed");
 }
 
+// bf16 form: one thread per (row, q|k, head, 8-element chunk of the first half): two 16-byte loads (elements
+// [8c, 8c + 8) and their partners + hd/2), 16-byte stores; the same per-element arithmetic as rope_patches_kernel
+__global__ void rope_patches8_kernel(int B, int S, int NP, int H, int hd, bf16_t* __restrict__ qkv, int64_t ld,
+                                     const float* __restrict__ cs, const float* __restrict__ sn) {
+#pragma clang fp contract(off)
+  const int half = hd >> 1, nc = half >> 3;
+  const int P = S - NP;
+  const int64_t total = (int64_t)B * P * 2 * H * nc;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % nc);
+    int64_t r = i / nc;
+    const int hq = (int)(r % (2 * H));
+    r /= (2 * H);
+    const int p = (int)(r % P);
+    const int b = (int)(r / P);
+    bf16_t* v = qkv + ((int64_t)b * S + NP + p) * ld + (int64_t)hq * hd + 8 * c;
+    float x1[8], x2[8], cl[8], sl[8], ch[8], sh[8], o1[8], o2[8];
+    io<bf16_t>::ld8(v, x1);
+    io<bf16_t>::ld8(v + half, x2);
+    const float* cp = cs + (int64_t)p * hd + 8 * c;
+    const float* sp = sn + (int64_t)p * hd + 8 * c;
+    io<float>::ld8(cp, cl);
+    io<float>::ld8(sp, sl);
+    io<float>::ld8(cp + half, ch);
+    io<float>::ld8(sp + half, sh);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o1[e] = x1[e] * cl[e] + (-x2[e]) * sl[e];
+      o2[e] = x2[e] * ch[e] + x1[e] * sh[e];
+    }
+    io<bf16_t>::st8(v, o1);
+    io<bf16_t>::st8(v + half, o2);
+  }
+}
+
 extern "C" int icap_rope_patches(int32_t dtype, int32_t B, int32_t S, int32_t NP, int32_t H, int32_t hd, void* qkv,
                                  int64_t ld_qkv, const float* cos_t, const float* sin_t, void* stream) {
   ICAP_REQUIRE(qkv && cos_t && sin_t, "icap_rope_patches: null pointer");
@@ -1246,6 +1281,13 @@ extern "C" int icap_rope_patches(int32_t dtype, int32_t B, int32_t S, int32_t NP
                "icap_rope_patches: bad geometry");
   const int64_t n = (int64_t)B * (S - NP) * H * hd;
   if (n == 0) return ICAP_OK;
+  if (dtype == ICAP_BF16 && hd % 16 == 0 && ld_qkv % 8 == 0 && (reinterpret_cast<uintptr_t>(qkv) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(cos_t) & 15) == 0 && (reinterpret_cast<uintptr_t>(sin_t) & 15) == 0) {
+    const int64_t n8 = n / 8;  // one thread per 8 pairs
+    hipLaunchKernelGGL(rope_patches8_kernel, dim3(nblk(n8, 256, 8192)), dim3(256), 0, S_(stream), B, S, NP, H, hd,
+                       reinterpret_cast<bf16_t*>(qkv), ld_qkv, cos_t, sin_t);
+    return check_launch("icap_rope_patches");
+  }
   DISPATCH_T(dtype, hipLaunchKernelGGL(rope_patches_kernel<T>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B,
                                        S, NP, H, hd, TP(qkv), ld_qkv, cos_t, sin_t));
   return check_launch("icap_rope_patches");

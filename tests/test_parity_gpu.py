@@ -296,6 +296,16 @@ def test_rope_patches_kernel_matches_torch(dev):
     ops.rope_patches(d, cos.to(dev), sin.to(dev), B=B, S=S, NP=NP, H=H, hd=hd)
     torch.cuda.synchronize()
     assert torch.equal(d.cpu(), ref.view(B * S, -1))
+    # bf16 (the 16-byte kernel): the same fp32 arithmetic on the bf16 inputs, rounded once
+    q16 = qkv.to(torch.bfloat16)
+    r16 = q16.float().view(B, S, 3, H, hd).clone()
+    pat = r16[:, NP:, :2]
+    rot = torch.cat((-pat[..., hd // 2:], pat[..., :hd // 2]), dim=-1)
+    r16[:, NP:, :2] = pat * cos[None, :, None, None, :] + rot * sin[None, :, None, None, :]
+    d16 = q16.to(dev)
+    ops.rope_patches(d16, cos.to(dev), sin.to(dev), B=B, S=S, NP=NP, H=H, hd=hd)
+    torch.cuda.synchronize()
+    assert torch.equal(d16.cpu(), r16.view(B * S, -1).to(torch.bfloat16))
 
 
 # ------------------------------------------------------------------------- configs[4] caption model (GPT-2 large)
