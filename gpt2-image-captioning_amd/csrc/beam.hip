@@ -325,6 +325,15 @@ extern "C" size_t icap_beam_workspace_bytes(int32_t B, int32_t W, int32_t T, int
   return (size_t)beam::layout(B, W, T, max_len).total * 4;
 }
 
+extern "C" int icap_beam_layout(int32_t B, int32_t W, int32_t T, int32_t max_len, int64_t* word_offsets) {
+  ICAP_REQUIRE(word_offsets != nullptr, "icap_beam_layout: null output");
+  ICAP_REQUIRE(B >= 0 && W > 0 && T > 0 && max_len > 0, "icap_beam_layout: bad sizes");
+  const beam::Layout l = beam::layout(B, W, T, max_len);
+  const int64_t o[9] = {l.run_score, l.run_seq, l.fin_score, l.fin_len, l.fin_seq, l.fin_cnt, l.done, l.anc, l.total};
+  for (int i = 0; i < 9; ++i) word_offsets[i] = o[i];
+  return ICAP_OK;
+}
+
 static int beam_check(const icap_beam_args* a) {
   ICAP_REQUIRE(a != nullptr, "icap_beam: null args");
   ICAP_REQUIRE(a->W >= 1 && a->W <= 8, "icap_beam: num_beams must be in [1, 8]");

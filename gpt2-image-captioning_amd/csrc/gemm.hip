@@ -517,24 +517,29 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   const bool ln_frag = LN_FRAG && fuse_ln && nks <= (int64_t)SK_WAVES * SKU;
   float ln_mean[MT], ln_rs[MT];
   if (LN_FRAG && ln_frag) {
-    // one pass over the fragments: per-row sum and sum of squares, reduced together (lane groups by shuffles, the
-    // 8 waves through LDS in a fixed order), var = E[x^2] - mean^2 in fp32 (bf16 inputs: the mean is an exact
-    // rounding away from any catastrophic cancellation that matters at bf16 output precision)
+    // one pass over the fragments: per-row sums of (x - x0) and (x - x0)^2 with x0 the row's first element (the
+    // shifted-data form: no cancellation between E[x^2] and mean^2 when |mean| >> std), reduced together (lane
+    // groups by shuffles, the 8 waves through LDS in a fixed order); mean = x0 + E[d], var = E[d^2] - E[d]^2
     auto chunk_in = [&](int u) { return (int64_t)(wave + u * SK_WAVES) * KSTEP + fg * EPC < K; };
-    float part[MT], part2[MT];
+    float part[MT], part2[MT], x0[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
+      float v0[8];
+      unpack_bf16(bload(ra, (uint32_t)((i * 16 + fr) * p.lda * ES)), v0);  // rows past M: zero
+      x0[i] = v0[0];
       part[i] = 0.f;
       part2[i] = 0.f;
 #pragma unroll
       for (int u = 0; u < SKU; ++u) {
         if (chunk_in(u)) {
+          const int64_t kc = (int64_t)(wave + u * SK_WAVES) * KSTEP + fg * EPC;
           float v[8];
           unpack_bf16(af[u][i], v);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            part[i] += v[e];
-            part2[i] += v[e] * v[e];
+            const float d = kc + e < K ? v[e] - x0[i] : 0.f;
+            part[i] += d;
+            part2[i] += d * d;
           }
         }
       }
@@ -556,8 +561,9 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
         t += lnp[w][i * 16 + fr];
         t2 += lnp2[w][i * 16 + fr];
       }
-      ln_mean[i] = t / (float)K;
-      const float var = t2 / (float)K - ln_mean[i] * ln_mean[i];
+      const float dm = t / (float)K;
+      ln_mean[i] = x0[i] + dm;
+      const float var = t2 / (float)K - dm * dm;
       ln_rs[i] = 1.f / sqrtf((var > 0.f ? var : 0.f) + p.ln_eps);
     }
   } else if (fuse_ln) {

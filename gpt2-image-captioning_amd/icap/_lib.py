@@ -107,6 +107,7 @@ SIGNATURES = {
     "icap_attention_decode": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, i64, f32, vp]),
     "icap_attention_decode_anc": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, vp, i64, f32, vp]),
     "icap_beam_workspace_bytes": (C.c_size_t, [i32, i32, i32, i32]),
+    "icap_beam_layout": (C.c_int, [i32, i32, i32, i32, vp]),
     "icap_beam_init": (C.c_int, [C.POINTER(BeamArgs), i32, vp]),
     "icap_beam_rowtop": (C.c_int, [i32, i64, i64, vp, i64, i32, vp, vp, vp, vp, vp]),
     "icap_beam_update": (C.c_int, [C.POINTER(BeamArgs), i32, i32, vp]),

@@ -33,6 +33,9 @@ Tensor = torch.Tensor
 
 WEIGHTS_FILE = "dinov3_vitl16_dinotxt_vision_head_and_text_encoder-a442d8f5.pth"  # dino.py:11-12
 BACKBONE_WEIGHTS_FILE = "dinov3_vitl16_pretrain_lvd1689m-8aa4cbdd.pth"
+# what extract_dino_embeddings stores: the backbone's L2-normalised pooled CLS, NOT the dino.txt head's output
+# (the reference's encode_image); written as the .pt file's "feature" field so the two cannot be mixed silently
+FEATURE_NAME = "dinov3_vitl16_backbone_pooled_cls"
 RESIZE_DEFAULT_SIZE = 256  # dino.py:13-16
 CROP_DEFAULT_SIZE = 224
 IMAGENET_DEFAULT_MEAN = (0.485, 0.456, 0.406)
@@ -167,13 +170,17 @@ class DINOv3ImageTower(nn.Module):
         return m
 
     def load_backbone_state_dict(self, sd: Dict[str, Tensor]):
-        """An HF DINOv3ViTModel state dict (a 'dinov3.' / 'backbone.' prefix is dropped)."""
+        """An HF DINOv3ViTModel state dict, or Meta's native DINOv3 checkpoint layout (the file the reference's
+        torch.hub loader reads, BACKBONE_WEIGHTS_FILE), converted by meta_to_hf_state_dict. A 'dinov3.' /
+        'backbone.' prefix is dropped."""
         out = {}
         for k, v in sd.items():
             for pre in ("dinov3.", "backbone."):
                 if k.startswith(pre):
                     k = k[len(pre):]
             out[k] = v
+        if is_meta_layout(out):
+            out = meta_to_hf_state_dict(out, self.config)
         self._core = None
         return self.load_state_dict(out, strict=True)
 
@@ -202,6 +209,60 @@ class DINOv3ImageTower(nn.Module):
     def encode_image(self, pixel_values: Tensor, compute_dtype: torch.dtype = torch.bfloat16) -> Tensor:
         """dino.py:175 `encode_image` stand-in: the backbone's pooled CLS (un-normalised) [B, 1024]."""
         return self.core(compute_dtype).features(pixel_values, normalize=False)
+
+
+def is_meta_layout(sd: Dict[str, Tensor]) -> bool:
+    return any(k.startswith("blocks.") or k in ("storage_tokens", "patch_embed.proj.weight") for k in sd)
+
+
+def meta_to_hf_state_dict(sd: Dict[str, Tensor], c: Optional[DinoConfig] = None) -> Dict[str, Tensor]:
+    """Meta's DINOv3 ViT checkpoint keys -> HF DINOv3ViTModel keys (the layout DINOv3ImageTower holds).
+
+    cls_token / mask_token / storage_tokens -> embeddings.{cls_token, mask_token, register_tokens} (reshaped to
+    [1, n, D]); patch_embed.proj -> embeddings.patch_embeddings; blocks.N.attn.qkv [3D, D] (+ bias [3D]) split into
+    q / k / v, the key bias dropped (Meta zeroes it through attn.qkv.bias_mask; HF's k_proj has no bias);
+    attn.proj -> attention.o_proj; ls{1,2}.gamma -> layer_scale{1,2}.lambda1; mlp.fc1 / fc2 -> mlp.up_proj /
+    down_proj; norm -> norm. rope_embed.periods is a derived constant: it is checked against this tower's RoPE
+    frequencies (rope_tables) and dropped. Any other key is passed through, so a strict load names it."""
+    c = c or DinoConfig()
+    D = c.hidden_size
+    out: Dict[str, Tensor] = {}
+    for k, v in sd.items():
+        if k in ("cls_token", "mask_token", "storage_tokens"):
+            name = {"cls_token": "cls_token", "mask_token": "mask_token", "storage_tokens": "register_tokens"}[k]
+            out["embeddings." + name] = v.reshape(1, -1, D)
+        elif k.startswith("patch_embed.proj."):
+            out["embeddings.patch_embeddings." + k.split(".")[-1]] = v
+        elif k == "rope_embed.periods":
+            hd = D // c.num_attention_heads
+            inv = 1 / c.rope_theta ** torch.arange(0, 1, 4 / hd, dtype=torch.float64)
+            if v.numel() != inv.numel() or float((1.0 / v.double() - inv).abs().max()) > 1e-6 * float(inv.max()):
+                raise ValueError("rope_embed.periods does not match the RoPE frequencies of this configuration")
+        elif k.startswith("blocks."):
+            _, i, rest = k.split(".", 2)
+            p = f"model.layer.{i}."
+            if rest in ("attn.qkv.weight", "attn.qkv.bias"):
+                kind = rest.split(".")[-1]
+                q, kk, vv = v.chunk(3, 0)
+                out[p + f"attention.q_proj.{kind}"] = q
+                out[p + f"attention.v_proj.{kind}"] = vv
+                if kind == "weight":
+                    out[p + "attention.k_proj.weight"] = kk
+            elif rest == "attn.qkv.bias_mask":
+                continue
+            elif rest.startswith("attn.proj."):
+                out[p + "attention.o_proj." + rest.split(".")[-1]] = v
+            elif rest in ("ls1.gamma", "ls2.gamma"):
+                out[p + f"layer_scale{rest[2]}.lambda1"] = v
+            elif rest.startswith("mlp.fc1."):
+                out[p + "mlp.up_proj." + rest.split(".")[-1]] = v
+            elif rest.startswith("mlp.fc2."):
+                out[p + "mlp.down_proj." + rest.split(".")[-1]] = v
+            else:  # norm1 / norm2 keep their names
+                out[p + rest] = v
+        else:
+            out[k] = v
+    return out
 
 
 class DinoCore:
@@ -378,6 +439,11 @@ def load_dinov3_models(model_weights_dir: Optional[str] = None, repo_or_dir: str
                 raise FileNotFoundError(f"Could not find '{f}' in directory '{model_weights_dir}'")
         sd = torch.load(os.path.join(model_weights_dir, BACKBONE_WEIGHTS_FILE), map_location="cpu", weights_only=True)
         model.load_backbone_state_dict(sd)
+        import warnings
+
+        warnings.warn(f"icap.dino: '{WEIGHTS_FILE}' (the dino.txt vision head) is present but not applied: "
+                      f"embeddings are the backbone's pooled CLS ({FEATURE_NAME}), not the reference's "
+                      "encode_image output; extraction files record this in their 'feature' field", stacklevel=2)
     else:
         model = DINOv3ImageTower.random_init(DinoConfig())
     return model.to(device).eval(), None
@@ -392,5 +458,5 @@ def extract_dino_embeddings(image_dir: str, output_path: str, dino_model: DINOv3
     from .images import extract_directory
 
     n = extract_directory(image_dir, output_path, dino_model.embed, dino_processor, dino_model.config.embedding_dim,
-                          batch_size, num_workers, device or dino_model.device)
+                          batch_size, num_workers, device or dino_model.device, feature=FEATURE_NAME)
     print(f"Saving {n} embeddings to {output_path}...")

@@ -38,8 +38,15 @@ class CaptionTrainer:
         self.grad_accum_steps = grad_accum_steps
         self.pg = process_group
         self.world = 1
-        if process_group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
+        self.distributed = process_group is not None or (torch.distributed.is_available()
+                                                         and torch.distributed.is_initialized())
+        if self.distributed:
             self.world = torch.distributed.get_world_size(process_group)
+            # DDP's construction-time guarantee: every rank starts from rank 0's replica (trainable masters, frozen
+            # GPT-2 / image-tower weights), whatever each process's RNG produced when it built the model
+            broadcast_replicas([model] + ([clip_model] if clip_model is not None else []), process_group)
+        # the bucketed communication-stream step also at world size 1 (exercises the RCCL calls on one GPU)
+        self.force_overlap = os.environ.get("ICAP_DP_FORCE_OVERLAP", "0") == "1" and self.distributed
         self.dev = model.device
         flat = model.flat()
         self.flat = flat
@@ -343,7 +350,7 @@ class CaptionTrainer:
             zero = self._micro == 0
         if step is None:
             step = self._micro + 1 >= self.grad_accum_steps
-        if step and self.world > 1 and self.dp_overlap:
+        if step and (self.world > 1 or self.force_overlap) and self.dp_overlap:
             self._overlapped_step(zero, use_graph and self._eager_steps >= 1)
             self._eager_steps += 1
         elif use_graph and self._eager_steps >= 1:
@@ -412,6 +419,38 @@ class CaptionTrainer:
     @property
     def last_loss(self) -> Tensor:
         return self.gws.loss
+
+
+@torch.no_grad()
+def broadcast_replicas(modules, process_group=None) -> None:
+    """Broadcast every parameter and buffer of `modules` from the group's rank 0, in place, then drop the compute
+    copies derived from them (GPT-2 / mapper / image-tower cores, the mapper's bf16 flat copy) so they are rebuilt
+    from the broadcast values. The trainable nn.Parameters may be views of the flat fp32 master buffer; an in-place
+    broadcast into a view writes the master."""
+    dist = torch.distributed
+    src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
+    seen = set()
+    for m in modules:
+        for t in list(m.parameters()) + list(m.buffers()):
+            if id(t) in seen or t.numel() == 0:
+                continue
+            seen.add(id(t))
+            if t.is_contiguous():
+                dist.broadcast(t.data, src=src, group=process_group)
+            else:
+                tmp = t.data.contiguous()
+                dist.broadcast(tmp, src=src, group=process_group)
+                t.data.copy_(tmp)
+    for m in modules:
+        for sub in m.modules():
+            if hasattr(sub, "invalidate_core"):
+                sub.invalidate_core()
+            elif getattr(sub, "_core", None) is not None:
+                sub._core = None
+        f = getattr(m, "_flat", None)
+        if f is not None:
+            f.sync_compute_copy()
+            m._synced_version = f.flat._version
 
 
 def flat_ranges(flat, params) -> List[Tuple[int, int]]:

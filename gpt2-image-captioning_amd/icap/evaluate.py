@@ -38,31 +38,50 @@ def generate_predictions(model, dataset, batch_size: int = 128, max_length: int 
     return preds
 
 
+METRIC_KEYS = ("BLEU-1", "BLEU-2", "BLEU-3", "BLEU-4", "ROUGE-L", "CIDEr")  # EvalMetrics.to_dict, eval.py:39-48
+
+
+def load_coco_references(annotations_path: str) -> Dict[int, list]:
+    """src/eval.py:110-130: image_id -> its reference captions, in annotation order."""
+    with open(annotations_path) as f:
+        coco = json.load(f)
+    refs: Dict[int, list] = {}
+    for a in coco["annotations"]:
+        refs.setdefault(a["image_id"], []).append(a["caption"])
+    return refs
+
+
 def compute_caption_metrics(preds, annotations_path: str) -> Dict[str, float]:
+    """src/eval.py:59-108,133-157 — BLEU-1..4 / ROUGE-L / CIDEr over the images present in both predictions and
+    references (ValueError when none are), keyed as EvalMetrics.to_dict (eval.py:39-48). pycocoevalcap is not in
+    this image: without it the dict is empty (the metrics are host-side scoring, outside the device path)."""
     try:
         from pycocoevalcap.bleu.bleu import Bleu
         from pycocoevalcap.cider.cider import Cider
         from pycocoevalcap.rouge.rouge import Rouge
     except ImportError:
         return {}
-    with open(annotations_path) as f:
-        coco = json.load(f)
-    gts: Dict[int, list] = {}
-    for a in coco["annotations"]:
-        gts.setdefault(a["image_id"], []).append(a["caption"])
-    res = {p["image_id"]: [p["caption"]] for p in preds}
-    gts = {k: gts[k] for k in res}
-    bleu, _ = Bleu(4).compute_score(gts, res)
-    rouge, _ = Rouge().compute_score(gts, res)
-    cider, _ = Cider().compute_score(gts, res)
-    return {"bleu_1": bleu[0], "bleu_4": bleu[3], "rouge_l": rouge, "cider": cider}
+    res_all = {p["image_id"]: [p["caption"]] for p in preds}
+    refs_all = load_coco_references(annotations_path)
+    common = set(res_all) & set(refs_all)
+    if not common:
+        raise ValueError("No common image IDs found between predictions and references")
+    res = {k: res_all[k] for k in common}
+    refs = {k: refs_all[k] for k in common}
+    out: Dict[str, float] = {}
+    bleu, _ = Bleu(4).compute_score(refs, res)
+    for k, v in zip(METRIC_KEYS[:4], bleu):
+        out[k] = v
+    out["ROUGE-L"], _ = Rouge().compute_score(refs, res)
+    out["CIDEr"], _ = Cider().compute_score(refs, res)
+    return out
 
 
 def evaluate_epoch(model, dataset, annotations_path, epoch, split_name, batch_size, num_workers, max_length,
                    temperature, top_p, device, output_dir) -> Dict[str, Any]:
     """src/eval.py:311-386: predictions -> `epoch_{epoch}_{split}_predictions.json` ([{"image_id", "caption"}],
     indent 2) and `epoch_{epoch}_{split}_metrics.json` ({"epoch", "split", "num_images", **metrics}), the
-    reference's file names and layouts. Returns the metrics dict (+ num_predictions)."""
+    reference's file names and layouts. Returns the metrics dict (EvalMetrics.to_dict keys)."""
     model.eval()
     os.makedirs(output_dir, exist_ok=True)
     preds = generate_predictions(model, dataset, batch_size, max_length, temperature, top_p, device)
@@ -71,5 +90,11 @@ def evaluate_epoch(model, dataset, annotations_path, epoch, split_name, batch_si
         json.dump(preds, f, indent=2)
     with open(os.path.join(output_dir, f"epoch_{epoch}_{split_name}_metrics.json"), "w") as f:
         json.dump({"epoch": epoch, "split": split_name, "num_images": len(preds), **m}, f, indent=2)
-    m["num_predictions"] = len(preds)
     return m
+
+
+def save_eval_summary(all_metrics, output_path: str) -> None:
+    """src/eval.py:479-491: the per-epoch validation dicts ({"epoch", "loss", **metrics}) as one JSON list."""
+    with open(output_path, "w") as f:
+        json.dump(all_metrics, f, indent=2)
+    print(f"Evaluation summary saved to: {output_path}")

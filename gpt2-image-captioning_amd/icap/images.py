@@ -10,7 +10,7 @@ extension, exactly as the reference lists them, so the saved .pt rows line up wi
 from __future__ import annotations
 
 import os
-from typing import Callable, List, Tuple
+from typing import Optional, Callable, List, Tuple
 
 import numpy as np
 import torch
@@ -46,10 +46,11 @@ class ImageDirectoryDataset(Dataset):
 
 @torch.no_grad()
 def extract_directory(image_dir: str, output_path: str, embed: Callable, processor, out_dim: int,
-                      batch_size: int = 32, num_workers: int = 4, device=None) -> int:
+                      batch_size: int = 32, num_workers: int = 4, device=None, feature: Optional[str] = None) -> int:
     """Every image of `image_dir` -> {"filenames": [...], "embeddings": fp32 [N, out_dim]} saved with torch.save
     (src/embeddings/clip.py:147-149 format). `embed(pixel_values)` returns L2-normalised features on the device.
-    Returns the number of images."""
+    feature: an extra "feature" string naming what the embeddings are (readers that index "filenames" /
+    "embeddings", src/dataset.py:127-137, ignore it). Returns the number of images."""
     ds = ImageDirectoryDataset(image_dir)
     dl = DataLoader(ds, batch_size=batch_size, shuffle=False, num_workers=num_workers,
                     collate_fn=ImageDirectoryDataset.collate_fn, persistent_workers=False)
@@ -62,5 +63,8 @@ def extract_directory(image_dir: str, output_path: str, embed: Callable, process
         embs.append(embed(px).cpu())
         names.extend(batch_names)
     final = torch.cat(embs, 0) if embs else torch.empty((0, out_dim))
-    torch.save({"filenames": names, "embeddings": final}, output_path)
+    out = {"filenames": names, "embeddings": final}
+    if feature is not None:
+        out["feature"] = feature
+    torch.save(out, output_path)
     return len(names)

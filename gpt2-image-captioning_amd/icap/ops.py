@@ -73,9 +73,9 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None,
          tile_only: bool = False, g256: bool = False) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
-    workspace: fp32 split-K scratch for launches on a stream other than the package's main one (the per-device
-    default serves every GEMM ordered on one stream). The split count depends on the shape alone, so the result
-    is bitwise the same with any workspace; one too small for the shape's split raises.
+    workspace: fp32 split-K scratch; by default one buffer per (device, stream), so GEMMs issued on different
+    streams never share slabs (gemm_workspace). The split count depends on the shape alone, so the result is
+    bitwise the same with any workspace; one too small for the shape's split raises.
     trans_ab: A and B are K-outer ([K, M] / [K, N] row-major: out = epi(alpha * A^T @ B)), bf16 only.
     ln: (gamma, beta, eps) — A is LayerNorm-ed over its K columns inside the GEMM (M <= 128 launches).
     alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).
@@ -112,7 +112,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     if resid is not None:
         a.resid, a.ldr = resid.data_ptr(), _ld(resid)
     a.drop_p, a.seed, a.offset, a.seed_ptr = drop.p, drop.seed, drop.offset, drop.ptr
-    ws = gemm_workspace(A.device) if workspace is None else workspace
+    ws = gemm_workspace(A.device, torch.cuda.current_stream(A.device) if A.is_cuda else None) \
+        if workspace is None else workspace
     a.workspace, a.workspace_bytes, a.split_k = ws.data_ptr(), ws.numel() * 4, split_k
     a.m_dev = _p(m_dev)
     a.path = 1 if tile_only else (3 if g256 else 0)
@@ -135,10 +136,14 @@ GEMM_WORKSPACE_BYTES = 192 << 20  # split-K slabs up to splits*M*N fp32 (LM-head
 _gemm_ws = {}
 
 
-def gemm_workspace(device) -> Tensor:
-    """Per-device fp32 split-K scratch (GEMMs of this package are ordered on one stream per device, so one
-    buffer serves them all). Allocate it before any graph capture with gemm_workspace(device)."""
-    key = (device.type, device.index)
+def gemm_workspace(device, stream=None) -> Tensor:
+    """fp32 split-K scratch of one (device, stream): launches ordered on one stream reuse a buffer safely, and
+    launches on two streams get two buffers, so concurrent split-K GEMMs never overwrite each other's slabs
+    (a GEMM's slabs are written and reduced inside its own stream-ordered launches). A HIP graph captures the
+    buffer of its capture stream; graphs replayed one after another (the trainer's step / segment graphs) share it
+    like eager launches on one stream do."""
+    sid = 0 if stream is None else int(stream.cuda_stream)
+    key = (device.type, device.index, sid)
     ws = _gemm_ws.get(key)
     if ws is None:
         ws = torch.empty(GEMM_WORKSPACE_BYTES // 4, dtype=torch.float32, device=device)
@@ -230,6 +235,17 @@ def attention_decode(cache: Tensor, out: Tensor, *, B: int, H: int, hd: int, pos
 
 
 # ---------------------------------------------------------------------------------------------- beam search
+BEAM_LAYOUT_FIELDS = ("run_score", "run_seq", "fin_score", "fin_len", "fin_seq", "fin_cnt", "done", "anc", "total")
+
+
+def beam_layout(B: int, W: int, T: int, max_len: int) -> dict:
+    """The beam workspace's word offsets as beam.hip lays it out (icap_beam_layout)."""
+    offs = (C.c_int64 * 9)()
+    if L.load().icap_beam_layout(B, W, T, max_len, offs) != 0:  # host-only query (also in dry runs)
+        raise L.IcapError(f"icap_beam_layout failed: {L.last_error()}")
+    return dict(zip(BEAM_LAYOUT_FIELDS, list(offs)))
+
+
 class BeamState:
     """Device state of one beam search (include/icap.h icap_beam_*): B captions x W beams, token budget
     max_len, T = P + max_len cache positions. Owns the workspace and the per-row candidate buffers."""
@@ -256,12 +272,10 @@ class BeamState:
         a.top_val, a.top_idx = self.top_val.data_ptr(), self.top_idx.data_ptr()
         a.top_m, a.top_ls = self.top_m.data_ptr(), self.top_ls.data_ptr()
         a.ws = self.ws.data_ptr()
-        # word offsets of the ancestry table and the per-caption done flags (beam.hip layout())
-        up4 = lambda n: (n + 3) & ~3  # noqa: E731
-        o = up4(R) + up4(R * max_len) + up4(R) + up4(R) + up4(R * max_len) + up4(B)
-        self.done = self.ws[o: o + B]
-        o += up4(B)
-        self.anc = self.ws[o: o + T * R]
+        # word offsets of the per-caption done flags and the ancestry table, from the library (icap_beam_layout)
+        offs = beam_layout(B, W, T, max_len)
+        self.done = self.ws[offs["done"]: offs["done"] + B]
+        self.anc = self.ws[offs["anc"]: offs["anc"] + T * R]
 
     def set_embedding(self, dtype: torch.dtype, D: int, n_positions: int, wte: Tensor, wpe: Tensor,
                       x: Optional[Tensor]) -> None:

@@ -117,11 +117,15 @@ def train(train_dataset, model, batch_size: int, num_epochs: int, num_workers: i
                 torch.distributed.broadcast_object_list(box, src=0)
                 m = box[0]
             val_metrics_history.append({"epoch": epoch + 1, "loss": avg, **m})
-            cider = m.get("cider", -1.0)
+            cider = m.get("CIDEr", -1.0)
             if cider > best_val_cider:
                 best_val_cider, best_epoch = cider, epoch + 1
                 if is_main:
                     model.save_parameters(os.path.join(outputs_dir, f"best_model_epoch_{best_epoch}.pt"))
             model.train()
+    if is_main and val_metrics_history:  # src/train.py:229-235 (the metric-curve PNG is out of scope)
+        from .evaluate import save_eval_summary
+
+        save_eval_summary(val_metrics_history, os.path.join(eval_dir, "val_metrics_summary.json"))
     return {"epoch_losses": epoch_loss_values, "val_metrics": val_metrics_history, "best_val_cider": best_val_cider,
             "best_epoch": best_epoch}

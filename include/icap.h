@@ -344,6 +344,11 @@ typedef struct {
   const void* wte; const void* wpe; void* x;  /* x [R, D] may be NULL (no next step)             */
 } icap_beam_args;
 size_t icap_beam_workspace_bytes(int32_t B, int32_t W, int32_t T, int32_t max_len);
+/* The workspace carve-up in 4-byte words: word_offsets[0..8] = run_score, run_seq, fin_score,   */
+/* fin_len, fin_seq, fin_cnt, done (int32 per caption: 1 once its search is over), anc (int32   */
+/* [T, B*W] KV ancestry, the table icap_attention_decode_anc reads), total. Callers that look    */
+/* at `done` (early exit) or `anc` take the offsets from here, never from a restated layout.      */
+int icap_beam_layout(int32_t B, int32_t W, int32_t T, int32_t max_len, int64_t* word_offsets);
 /* running scores (0 for beam 0, -1e9 for the others, :3318-3320), no finished hypotheses, and   */
 /* the KV ancestry of the P prefix positions (every row its own).                               */
 int icap_beam_init(const icap_beam_args* a, int32_t P, void* stream);

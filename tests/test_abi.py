@@ -103,3 +103,16 @@ def test_gemm_kernel_name_query_without_gpu():
     f32 = lib.icap_gemm_kernel_name(C.byref(_gemm_args(8320, 768, 768, c_dtype=_lib.F32))).decode()
     assert "unsigned short, float" in f32
     assert lib.icap_gemm_kernel_name(C.byref(_gemm_args(8, 8, 3))) is None  # invalid K
+
+
+def test_beam_layout_exported_and_consistent():
+    """BeamState takes the done / anc word offsets from icap_beam_layout (the library's own carve-up),
+    not a Python restatement. The offsets are increasing, 16-byte aligned, and total matches the workspace size."""
+    from icap import ops
+
+    for B, W, T, L in [(1, 1, 1, 1), (3, 4, 67, 50), (128, 4, 65, 50), (7, 8, 129, 128)]:
+        o = ops.beam_layout(B, W, T, L)
+        vals = [o[k] for k in ops.BEAM_LAYOUT_FIELDS]
+        assert vals == sorted(vals) and all(v % 4 == 0 for v in vals), o
+        assert o["total"] * 4 == _lib.load().icap_beam_workspace_bytes(B, W, T, L)
+        assert o["anc"] + T * B * W <= o["total"] and o["done"] + B <= o["anc"]

@@ -36,12 +36,16 @@ def _noise(dev, n):
     s = torch.cuda.Stream(dev)
     a = torch.randn((4096, 4096), device=dev).to(torch.bfloat16)
     c = torch.empty((4096, 4096), device=dev, dtype=torch.bfloat16)
+    # a split-K shape with the DEFAULT workspace (one per stream since r03: the noise stream gets its own slabs)
+    sa = torch.randn((256, 8192), device=dev).to(torch.bfloat16)
+    sc = torch.empty((256, 512), device=dev, dtype=torch.bfloat16)
     torch.cuda.synchronize(dev)
 
     def launch():
         with torch.cuda.stream(s):
-            for _ in range(n):
-                ops.gemm(a, a, c, split_k=1)  # no split-K: never touches the default workspace
+            for i in range(n):
+                ops.gemm(a, a, c)
+                ops.gemm(sa, sa[:512], sc)
     return launch, s
 
 

@@ -178,6 +178,62 @@ def test_trainer_overlapped_bucket_allreduce_world2(mapper, freeze, bf16):
             assert v["max_err"] < 1e-2, v
 
 
+def _replica_broadcast(rank, world, arg):
+    """Ranks build their models from DIFFERENT RNG seeds; constructing the CaptionTrainer under the process group
+    must leave every parameter and buffer equal to rank 0's (DDP's construction-time broadcast), including the
+    trainable masters inside the flat buffer and the frozen GPT-2 weights, and a data-parallel step (stand-in
+    per-rank gradients, then the real all-reduce) keeps them equal."""
+    import icap.weights
+    from dryrun import dry_run
+    from icap import CaptionTrainer
+    from test_dryrun_bounds import batch, tiny_model
+
+    mapper, freeze = arg
+    torch.manual_seed(1000 + 17 * rank)
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model(mapper, freeze=freeze)
+
+        def digest():
+            return [float(t.detach().double().sum()) + float((t.detach().double() ** 2).sum())
+                    for t in list(model.parameters()) + list(model.buffers())]
+
+        before = digest()
+        t = CaptionTrainer(model, 3, 12, num_training_steps=3)
+        after = digest()
+        flat_sum = float(t.flat.flat.double().sum())
+        # two DP steps: the optimizer is a recorded C-ABI call, so stand in an update that depends only on the
+        # reduced gradient (identical on every rank iff the all-reduce and the replicas are)
+        t.dp_overlap = False
+        n = t.flat.flat_grad.numel()
+        orig_fb = t._fwd_bwd
+
+        def fwd_bwd(first, scale):
+            orig_fb(first, scale)
+            t.flat.flat_grad.copy_((torch.arange(n, dtype=torch.float32) % 7) * (rank + 1) * scale)
+
+        def optimizer():
+            t.flat.flat.sub_(1e-3 * t.flat.flat_grad)
+
+        t._fwd_bwd, t._optimizer = fwd_bwd, optimizer
+        for _ in range(2):
+            t.load_batch(*batch(3, 12))
+            t.micro_step()
+        stepped = digest()
+        bad = rec.check()
+    return {"before": before, "after": after, "flat": flat_sum, "stepped": stepped, "bad": bad[:5]}
+
+
+@pytest.mark.parametrize("mapper,freeze", [("transformer", True), ("transformer", False), ("mlp", True)])
+def test_trainer_broadcasts_replicas_world2(mapper, freeze):
+    out = _run("_replica_broadcast", (mapper, freeze))
+    assert out[0]["before"] != out[1]["before"]  # the ranks really built different models
+    assert out[0]["after"] == out[1]["after"]  # bitwise-equal replicas after construction
+    assert out[0]["flat"] == out[1]["flat"]
+    assert out[0]["stepped"] == out[1]["stepped"] and out[0]["stepped"] != out[0]["after"]
+    assert not out[0]["bad"] and not out[1]["bad"]
+
+
 # ---------------------------------------------------------------------------------------- 2. train() shards
 
 

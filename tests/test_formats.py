@@ -172,4 +172,35 @@ def test_evaluation_json_files_match_reference_layout(tmp_path):
     with open(tmp_path / "epoch_3_val_metrics.json") as f:
         meta = json.load(f)
     assert meta["epoch"] == 3 and meta["split"] == "val" and meta["num_images"] == 3
-    assert m["num_predictions"] == 3
+    assert m == {}  # pycocoevalcap absent: no metric keys (present: EvalMetrics.to_dict's six)
+
+
+def test_val_metrics_summary_written_by_train(tmp_path):
+    """src/train.py:229-235 -> src/eval.py:479-491: after training with a validation set, train() writes
+    eval_results/val_metrics_summary.json = the list of per-epoch {"epoch", "loss", **metrics} dicts (indent 2),
+    the same list it returns as "val_metrics"."""
+    import icap
+    import icap.weights
+    from dryrun import dry_run
+    from icap.dataset import SyntheticCaptionDataset
+    from test_dryrun_bounds import tiny_model
+
+    ds = SyntheticCaptionDataset(4, max_length=12, real=5, vocab_size=512, eos=511, embed_dim=64)
+    ann = tmp_path / "ann.json"
+    ann.write_text(json.dumps({"annotations": []}))
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model()
+        model.generate = lambda emb, **_: torch.full((emb.shape[0], 3), 7, dtype=torch.int64)
+        res = icap.train(ds, model, batch_size=2, num_epochs=2, num_workers=0, device=torch.device("cpu"),
+                         outputs_dir=str(tmp_path / "out"), save_every_epoch=5, use_graph=False,
+                         val_dataset=ds, val_annotations_path=str(ann))
+    path = tmp_path / "out" / "eval_results" / "val_metrics_summary.json"
+    with open(path) as f:
+        summary = json.load(f)
+    assert summary == res["val_metrics"]
+    assert [e["epoch"] for e in summary] == [1, 2]
+    assert all(set(e) >= {"epoch", "loss"} for e in summary)
+    assert path.read_text().startswith("[\n  {")  # json.dump(..., indent=2)
+    for e in (1, 2):
+        assert (tmp_path / "out" / "eval_results" / f"epoch_{e}_val_predictions.json").exists()

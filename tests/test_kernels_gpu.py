@@ -198,6 +198,33 @@ def test_gemm_fused_layernorm(dev, dtype, M, N):
     assert rel_err(out, ref) < tol
 
 
+@pytest.mark.parametrize("offset", [0.0, 300.0, 3000.0])
+def test_gemm_fused_layernorm_large_mean(dev, offset):
+    """the bf16 fused LN statistics (one pass over the MFMA fragments) on rows whose mean is far larger
+    than their spread. The shifted sums (x - x0) keep the variance exact where E[x^2] - mean^2 in fp32 would cancel;
+    fused and unfused LN-GEMM both stay within bf16 rounding of an fp64 LN-GEMM of the same bf16 inputs."""
+    M, N, K = 128, 2304, 768
+    x = (rnd((M, K), dev, scale=8.0, seed=66) + offset).to(torch.bfloat16)
+    g = rnd((K,), dev, seed=67) * 0.2 + 1
+    b = rnd((K,), dev, seed=68) * 0.1
+    W = rnd((N, K), dev, torch.bfloat16, 0.05, seed=69)
+    xd = x.double()
+    mu = xd.mean(1, keepdim=True)
+    var = ((xd - mu) ** 2).mean(1, keepdim=True)
+    yref = ((xd - mu) / torch.sqrt(var + 1e-5) * g.double() + b.double())
+    ref = yref @ W.double().t()
+    y = torch.empty((M, K), device=dev, dtype=torch.bfloat16)
+    ops.layernorm_fwd(x, g, b, 1e-5, y, None, None)
+    unf = torch.empty((M, N), device=dev, dtype=torch.float32)
+    ops.gemm(y, W, unf)
+    out = torch.empty((M, N), device=dev, dtype=torch.float32)
+    ops.gemm(x, W, out, ln=(g, b, 1e-5))
+    e_fused, e_unf = rel_err(out, ref), rel_err(unf, ref)
+    print(f"offset {offset}: fused {e_fused:.3g} unfused {e_unf:.3g}")
+    assert e_fused < 1.5e-2 and e_unf < 1.5e-2
+    assert e_fused < 2 * e_unf + 1e-3  # no worse than the two-pass LayerNorm kernel's bf16 rounding
+
+
 @pytest.mark.parametrize("patch", [32, 14])
 def test_im2col_patches(dev, patch):
     """Conv2d(stride=patch) patch rows (HF/models/clip/modeling_clip.py:148-154), incl. ViT-L/14's p = 14
