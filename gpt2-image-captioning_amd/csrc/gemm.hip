@@ -74,6 +74,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
                                                                   int nk_split, uint32_t drop_thresh, float inv_keep) {
   static_assert(!KOUT || (sizeof(TI) == 2 && 16 * WM * TM == 128 && 16 * WN * TN == 128),
                 "K-outer operands: bf16, 128 x 128 tiles");
+  // MX block-scaled fp8 (TI = fp8_t): a stage's 128-byte LDS row is one 128-deep K step of
+  // v_mfma_scale_f32_16x16x128_f8f6f4 (twice the bf16 flops per staged byte and per fragment byte read); the
+  // per-32 E8M0 scales of the wave's 4 fragment rows of A and of B come in one 16-byte load each per stage
+  constexpr bool MX = sizeof(TI) == 1;
+  static_assert(!MX || (!KOUT && TM == 4 && TN == 4 && WM == 2 && WN == 2), "MX fp8: 128 x 128 tiles of 4 waves");
   constexpr int NW = WM * WN;
   constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
   constexpr int STB = (BM + BN) * GROWB;    // bytes per stage
@@ -180,8 +185,37 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   const int64_t kbase = (int64_t)kt0 * BKE;
   const int fr = lane & 15, fg = lane >> 4;
 
-  auto read_frags = [&](const char* As, uint4 (&af)[2][TM], uint4 (&bfr)[2][TN]) {
+  // MX scales (mx_scale_off layout): this lane's 16 bytes per stage = the scales of rows i*16 + fr (i = 0..3) of the
+  // wave's 64-row group, blocks 0..3; the lane's own block is fg (byte 8 fg of each word after the shift below)
+  const int64_t rga = MX ? (M + 63) / 64 : 0, rgb = MX ? (N + 63) / 64 : 0;
+  const __amdgpu_buffer_rsrc_t rsa = make_rsrc(MX ? p.a_scale : nullptr, MX ? (uint64_t)(K / 32) * rga * 64 : 0);
+  const __amdgpu_buffer_rsrc_t rsb = make_rsrc(MX ? p.b_scale : nullptr, MX ? (uint64_t)(K / 32) * rgb * 64 : 0);
+  auto load_scales = [&](int st, uint4& sa, uint4& sb) {
+    if constexpr (MX) {
+      sa = bload(rsa, (uint32_t)((((int64_t)st * rga + (m0 >> 6) + wm) * 16 + fr) * 16));
+      sb = bload(rsb, (uint32_t)((((int64_t)st * rgb + (n0 >> 6) + wn) * 16 + fr) * 16));
+    }
+  };
+  uint4 sca_cur{}, scb_cur{}, sca_nxt{}, scb_nxt{};
+
+  // fragments of one stage: bf16 / f32 two 16-byte k-steps per row fragment; MX one 32-byte operand
+  constexpr int KS = MX ? 1 : 2;
+  typedef typename std::conditional<MX, i32x8_t, uint4>::type frag_t;
+  auto read_frags = [&](const char* As, frag_t (&af)[KS][TM], frag_t (&bfr)[KS][TN]) {
     const char* Bs = As + BM * GROWB;
+    if constexpr (MX) {  // lane (fr, fg): chunks 2 fg, 2 fg + 1 of its row = k 32 fg .. 32 fg + 31
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * 16 * TM + i * 16 + fr;
+        af[0][i] = ld_mx_frag(As + lds_off(row, 2 * fg), As + lds_off(row, 2 * fg + 1));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * 16 * TN + j * 16 + fr;
+        bfr[0][j] = ld_mx_frag(Bs + lds_off(row, 2 * fg), Bs + lds_off(row, 2 * fg + 1));
+      }
+      return;
+    }
     if constexpr (KOUT) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -192,9 +226,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       }
       return;
     }
+    if constexpr (!MX) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int ch = ks * 4 + fg;
+      const int ch = ks * 4 + fg;  // chunks fg and 4 + fg: two MFMA k-steps
 #pragma unroll
       for (int i = 0; i < TM; ++i)
         af[ks][i] = *reinterpret_cast<const uint4*>(As + lds_off(wm * 16 * TM + i * 16 + fr, ch));
@@ -202,42 +237,62 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       for (int j = 0; j < TN; ++j)
         bfr[ks][j] = *reinterpret_cast<const uint4*>(Bs + lds_off(wn * 16 * TN + j * 16 + fr, ch));
     }
+    }
   };
-  auto mfmas = [&](const uint4 (&af)[2][TM], const uint4 (&bfr)[2][TN]) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+  auto mfmas = [&](const frag_t (&af)[KS][TM], const frag_t (&bfr)[KS][TN]) {
+    if constexpr (MX) {
+      const uint32_t wa[4] = {sca_cur.x, sca_cur.y, sca_cur.z, sca_cur.w};
+      const uint32_t wb[4] = {scb_cur.x, scb_cur.y, scb_cur.z, scb_cur.w};
+      const int sh = 8 * fg;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[i][j], af[ks][i], bfr[ks][j]);  // lane = col, regs = 4 rows
+        for (int j = 0; j < TN; ++j) mfma_mx(acc[i][j], af[0][i], bfr[0][j], wa[i] >> sh, wb[j] >> sh);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) mfma_chunk<TI>(acc[i][j], af[ks][i], bfr[ks][j]);  // lane = col, regs = 4 rows
+    }
   };
 
   if (NST == 2) {
     load_stage(kbase, 0);
+    load_scales(kt0, sca_cur, scb_cur);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       // all fragment reads of this stage first: hipcc waits vmcnt(0) before any LDS read that follows an
       // LDS-DMA issue, so the next stage's DMA is issued only after the reads (and overlaps the MFMAs)
-      uint4 af[2][TM], bfr[2][TN];
+      frag_t af[KS][TM], bfr[KS][TN];
       read_frags(smem + cur * STB, af, bfr);
       // the other buffer was last read in iteration kt-1, which every wave finished before the barrier below
-      if (kt + 1 < nk) load_stage(kbase + (int64_t)(kt + 1) * BKE, cur ^ 1);
+      if (kt + 1 < nk) {
+        load_stage(kbase + (int64_t)(kt + 1) * BKE, cur ^ 1);
+        load_scales(kt0 + kt + 1, sca_nxt, scb_nxt);
+      }
       mfmas(af, bfr);
       // keep the MFMAs above the wait: they are register-only, so without this fence hipcc sinks them below the
       // vmcnt/barrier and the DMA is waited for right after it is issued (cdna_hip_programming.md §5.4 rule 18)
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage kt+1 has landed
       __syncthreads();                                      // ... and every other wave's
+      if constexpr (MX) {
+        sca_cur = sca_nxt;
+        scb_cur = scb_nxt;
+      }
     }
   } else {
     for (int kt = 0; kt < nk; ++kt) {
       if (kt > 0) __syncthreads();  // every wave has finished reading the previous stage
       load_stage(kbase + (int64_t)kt * BKE, 0);
+      load_scales(kt0 + kt, sca_cur, scb_cur);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      uint4 af[2][TM], bfr[2][TN];
+      frag_t af[KS][TM], bfr[KS][TN];
       read_frags(smem, af, bfr);
       mfmas(af, bfr);
     }
@@ -763,6 +818,8 @@ static bool g256_pick(const icap_gemm_args& p) {
   return (p.K >= 2048 && tiles * 4 >= cus * 3 && full) || (rounds >= 4 && tiles * 10 >= rounds * cus * 8);
 }
 
+static bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
+
 namespace {
 // What icap_gemm launches for one call (shared by the launcher and icap_gemm_kernel_name).
 struct GemmPlan {
@@ -778,21 +835,30 @@ struct GemmPlan {
 };
 }  // namespace
 
-static bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
-
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
   ICAP_REQUIRE(p.path == 0 || p.path == 1 || p.path == 3, "icap_gemm: path must be 0, 1 or 3");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
-  ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16, "icap_gemm: bad in_dtype");
+  ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16 || p.in_dtype == ICAP_FP8_MX,
+               "icap_gemm: bad in_dtype");
   ICAP_REQUIRE(p.c_dtype == ICAP_F32 || p.c_dtype == ICAP_BF16, "icap_gemm: bad c_dtype");
-  const int epc = p.in_dtype == ICAP_BF16 ? 8 : 4;
+  const bool mx = p.in_dtype == ICAP_FP8_MX;
+  if (mx) {
+    ICAP_REQUIRE(p.K % 128 == 0 && p.lda % 16 == 0 && p.ldb % 16 == 0,
+                 "icap_gemm: FP8_MX needs K % 128 == 0 and lda, ldb multiples of 16");
+    ICAP_REQUIRE(p.a_scale && p.b_scale && al16(p.a_scale) && al16(p.b_scale),
+                 "icap_gemm: FP8_MX needs 16-byte aligned a_scale / b_scale");
+    ICAP_REQUIRE(!p.trans_ab && !p.ln_gamma && p.path != 3, "icap_gemm: FP8_MX takes no trans_ab / ln / path 3");
+    ICAP_REQUIRE((p.K / 32) * ((p.M + 63) / 64) * 64 < 0x7fffffffll && (p.K / 32) * ((p.N + 63) / 64) * 64 < 0x7fffffffll,
+                 "icap_gemm: FP8_MX scale arrays must stay below 2 GiB");
+  }
+  const int epc = p.in_dtype == ICAP_BF16 ? 8 : mx ? 16 : 4;
   ICAP_REQUIRE(p.trans_ab || p.K % epc == 0, "icap_gemm: K must be a multiple of 8 (bf16) / 4 (f32)");
   ICAP_REQUIRE(p.lda % epc == 0 && p.ldb % epc == 0, "icap_gemm: lda/ldb must be multiples of 8 (bf16) / 4 (f32)");
   ICAP_REQUIRE((p.trans_ab || (p.lda >= p.K && p.ldb >= p.K)) && p.ldc >= p.N, "icap_gemm: leading dimension too small");
   ICAP_REQUIRE((reinterpret_cast<uintptr_t>(p.A) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.B) & 15) == 0,
                "icap_gemm: A and B must be 16-byte aligned");
-  const int es = p.in_dtype == ICAP_BF16 ? 2 : 4;
+  const int es = p.in_dtype == ICAP_BF16 ? 2 : mx ? 1 : 4;
   ICAP_REQUIRE((int64_t)256 * p.lda * es < 0x7fffffffll && (int64_t)256 * p.ldb * es < 0x7fffffffll,
                "icap_gemm: a 256-row operand panel must stay below 2 GiB");
   ICAP_REQUIRE(p.beta == 0.f || p.c_dtype == ICAP_F32, "icap_gemm: beta != 0 requires f32 C");
@@ -817,7 +883,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   const bool fuse_ln = p.ln_gamma != nullptr;
   ICAP_REQUIRE(!fuse_ln || (p.ln_beta && p.M <= 128 && p.split_k == 0 && !p.trans_ab && p.K <= 4096),
                "icap_gemm: ln_gamma needs ln_beta, M <= 128, K <= 4096, no split_k / trans_ab");
-  if (p.M <= 128 && p.split_k == 0 && (tiles <= 128 || fuse_ln) && !p.trans_ab) {
+  if (p.M <= 128 && p.split_k == 0 && (tiles <= 128 || fuse_ln) && !p.trans_ab && !mx) {
     pl.skinny = true;
     // the fewest 16-column slabs per block that keep the grid within one pass over the CUs (every CU streams one
     // block's A rows + W slab; a second block on a CU doubles its bytes), then enough k-steps in flight per wave
@@ -875,6 +941,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   pl.splits = (int)splits;
   pl.nk_split = (int)nk_split;
   pl.variant = gemm_variant(p, nk_split);
+  if (mx && pl.variant == 5) pl.variant = 4;  // MX at 4 blocks / CU (128 VGPRs) spills: 3 blocks / CU
   if (narrow) {
     tiles_n = (p.N + 63) / 64;
     tiles = tiles_m * tiles_n;
@@ -905,7 +972,7 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
   if (a == nullptr) return nullptr;
   GemmPlan pl;
   if (gemm_plan(*a, pl) != ICAP_OK) return nullptr;
-  const char* ti = a->in_dtype == ICAP_BF16 ? "unsigned short" : "float";
+  const char* ti = a->in_dtype == ICAP_BF16 ? "unsigned short" : a->in_dtype == ICAP_FP8_MX ? "icap::fp8_t" : "float";
   const char* tc = a->c_dtype == ICAP_BF16 ? "unsigned short" : "float";
   char fmt[96];
   if (pl.g256) {
@@ -994,6 +1061,14 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     }
   } else if (p.in_dtype == ICAP_BF16) {
     if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(bf16_t, bf16_t) } else { ICAP_GEMM_LAUNCH(bf16_t, float) }
+  } else if (p.in_dtype == ICAP_FP8_MX) {  // variants 0 / 4 only (gemm_plan)
+    if (p.c_dtype == ICAP_BF16) {
+      if (pl.variant == 0) hipLaunchKernelGGL((gemm_kernel<fp8_t, bf16_t, 2, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm_kernel<fp8_t, bf16_t, 1, 3, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    } else {
+      if (pl.variant == 0) hipLaunchKernelGGL((gemm_kernel<fp8_t, float, 2, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      else hipLaunchKernelGGL((gemm_kernel<fp8_t, float, 1, 3, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+    }
   } else {
     if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(float, bf16_t) } else { ICAP_GEMM_LAUNCH(float, float) }
   }

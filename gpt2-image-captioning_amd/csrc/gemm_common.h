@@ -12,6 +12,38 @@ namespace icap {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+
+// OCP e4m3fn storage element of the MX block-scaled path (ICAP_FP8_MX): one byte, per-32-element E8M0 scales kept
+// beside the data (icap_gemm_args.a_scale / b_scale)
+struct fp8_t {
+  uint8_t v;
+};
+
+// One block-scaled MFMA 16x16x128 (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3 A and B): lane l supplies row (l & 15),
+// k = 32 (l >> 4) .. +31 as two 16-byte chunks (lo: k 32g..32g+15, hi: 32g+16..), and the E8M0 scale of that row's
+// 32-element block in byte 0 of sa / sb (tools/microbench/mx_probe.hip pins the map).
+__device__ __forceinline__ void mfma_mx(f32x4_t& acc, const i32x8_t& a, const i32x8_t& b, uint32_t sa, uint32_t sb) {
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, (int)sa, 0, (int)sb);
+}
+// the 32-byte MX operand of one lane from two 16-byte LDS chunks (written straight into the tuple's halves so the
+// 8 registers are allocated adjacent: no copies before the MFMA)
+__device__ __forceinline__ i32x8_t ld_mx_frag(const char* lo, const char* hi) {
+  typedef int i32x4_t __attribute__((ext_vector_type(4)));
+  i32x8_t v;
+  v.lo = *reinterpret_cast<const i32x4_t*>(lo);
+  v.hi = *reinterpret_cast<const i32x4_t*>(hi);
+  return v;
+}
+
+// MX scale layout of an operand with R rows and K columns (K % 128 == 0): for 128-element K stage s and 64-row group
+// g = row / 64, 256 bytes at ((s * ceil(R / 64) + g) * 16 + row % 16) * 16: 16 bytes per row % 16, holding for
+// q = (row / 16) % 4 the 4 scale bytes of the stage's 32-element blocks (byte q * 4 + kb). One 16-byte load gives
+// a lane the scales of the 4 rows i * 16 + r16 (i = 0..3) of a 64-row wave tile.
+__host__ __device__ __forceinline__ int64_t mx_scale_off(int64_t R, int64_t row, int64_t kblock) {
+  const int64_t rg = (R + 63) / 64, s = kblock >> 2;
+  return ((s * rg + (row >> 6)) * 16 + (row & 15)) * 16 + ((row >> 4) & 3) * 4 + (kblock & 3);
+}
 
 constexpr int GBM = 128, GBN = 128, GROWB = 128, GNT = 256;  // default 128x128 tile, 128-byte LDS rows
 constexpr uint32_t OOB = 0x80000000u;              // buffer offset beyond any num_records -> loads 0

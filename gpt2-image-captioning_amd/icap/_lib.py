@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must be imported first: the .so binds to torch's HI
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libicap_hip.so")
 
-F32, BF16 = 0, 1
+F32, BF16, FP8_MX = 0, 1, 2
 ACT_NONE, ACT_GELU_NEW, ACT_RELU, ACT_QUICK_GELU, ACT_TANH, ACT_GELU_ERF = 0, 1, 2, 3, 4, 5
 
 vp = C.c_void_p
@@ -45,6 +45,7 @@ class GemmArgs(C.Structure):
         ("trans_ab", i32),
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
         ("path", i32),
+        ("a_scale", vp), ("b_scale", vp),
     ]
 
 
@@ -98,6 +99,8 @@ SIGNATURES = {
     "icap_device_arch_ok": (C.c_int, []),
     "icap_gemm": (C.c_int, [C.POINTER(GemmArgs), vp]),
     "icap_gemm_kernel_name": (C.c_char_p, [C.POINTER(GemmArgs)]),
+    "icap_mx_scale_bytes": (sz, [i64, i64]),
+    "icap_quantize_mx": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, vp, vp, vp]),
     "icap_layernorm_fwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, f32, vp, i64, vp, vp, vp, vp]),
     "icap_layernorm_bwd_workspace_bytes": (sz, [i64, i64]),
     "icap_layernorm_bwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, vp,

@@ -65,6 +65,66 @@ class Dropout:
 NO_DROP = Dropout()
 
 
+class MXTensor:
+    """An ICAP_FP8_MX GEMM operand: e4m3 bytes q [R, K] (uint8, row stride % 16 == 0) + E8M0 block scales in the
+    layout icap_quantize_mx writes (include/icap.h icap_gemm_args.a_scale). Row views (rows r0:r1 with r0 % 64 == 0)
+    are not supported: an operand is always the whole quantised matrix."""
+
+    __slots__ = ("q", "scale", "R", "K")
+
+    def __init__(self, q: Tensor, scale: Tensor, R: int, K: int):
+        if q.dtype != torch.uint8 or scale.dtype != torch.uint8:
+            raise L.IcapError("MXTensor: q and scale must be uint8")
+        self.q, self.scale, self.R, self.K = q, scale, R, K
+
+    @staticmethod
+    def empty(R: int, K: int, device) -> "MXTensor":
+        nb = mx_scale_bytes(R, K)
+        return MXTensor(torch.empty((R, K), dtype=torch.uint8, device=device),
+                        torch.empty(nb, dtype=torch.uint8, device=device), R, K)
+
+    @property
+    def shape(self):
+        return (self.R, self.K)
+
+    @property
+    def device(self):
+        return self.q.device
+
+    @property
+    def dtype(self):
+        return "fp8_mx"
+
+    @property
+    def is_cuda(self):
+        return self.q.is_cuda
+
+    def data_ptr(self):
+        return self.q.data_ptr()
+
+
+def mx_scale_bytes(R: int, K: int) -> int:
+    n = int(L.load().icap_mx_scale_bytes(R, K))
+    if n == 0 and R * K:
+        raise L.IcapError(f"mx_scale_bytes: K = {K} must be a multiple of 128")
+    return n
+
+
+def quantize_mx(x: Tensor, out: Optional[MXTensor] = None, rows: Optional[int] = None,
+                rows_dev: Optional[Tensor] = None) -> MXTensor:
+    """x [R, K] (f32 / bf16) -> MX e4m3 + E8M0 per-32 scales (icap_quantize_mx). rows_dev: device int32 row count
+    (rows past it are not read)."""
+    R = x.shape[0] if rows is None else rows
+    K = x.shape[1]
+    if out is None:
+        out = MXTensor.empty(R, K, x.device)
+    if out.R != R or out.K != K:
+        raise L.IcapError("quantize_mx: output shape mismatch")
+    call("icap_quantize_mx", dtype_code(x.dtype), R, K, x.data_ptr(), _ld(x), out.q.data_ptr(), _ld(out.q),
+         out.scale.data_ptr(), _p(rows_dev), _stream())
+    return out
+
+
 def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, act: int = L.ACT_NONE,
          aux: Optional[Tensor] = None, dact: int = L.ACT_NONE, dact_src: Optional[Tensor] = None,
          resid: Optional[Tensor] = None, alpha: float = 1.0, beta: float = 0.0, drop: Dropout = NO_DROP,
@@ -83,6 +143,9 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     m_dev: device int32 row count <= M (rows past it are neither computed nor stored).
     tile_only: the 128-row tile kernels only; g256: the 256 x 256 kernel wherever eligible (A/B measurements,
     path-equality tests)."""
+    mx = isinstance(A, MXTensor)
+    if mx != isinstance(B, MXTensor):
+        raise L.IcapError("gemm: A and B must both be MXTensor (fp8 MX) or both plain tensors")
     if trans_ab:
         M = A.shape[1] if M is None else M
         K = A.shape[0] if K is None else K
@@ -94,12 +157,20 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     a = GemmArgs()
     a.trans_ab = 1 if trans_ab else 0
     a.M, a.N, a.K = M, N, K
-    a.in_dtype = dtype_code(A.dtype)
     a.c_dtype = dtype_code(out.dtype)
-    if B.dtype != A.dtype:
-        raise L.IcapError("gemm: A and B must share a dtype")
-    a.A, a.lda = A.data_ptr(), _ld(A)
-    a.B, a.ldb = B.data_ptr(), _ld(B)
+    if mx:
+        if M != A.R or N != B.R or K != A.K or K != B.K:
+            raise L.IcapError("gemm: MX operands are whole matrices (M, N, K must equal their shapes)")
+        a.in_dtype = L.FP8_MX
+        a.A, a.lda = A.q.data_ptr(), _ld(A.q)
+        a.B, a.ldb = B.q.data_ptr(), _ld(B.q)
+        a.a_scale, a.b_scale = A.scale.data_ptr(), B.scale.data_ptr()
+    else:
+        a.in_dtype = dtype_code(A.dtype)
+        if B.dtype != A.dtype:
+            raise L.IcapError("gemm: A and B must share a dtype")
+        a.A, a.lda = A.data_ptr(), _ld(A)
+        a.B, a.ldb = B.data_ptr(), _ld(B)
     a.C, a.ldc = out.data_ptr(), _ld(out)
     a.alpha, a.beta = alpha, beta
     a.bias = _p(bias)

@@ -36,7 +36,9 @@
 extern "C" {
 #endif
 
-enum { ICAP_F32 = 0, ICAP_BF16 = 1 };
+/* ICAP_FP8_MX: GEMM operands only (icap_gemm in_dtype): OCP e4m3fn bytes with one E8M0 scale per 32-element */
+/* K block (OCP MX), the scales in the layout icap_quantize_mx writes (icap_gemm_args.a_scale / b_scale).      */
+enum { ICAP_F32 = 0, ICAP_BF16 = 1, ICAP_FP8_MX = 2 };
 enum {
   ICAP_ACT_NONE = 0,
   ICAP_ACT_GELU_NEW = 1,   /* HF/activations.py:59-66 (GPT-2 gelu_new)        */
@@ -110,7 +112,23 @@ typedef struct {
   /*     m_dev / split-K, M and N >= 256) —                                                                      */
   /* for A/B measurements and for tests that compare the two paths (identical MFMA chains: bitwise equal).     */
   int32_t path;
+  /* in_dtype == ICAP_FP8_MX: the E8M0 block scales of A (M rows) and B (N rows), K % 128 == 0, lda / ldb      */
+  /* multiples of 16, 16-byte aligned. For a 128-element K stage s and 64-row group g, 256 bytes at offset      */
+  /* (s * ceil(R/64) + g) * 256: row r's 4 block scales at ((r % 16) * 16 + ((r / 16) % 4) * 4) (R = M or N),   */
+  /* i.e. K/32 * ceil(R/64) * 64 bytes. The product is sum_k a[m,k] 2^(sa-127) b[n,k] 2^(sb-127) in fp32       */
+  /* (v_mfma_scale_f32_16x16x128_f8f6f4), then the same epilogue as bf16 / f32 inputs.                       */
+  const uint8_t* a_scale; const uint8_t* b_scale;
 } icap_gemm_args;
+/* MX block quantisation (the A / B operands of an ICAP_FP8_MX GEMM): x [R, K] (f32 or bf16, row stride ldx) */
+/* -> q [R, K] OCP e4m3fn bytes (row stride ldq % 16 == 0) + the E8M0 scales in icap_gemm_args.a_scale      */
+/* layout (icap_mx_scale_bytes(R, K) bytes). Per 32-element block: X = min integer with amax <= 448 * 2^X    */
+/* (no element saturates), code X + 127; element = RNE_e4m3(v * 2^-X). K % 128 == 0; 16-byte aligned rows.  */
+/* No reference counterpart: the reference computes in fp32 (BASELINE configs[4] asks for the fp8 path);     */
+/* GPT-2 large's frozen weights are quantised once, activations before each fp8 product.                    */
+size_t icap_mx_scale_bytes(int64_t R, int64_t K);
+/* rows_dev: optional device int32 row count (<= R): rows past it are not read (the compacted LM-head rows). */
+int icap_quantize_mx(int32_t dtype, int64_t R, int64_t K, const void* x, int64_t ldx, void* q, int64_t ldq,
+                     void* scales, const int32_t* rows_dev, void* stream);
 /* name of the kernel instantiation icap_gemm launches for these arguments    */
 /* (as rocprofv3 prints it, minus the parameter list); NULL on invalid args.   */
 const char* icap_gemm_kernel_name(const icap_gemm_args* a);

@@ -813,3 +813,89 @@ def train_steps(gpt_sd, gcfg: GPT2Cfg, map_sd, mcfg: MapperCfg, batches, lr0: fl
             norms.append(clip_and_adamw(params, grads, st, lr0, warmup, total_steps))
         losses.append(float(loss.detach()))
     return losses, norms, {k: v.detach() for k, v in map_sd.items()}, {k: v.detach() for k, v in gpt_sd.items()}
+
+
+# ------------------------------------------------------------------------------------------------ MX fp8 (configs[4])
+# BASELINE configs[4] asks for an fp8 MFMA path; the reference itself computes in fp32, so the fp8 products have no
+# reference counterpart and their contract is restated here from the OCP Microscaling (MX) format: blocks of 32
+# elements along K share one E8M0 power-of-two scale, elements are OCP e4m3fn (max finite 448). The device's
+# quantiser (csrc/quant.hip) is checked against mx_quantize bit for bit; the end-to-end fp8 model is checked
+# against the reference goldens (tests/golden/large*.npz) within stated tolerances.
+
+E4M3_MAX = 448.0
+
+
+def e4m3_decode(codes: np.ndarray) -> np.ndarray:
+    """OCP e4m3fn byte -> float64 (bias 7, subnormals 2^-6 * m/8, 0x7f / 0xff NaN)."""
+    c = np.asarray(codes).astype(np.int64)
+    s = np.where(c & 0x80, -1.0, 1.0)
+    e = (c >> 3) & 15
+    m = c & 7
+    v = np.where(e == 0, m / 8.0 * 2.0 ** -6, (1.0 + m / 8.0) * 2.0 ** (e - 7.0))
+    v = np.where((e == 15) & (m == 7), np.nan, v)
+    return s * v
+
+
+def e4m3_round(x: np.ndarray) -> np.ndarray:
+    """Round-to-nearest-even onto the e4m3fn grid (|x| <= 448 assumed): step 2^(e-3) in binade e >= -6, 2^-9 below."""
+    x = np.asarray(x, dtype=np.float64)
+    a = np.abs(x)
+    e = np.floor(np.log2(np.maximum(a, 2.0 ** -6)))
+    step = 2.0 ** (e - 3)
+    return np.sign(x) * np.round(a / step) * step  # numpy rounds halves to even
+
+
+_E4M3_VALUES = e4m3_decode(np.arange(256))
+
+
+def e4m3_encode(v: np.ndarray) -> np.ndarray:
+    """Values already on the e4m3 grid -> their byte codes (+0 -> 0x00, -0 -> 0x80)."""
+    v = np.asarray(v, dtype=np.float64)
+    pos = np.arange(128)
+    table = {float(_E4M3_VALUES[i]): i for i in pos if not np.isnan(_E4M3_VALUES[i])}
+    a = np.abs(v)
+    codes = np.vectorize(lambda t: table[float(t)])(a).astype(np.uint8)
+    return np.where(np.signbit(v), codes | 0x80, codes).astype(np.uint8)
+
+
+def mx_exponent(amax: np.ndarray) -> np.ndarray:
+    """Smallest X with amax <= 448 * 2^X (so no element saturates), clamped to [-127, 127]; amax == 0 -> 0."""
+    amax = np.asarray(amax, dtype=np.float64)
+    safe = np.where(amax > 0, amax, 1.0)
+    x = np.ceil(np.log2(safe / E4M3_MAX))
+    # guard the log2 rounding at exact powers of two: enforce the defining inequality exactly
+    x = np.where(E4M3_MAX * 2.0 ** (x - 1) >= safe, x - 1, x)
+    x = np.where(E4M3_MAX * 2.0 ** x < safe, x + 1, x)
+    x = np.where(amax > 0, x, 0.0)
+    return np.clip(x, -127, 127).astype(np.int64)
+
+
+def mx_quantize(x: np.ndarray):
+    """x [R, K] (K % 32 == 0; fp32 values) -> (e4m3 codes uint8 [R, K], E8M0 codes uint8 [R, K/32]):
+    X per block (mx_exponent), element = RNE_e4m3(v * 2^-X) (the scaling is exact), code X + 127."""
+    x = np.asarray(x, dtype=np.float32).astype(np.float64)
+    R, K = x.shape
+    blk = x.reshape(R, K // 32, 32)
+    X = mx_exponent(np.abs(blk).max(-1))
+    q = e4m3_round(blk * 2.0 ** (-X[..., None]))
+    return e4m3_encode(q).reshape(R, K), (X + 127).astype(np.uint8)
+
+
+def mx_dequantize(codes: np.ndarray, scales: np.ndarray) -> np.ndarray:
+    R, K = codes.shape
+    v = e4m3_decode(codes).reshape(R, K // 32, 32) * 2.0 ** (scales.astype(np.float64)[..., None] - 127)
+    return v.reshape(R, K)
+
+
+def mx_scale_layout(scales: np.ndarray) -> np.ndarray:
+    """E8M0 codes [R, K/32] -> the byte array the device GEMM reads (include/icap.h icap_gemm_args.a_scale): for
+    128-element stage s and 64-row group g, 256 bytes at (s * ceil(R/64) + g) * 256, row r's 4 codes at
+    (r % 16) * 16 + ((r / 16) % 4) * 4. Rows past R (up to the next multiple of 64) hold 127."""
+    R, nkb = scales.shape
+    rg = (R + 63) // 64
+    out = np.full(nkb * rg * 64, 127, dtype=np.uint8)
+    for r in range(R):
+        for kb in range(nkb):
+            s = kb // 4
+            out[((s * rg + r // 64) * 16 + r % 16) * 16 + ((r // 16) % 4) * 4 + kb % 4] = scales[r, kb]
+    return out

@@ -15,7 +15,7 @@ import torch
 
 from icap import _lib, ops
 
-ES = {0: 4, 1: 2}
+ES = {0: 4, 1: 2, 2: 1}
 
 
 def _extent(ptr, nbytes):
@@ -43,6 +43,8 @@ def accesses(name, args):
                 ("resid", g.resid, _rows(g.M, g.ldr, g.N, ec)), ("seed_ptr", g.seed_ptr, 8),
                 ("workspace", g.workspace, g.workspace_bytes), ("m_dev", g.m_dev, 4),
                 ("ln_gamma", g.ln_gamma, g.K * 4), ("ln_beta", g.ln_beta, g.K * 4)]
+        if g.in_dtype == 2:  # MX block scales (include/icap.h a_scale / b_scale layout)
+            out += [("a_scale", g.a_scale, ops.mx_scale_bytes(g.M, g.K)), ("b_scale", g.b_scale, ops.mx_scale_bytes(g.N, g.K))]
     elif name in ("icap_attention_fwd", "icap_attention_bwd"):
         t = a[0]._obj
         es = ES[t.dtype]
@@ -115,6 +117,10 @@ def accesses(name, args):
     elif name == "icap_broadcast_rows":
         dt, B, R, D, src, dst, bs, _s = a
         out += [("src", src, R * D * 4), ("dst", dst, ((B - 1) * bs + R * D) * ES[dt])]
+    elif name == "icap_quantize_mx":
+        dt, R, K, x, ldx, q, ldq, sc, rdev, _s = a
+        out += [("x", x, _rows(R, ldx, K, ES[dt])), ("q", q, _rows(R, ldq, K, 1)), ("scales", sc, ops.mx_scale_bytes(R, K)),
+                ("rows_dev", rdev, 4)]
     elif name == "icap_counter_increment":
         out.append(("counter", a[0], 8))
     elif name == "icap_im2col_patches":

@@ -32,6 +32,10 @@ def _snapshot(t):
     return [(n, x.detach().clone()) for n, x in snap if x is not None]
 
 
+def _bits(x):
+    return x.view({2: torch.int16, 4: torch.int32, 8: torch.int64}[x.element_size()])
+
+
 def _noise(dev, n):
     s = torch.cuda.Stream(dev)
     a = torch.randn((4096, 4096), device=dev).to(torch.bfloat16)

@@ -1,0 +1,102 @@
+"""MX fp8 GEMM path on the device (BASELINE configs[4]).
+
+1. icap_quantize_mx == oracle.mx_quantize bit for bit (element codes as values, scale bytes in the GEMM's layout,
+   padded row groups at scale 1.0), bf16 and f32 inputs, zero blocks, wide dynamic range.
+2. icap_gemm with ICAP_FP8_MX operands == fp64 product of the DEQUANTISED operands (the only rounding left is the
+   fp32 accumulation): per-element error <= 1e-5 of sum |a||b|.
+3. The epilogues (bias + gelu_new + aux, residual + dropout, backward dact, beta) and split-K, m_dev behave as on
+   bf16 inputs: the fp8 launch equals the bf16 launch run on the dequantised operands (rounded to bf16, which is
+   exact for e4m3 values times power-of-two scales in bf16 range) within fp32 accumulation-order noise."""
+
+import numpy as np
+import pytest
+import torch
+
+from icap import _lib as L
+from icap import ops
+from oracle import icap_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def rnd(shape, dev, dtype=torch.float32, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(device=dev, dtype=dtype)
+
+
+def _wide(R, K, dev, dtype, seed):
+    """Rows whose 32-blocks span ~2^-10 .. 2^10 in magnitude (one scale per block matters)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    mag = torch.exp2(torch.randint(-10, 11, (R, K // 32, 1), generator=g).float()).repeat(1, 1, 32).reshape(R, K)
+    return (torch.randn((R, K), generator=g) * mag).to(device=dev, dtype=dtype)
+
+
+def _dequant(mx: ops.MXTensor) -> torch.Tensor:
+    codes = mx.q.cpu().numpy()
+    lay = mx.scale.cpu().numpy()
+    R, K = mx.R, mx.K
+    rg = (R + 63) // 64
+    s = np.empty((R, K // 32), dtype=np.uint8)
+    for kb in range(K // 32):
+        st = kb // 4
+        r = np.arange(R)
+        s[:, kb] = lay[((st * rg + r // 64) * 16 + r % 16) * 16 + ((r // 16) % 4) * 4 + kb % 4]
+    return torch.from_numpy(O.mx_dequantize(codes, s))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("R,K", [(1, 128), (70, 256), (200, 1280), (64, 5120)])
+def test_quantize_mx_matches_oracle(dev, dtype, R, K):
+    x = _wide(R, K, dev, dtype, seed=R + K)
+    x[0, :32] = 0  # an all-zero block
+    mx = ops.quantize_mx(x)
+    torch.cuda.synchronize()
+    codes, sc = O.mx_quantize(x.float().cpu().numpy())
+    assert np.array_equal(O.e4m3_decode(mx.q.cpu().numpy()), O.e4m3_decode(codes))
+    assert np.array_equal(mx.scale.cpu().numpy(), O.mx_scale_layout(sc))
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (200, 384, 1280), (8320 // 4, 1280, 5120), (96, 50304 // 8, 640)])
+def test_gemm_mx_equals_dequantized_product(dev, M, N, K):
+    A = ops.quantize_mx(_wide(M, K, dev, torch.bfloat16, seed=1))
+    B = ops.quantize_mx(rnd((N, K), dev, torch.bfloat16, 0.05, seed=2))
+    C = torch.empty((M, N), device=dev, dtype=torch.float32)
+    ops.gemm(A, B, C)
+    a, b = _dequant(A), _dequant(B)
+    ref = a @ b.t()
+    scale = a.abs() @ b.abs().t()
+    err = ((C.cpu().double() - ref).abs() / (scale + 1e-30)).max().item()
+    assert err < 1e-5, err
+
+
+def test_gemm_mx_epilogues_split_k_and_m_dev(dev):
+    M, N, K = 256, 768, 1280
+    A32 = rnd((M, K), dev, torch.bfloat16, 0.5, seed=11)
+    B32 = rnd((N, K), dev, torch.bfloat16, 0.05, seed=12)
+    A, B = ops.quantize_mx(A32), ops.quantize_mx(B32)
+    Ad = _dequant(A).to(dev).to(torch.bfloat16)  # exact: e4m3 x 2^k is a bf16 value here
+    Bd = _dequant(B).to(dev).to(torch.bfloat16)
+    assert torch.equal(Ad.double().cpu(), _dequant(A))
+    bias = rnd((N,), dev, scale=0.3, seed=13)
+    resid = rnd((M, N), dev, torch.bfloat16, seed=14)
+    drop = ops.Dropout(0.1, seed=5, offset=3)
+    outs = {}
+    for name, a, b in (("mx", A, B), ("bf16", Ad, Bd)):
+        C = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        aux = torch.empty_like(C)
+        ops.gemm(a, b, C, bias=bias, act=L.ACT_GELU_NEW, aux=aux, resid=resid, drop=drop, split_k=1)
+        dZ = torch.empty_like(C)
+        ops.gemm(a, b, dZ, dact=L.ACT_GELU_NEW, dact_src=aux, alpha=0.5, split_k=1)
+        Cs = torch.empty((M, N), device=dev, dtype=torch.float32)
+        ops.gemm(a, b, Cs, split_k=4)  # forced split-K: fp32 slabs + reduce
+        Cb = rnd((M, N), dev, seed=15)
+        ops.gemm(a, b, Cb, alpha=2.0, beta=1.0)
+        mdev = torch.tensor([100], dtype=torch.int32, device=dev)
+        Cm = torch.full((M, N), 7.0, device=dev)
+        ops.gemm(a, b, Cm, m_dev=mdev)
+        outs[name] = (C, aux, dZ, Cs, Cb, Cm)
+    for x, y, nm in zip(outs["mx"], outs["bf16"], ("C", "aux", "dZ", "split-K", "beta", "m_dev")):
+        d = (x.double() - y.double()).abs().max().item() / y.double().abs().max().clamp_min(1e-30).item()
+        assert d < 1e-2, (nm, d)  # bf16 outputs: one rounding of fp32 sums in a different order
+    assert torch.equal(outs["mx"][0] == resid, outs["bf16"][0] == resid)  # same dropout positions
+    assert torch.all(outs["mx"][5][100:] == 7.0)  # rows past m_dev untouched

@@ -3,6 +3,7 @@
 # -m gpu test, then the default bench line. Stops at the first failing step.
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd); O=$R/gpurun_out/r03; mkdir -p $O; cd $R
+if [ -x tools/microbench/mx_probe ]; then timeout -k 10 60 ./tools/microbench/mx_probe $O/mx_probe.bin || exit $?; fi
 timeout -k 10 400 python -u -m pytest tests/test_dp_nccl_gpu.py tests/test_splitk_streams_gpu.py tests/test_determinism_gpu.py tests/test_beam.py "tests/test_kernels_gpu.py::test_gemm_fused_layernorm_large_mean" -m gpu -x -v -s --timeout 200 --timeout-method thread > $O/pytest_new.log 2>&1
 rc=$?; grep -E "FAIL|ERROR|passed|failed|offset" $O/pytest_new.log | tail -12; [ $rc -eq 0 ] || exit $rc
 if [ "$1" == "full" ]; then
