@@ -203,16 +203,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   typedef typename std::conditional<MX, i32x8_t, uint4>::type frag_t;
   auto read_frags = [&](const char* As, frag_t (&af)[KS][TM], frag_t (&bfr)[KS][TN]) {
     const char* Bs = As + BM * GROWB;
-    if constexpr (MX) {  // lane (fr, fg): chunks 2 fg, 2 fg + 1 of its row = k 32 fg .. 32 fg + 31
+    if constexpr (MX) {  // lane (fr, fg): chunks fg and 4 + fg of its row = k 16 fg.. and 64 + 16 fg..
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * 16 * TM + i * 16 + fr;
-        af[0][i] = ld_mx_frag(As + lds_off(row, 2 * fg), As + lds_off(row, 2 * fg + 1));
+        af[0][i] = ld_mx_frag(As + lds_off(row, fg), As + lds_off(row, 4 + fg));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * 16 * TN + j * 16 + fr;
-        bfr[0][j] = ld_mx_frag(Bs + lds_off(row, 2 * fg), Bs + lds_off(row, 2 * fg + 1));
+        bfr[0][j] = ld_mx_frag(Bs + lds_off(row, fg), Bs + lds_off(row, 4 + fg));
       }
       return;
     }

@@ -20,9 +20,11 @@ struct fp8_t {
   uint8_t v;
 };
 
-// One block-scaled MFMA 16x16x128 (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3 A and B): lane l supplies row (l & 15),
-// k = 32 (l >> 4) .. +31 as two 16-byte chunks (lo: k 32g..32g+15, hi: 32g+16..), and the E8M0 scale of that row's
-// 32-element block in byte 0 of sa / sb (tools/microbench/mx_probe.hip pins the map).
+// One block-scaled MFMA 16x16x128 (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3 A and B). Lane map, measured
+// (tools/microbench/mx_probe.hip + tools/mx_probe_check.py, profiles/r03_mx_probe_check.txt): lane l = (g = l >> 4,
+// r = l & 15) supplies row r's bytes k = 16 g .. 16 g + 15 (operand bytes 0-15) and k = 64 + 16 g .. (bytes 16-31) —
+// the bf16 16x16x32 kernel's chunk pattern {g, 4 + g} of a 128-byte row — and, in byte op_sel of its scale VGPR,
+// the E8M0 scale of row r's 32-element block g (k = 32 g .. 32 g + 31), whichever lane holds that block's data.
 __device__ __forceinline__ void mfma_mx(f32x4_t& acc, const i32x8_t& a, const i32x8_t& b, uint32_t sa, uint32_t sb) {
   acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, (int)sa, 0, (int)sb);
 }

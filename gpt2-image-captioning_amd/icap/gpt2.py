@@ -110,6 +110,9 @@ class GPT2LMHeadModel(nn.Module):
         self.transformer = _Transformer(self.config)
         self.lm_head = nn.Linear(self.config.n_embd, self.config.vocab_size, bias=False)
         self.lm_head.weight = self.transformer.wte.weight  # tied (modeling_gpt2.py:638)
+        # BASELINE configs[4]'s fp8 path: the frozen model's training / prefill-forward and dX products run as MX
+        # block-scaled e4m3 GEMMs (weights quantised once, activations before each product); bf16 compute only
+        self.fp8_mx = False
         self._core: Optional["GPT2Core"] = None
         self._core_key = None
 
@@ -185,7 +188,7 @@ class GPT2LMHeadModel(nn.Module):
 
     def core(self, dtype: torch.dtype) -> "GPT2Core":
         dev = self.transformer.wte.weight.device
-        key = (dtype, dev)
+        key = (dtype, dev, bool(self.fp8_mx))
         if self._core is None or self._core_key != key:
             self._core = GPT2Core(self, dtype)
             self._core_key = key
@@ -226,6 +229,9 @@ class GPT2Core:
         self.hd = self.D // self.H
         self.V = c.vocab_size
         self.Vp = pad_vocab(self.V)
+        self.fp8 = bool(getattr(model, "fp8_mx", False))
+        if self.fp8 and (dtype != torch.bfloat16 or self.D % 128):
+            raise L.IcapError("fp8_mx needs the bf16 compute dtype and n_embd % 128 == 0")
         self.layers: List[_LayerW] = []
         self.refresh()
 
@@ -271,6 +277,13 @@ class GPT2Core:
             self.wpe = torch.empty_like(t.wpe.weight.data, dtype=self.dtype)
             ops.convert(t.wpe.weight.data, self.wpe)
         self.eps = self.cfg.layer_norm_epsilon
+        if self.fp8:  # MX e4m3 copies of every frozen product's weight operand, both orientations
+            for lw in self.layers:
+                for nm in ("w_attn", "w_proj", "w_fc", "w_mp"):
+                    setattr(lw, "q" + nm + "_t", ops.quantize_mx(getattr(lw, nm + "_t")))
+                    setattr(lw, "q" + nm, ops.quantize_mx(getattr(lw, nm)))
+            self.qwte = ops.quantize_mx(self.wte)
+            self.qwte_t = ops.quantize_mx(self.wte_t)
 
     @torch.no_grad()
     def bind_flat(self, flat) -> None:
@@ -279,6 +292,8 @@ class GPT2Core:
         The [in,out] (dX) orientation, wpe and the fp32 biases / LayerNorm parameters are views of that storage;
         the [out,in] (forward) transposes and the padded LM-head table are copies that refresh_from_flat()
         rewrites in place (HIP-graph capturable) after each step."""
+        if self.fp8:
+            raise L.IcapError("fp8_mx is the frozen-GPT-2 path (weights quantised once); train GPT-2 in bf16")
         t = self.model.transformer
         for blk, lw in zip(t.h, self.layers):
             lw.w_attn, lw.w_proj = flat.view_c(blk.attn.c_attn.weight), flat.view_c(blk.attn.c_proj.weight)
@@ -353,7 +368,20 @@ class GPT2Core:
         ws.dqkv = e(M, 3 * D)
         ws.do, ws.da = e(M, D), e(M, D)
         ws.dhf = e(Mh, D)
+        ws.qD = ws.q3D = ws.q4D = ws.qhf = ws.qdl = None
+        if self.fp8:  # MX operand buffers (each product quantises its activation operand into one of these)
+            mx = lambda R, K: ops.MXTensor.empty(R, K, dev)  # noqa: E731
+            ws.qD, ws.q3D, ws.q4D = mx(M, D), mx(M, 3 * D), mx(M, 4 * D)
+            ws.qhf, ws.qdl = mx(Mh, D), mx(Mh, self.Vp)
         return ws
+
+    def _mm(self, A: Tensor, qA, W: Tensor, qW, out: Tensor, rows_dev: Optional[Tensor] = None, **kw) -> Tensor:
+        """out = epi(A . W^T): the bf16 / f32 GEMM, or (fp8_mx) quantise A into qA and run the MX product with
+        the weight's MX copy qW (same epilogue arguments)."""
+        if qA is None:
+            return ops.gemm(A, W, out, **kw)
+        ops.quantize_mx(A, qA, rows=qA.R, rows_dev=rows_dev)
+        return ops.gemm(qA, qW, out, **kw)
 
     # -- dropout sites (distinct offsets so masks never coincide) -------------------------------------------
     def drops(self, train: bool, seed: int, counter: Optional[Tensor], M: int, B: int, S: int):
@@ -392,8 +420,8 @@ class GPT2Core:
         ops.layernorm_fwd(ws.x[-1], self.lnf_g, self.lnf_b, self.eps, ws.hf, ws.meanf, ws.rstdf,
                           y_rowmap=ws.row_slot if cp else None)
         rows = ws.head_rows_hint if (cp and ws.head_rows_hint is not None) else ws.Mh
-        ops.gemm(ws.hf, self.wte, ws.logits, M=ws.Mh, m_dev=ws.n_valid if cp else None,
-                 alg_flops=2.0 * rows * self.V * self.D)
+        self._mm(ws.hf, ws.qhf, self.wte, getattr(self, "qwte", None), ws.logits, rows_dev=ws.n_valid if cp else None,
+                 M=ws.Mh, m_dev=ws.n_valid if cp else None, alg_flops=2.0 * rows * self.V * self.D)
         if labels is not None:
             dl = (dlogits if dlogits is not None else ws.logits) if fuse_dlogits else None
             ops.cross_entropy(ws.logits, self.V, ws.labels_c if cp else ws.labels_shift, ws.n_valid, ws.loss, dl,
@@ -404,14 +432,15 @@ class GPT2Core:
         scale = 1.0 / math.sqrt(hd)
         for l, lw in enumerate(self.layers):
             x = ws.x[l]
+            q = lw if self.fp8 else SimpleNamespace(qw_attn_t=None, qw_proj_t=None, qw_fc_t=None, qw_mp_t=None)
             ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, ws.a1[l], ws.mean1[l], ws.rstd1[l])
-            ops.gemm(ws.a1[l], lw.w_attn_t, ws.qkv[l], bias=lw.b_attn)
+            self._mm(ws.a1[l], ws.qD, lw.w_attn_t, q.qw_attn_t, ws.qkv[l], bias=lw.b_attn)
             ops.attention_fwd(ws.qkv[l], ws.o[l], B=B, S=S, H=H, hd=hd, scale=scale, causal=True, key_mask=causal_mask,
                               lse=ws.lse[l], drop=dr.attn(l))
-            ops.gemm(ws.o[l], lw.w_proj_t, ws.h1[l], bias=lw.b_proj, resid=x, drop=dr.ra(l))
+            self._mm(ws.o[l], ws.qD, lw.w_proj_t, q.qw_proj_t, ws.h1[l], bias=lw.b_proj, resid=x, drop=dr.ra(l))
             ops.layernorm_fwd(ws.h1[l], lw.ln2_g, lw.ln2_b, self.eps, ws.a2[l], ws.mean2[l], ws.rstd2[l])
-            ops.gemm(ws.a2[l], lw.w_fc_t, ws.f[l], bias=lw.b_fc, act=L.ACT_GELU_NEW, aux=ws.z[l])
-            ops.gemm(ws.f[l], lw.w_mp_t, ws.x[l + 1], bias=lw.b_mp, resid=ws.h1[l], drop=dr.rm(l))
+            self._mm(ws.a2[l], ws.qD, lw.w_fc_t, q.qw_fc_t, ws.f[l], bias=lw.b_fc, act=L.ACT_GELU_NEW, aux=ws.z[l])
+            self._mm(ws.f[l], ws.q4D, lw.w_mp_t, q.qw_mp_t, ws.x[l + 1], bias=lw.b_mp, resid=ws.h1[l], drop=dr.rm(l))
 
     # -- backward (dX through the frozen GPT-2; + dW when trainable) ---------------------------------------------
     def backward(self, ws, dr, causal_mask, dlogits: Tensor, grads=None, dw=None) -> Tensor:
@@ -430,8 +459,8 @@ class GPT2Core:
         if cp and rows > 128:  # long K (50304), few output tiles: split K so ~2 blocks/CU work on the live rows
             tiles = -(-rows // 128) * -(-D // 128)
             split = max(1, min(16, round(512 / max(tiles, 1))))
-        ops.gemm(dlogits, self.wte_t, ws.dhf, M=ws.Mh, m_dev=ws.n_valid if cp else None,
-                 alg_flops=2.0 * rows * D * self.V, split_k=split)
+        self._mm(dlogits, ws.qdl, self.wte_t, getattr(self, "qwte_t", None), ws.dhf, rows_dev=ws.n_valid if cp else None,
+                 M=ws.Mh, m_dev=ws.n_valid if cp else None, alg_flops=2.0 * rows * D * self.V, split_k=split)
         if grads is not None:  # d(wte) from the tied LM head: dW[V,D] += dlogits^T . hf
             dw.dW(dlogits, ws.hf, grads.wte, M=M, N=self.V)
         ops.layernorm_bwd(ws.x[-1], self.lnf_g, ws.meanf, ws.rstdf, ws.dhf, ws.dx, dx_drop=ws.dxd,
@@ -446,11 +475,12 @@ class GPT2Core:
             if g is not None:
                 dw.dW(dy, ws.f[l], g.w_mp, M=M, transpose_out=True)
                 dw.db(dy, g.b_mp, M=M)
-            ops.gemm(dy, lw.w_mp, ws.dff, dact=L.ACT_GELU_NEW, dact_src=ws.z[l])
+            q = lw if self.fp8 else SimpleNamespace(qw_attn=None, qw_proj=None, qw_fc=None, qw_mp=None)
+            self._mm(dy, ws.qD, lw.w_mp, q.qw_mp, ws.dff, dact=L.ACT_GELU_NEW, dact_src=ws.z[l])
             if g is not None:
                 dw.dW(ws.dff, ws.a2[l], g.w_fc, M=M, transpose_out=True)
                 dw.db(ws.dff, g.b_fc, M=M)
-            ops.gemm(ws.dff, lw.w_fc, ws.da)
+            self._mm(ws.dff, ws.q4D, lw.w_fc, q.qw_fc, ws.da)
             ops.layernorm_bwd(ws.h1[l], lw.ln2_g, ws.mean2[l], ws.rstd2[l], ws.da, dnew, dres=dres, dx_drop=ws.dxd,
                               drop=dr.ra(l), dgamma=g.ln2_g if g else None, dbeta=g.ln2_b if g else None,
                               workspace=dw.ln_ws if dw else None)
@@ -459,13 +489,13 @@ class GPT2Core:
             if g is not None:
                 dw.dW(dy, ws.o[l], g.w_proj, M=M, transpose_out=True)
                 dw.db(dy, g.b_proj, M=M)
-            ops.gemm(dy, lw.w_proj, ws.do)
+            self._mm(dy, ws.qD, lw.w_proj, q.qw_proj, ws.do)
             ops.attention_bwd(ws.qkv[l], ws.do, ws.lse[l], ws.dqkv, B=B, S=S, H=H, hd=hd, scale=scale, causal=True,
                               key_mask=causal_mask, drop=dr.attn(l), out=ws.o[l])
             if g is not None:
                 dw.dW(ws.dqkv, ws.a1[l], g.w_attn, M=M, transpose_out=True)
                 dw.db(ws.dqkv, g.b_attn, M=M)
-            ops.gemm(ws.dqkv, lw.w_attn, ws.da)
+            self._mm(ws.dqkv, ws.q3D, lw.w_attn, q.qw_attn, ws.da)
             nxt = dr.rm(l - 1) if l > 0 else dr.embd
             ops.layernorm_bwd(ws.x[l], lw.ln1_g, ws.mean1[l], ws.rstd1[l], ws.da, dnew, dres=dres, dx_drop=ws.dxd,
                               drop=nxt, dgamma=g.ln1_g if g else None, dbeta=g.ln1_b if g else None,
@@ -493,7 +523,7 @@ class GPT2Core:
         ops.gpt2_embed(x_in, S * D, self.wte, self.wpe, None, ws.x[0], B=B, P=S, L_=0, D=D, drop=dr.embd)
         self._blocks_fwd(ws, dr, B, S, ws.M, causal_mask=ws.key_mask if mask is not None else None)
         ops.layernorm_fwd(ws.x[-1], self.lnf_g, self.lnf_b, self.eps, ws.hf, ws.meanf, ws.rstdf)
-        ops.gemm(ws.hf, self.wte, ws.logits, alg_flops=2.0 * ws.M * self.V * self.D)
+        self._mm(ws.hf, ws.qhf, self.wte, getattr(self, "qwte", None), ws.logits, alg_flops=2.0 * ws.M * self.V * self.D)
         loss = None
         if lab is not None:
             ops.cross_entropy(ws.logits, self.V, ws.labels_shift, ws.n_valid, ws.loss, None, ws.ce_ws)
@@ -528,25 +558,46 @@ class GPT2Core:
         # per-token steps (rows = B <= 128): ln_1 / ln_2 run inside the QKV / c_fc GEMMs (one launch each
         # instead of two; the decode step is bound by its ~90 launches, not by bytes)
         fuse_ln = rows <= 128
+        # fp8_mx: the tile-kernel products (prefill, beam steps over R = B*W > 128 rows) run as MX GEMMs
+        mx = self.fp8 and not fuse_ln
+        qD, q4 = (self._dq(ds, rows, D), self._dq(ds, rows, 4 * D)) if mx else (None, None)
+        nq = SimpleNamespace(qw_attn_t=None, qw_proj_t=None, qw_fc_t=None, qw_mp_t=None)
         for l, lw in enumerate(self.layers):
+            q = lw if mx else nq
             qkv = ds.cache[l][pos0 * B: (pos0 + npos) * B]
             if fuse_ln:
                 ops.gemm(x, lw.w_attn_t, qkv, bias=lw.b_attn, M=rows, ln=(lw.ln1_g, lw.ln1_b, self.eps))
             else:
                 ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, a, None, None, rows=rows)
-                ops.gemm(a, lw.w_attn_t, qkv, bias=lw.b_attn, M=rows)
+                self._mm(a, qD, lw.w_attn_t, q.qw_attn_t, qkv, bias=lw.b_attn, M=rows)
             if prefill:
                 ops.attention_fwd(ds.cache[l], o, B=B, S=npos, H=H, hd=hd, scale=scale, causal=True, rsb=1, rss=B)
             else:
                 ops.attention_decode(ds.cache[l], o, B=B, H=H, hd=hd, pos=pos0, scale=scale,
                                      anc=getattr(ds, "anc", None))
-            ops.gemm(o, lw.w_proj_t, h1, bias=lw.b_proj, resid=x, M=rows)
+            self._mm(o, qD, lw.w_proj_t, q.qw_proj_t, h1, bias=lw.b_proj, resid=x, M=rows)
             if fuse_ln:
                 ops.gemm(h1, lw.w_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows, ln=(lw.ln2_g, lw.ln2_b, self.eps))
             else:
                 ops.layernorm_fwd(h1, lw.ln2_g, lw.ln2_b, self.eps, a, None, None, rows=rows)
-                ops.gemm(a, lw.w_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows)
-            ops.gemm(f, lw.w_mp_t, x, bias=lw.b_mp, resid=h1, M=rows)
+                self._mm(a, qD, lw.w_fc_t, q.qw_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows)
+            self._mm(f, q4, lw.w_mp_t, q.qw_mp_t, x, bias=lw.b_mp, resid=h1, M=rows)
+
+    def _dq(self, ds, rows: int, K: int):
+        """MX operand buffer of the decode state for (rows, K) (allocated on first use, outside graph capture:
+        the eager warm-up pass of a runner reaches every shape first)."""
+        if not hasattr(ds, "mx"):
+            ds.mx = {}
+        key = (rows, K)
+        if key not in ds.mx:
+            ds.mx[key] = ops.MXTensor.empty(rows, K, self.dev)
+        return ds.mx[key]
+
+    def _head_mm(self, ds, a: Tensor, rows: int) -> None:
+        """LM head of `rows` decode rows (bf16 skinny / tile GEMM; fp8_mx: MX when it takes the tile kernel)."""
+        mx = self.fp8 and rows > 128
+        self._mm(a, self._dq(ds, rows, self.D) if mx else None, self.wte, self.qwte if mx else None, ds.logits,
+                 M=rows, alg_flops=2.0 * rows * self.V * self.D)
 
     def _decode_head(self, ds, x_last: Tensor, step: int, pos_next: int, samp=None):
         """ln_f + LM head on the last position, then the next token: argmax (greedy) or, with samp = (temperature,
@@ -556,7 +607,7 @@ class GPT2Core:
         B = ds.B
         a = ds.a[:B]
         ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
-        ops.gemm(a, self.wte, ds.logits, M=B, alg_flops=2.0 * B * self.V * self.D)
+        self._head_mm(ds, a, B)
         forced = None
         if samp is not None:
             temperature, top_p, seed_dev, forced = samp
@@ -662,7 +713,7 @@ class GPT2Core:
         R = ds.B
         a = ds.a[:R]
         ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=R)
-        ops.gemm(a, self.wte, ds.logits, M=R, alg_flops=2.0 * R * self.V * self.D)
+        self._head_mm(ds, a, R)
         nxt_x = ds.x[:R] if pos + 1 < ds.T else None
         ds.beam.step(ds.logits, step, pos, nxt_x)
 

@@ -39,7 +39,8 @@ def load_gpt2_tokenizer(path: Optional[str] = None):
 class ImageCaptioningModel(nn.Module):
     def __init__(self, mapping_network: nn.Module, image_prefix_length: Optional[int] = None,
                  prefix_task_prompt: Optional[str] = None, tokenizer=None, gpt: Optional[GPT2LMHeadModel] = None,
-                 freeze_gpt_weights: bool = True, compute_dtype: torch.dtype = torch.bfloat16) -> None:
+                 freeze_gpt_weights: bool = True, compute_dtype: torch.dtype = torch.bfloat16,
+                 gpt_fp8: bool = False) -> None:
         super().__init__()
         self.image_prefix_length = image_prefix_length or mapping_network.prefix_length
         self.mapping_network = mapping_network
@@ -61,6 +62,10 @@ class ImageCaptioningModel(nn.Module):
                 emb = self.gpt.transformer.wte.weight[ids.reshape(-1)].clone()
             self.task_prefix_embeds = nn.Parameter(emb, requires_grad=True)
         self.compute_dtype = compute_dtype
+        # BASELINE configs[4]: the frozen GPT-2's training / forward products as MX fp8 GEMMs (icap.gpt2.GPT2Core)
+        if gpt_fp8 and (not freeze_gpt_weights or compute_dtype != torch.bfloat16):
+            raise ValueError("gpt_fp8 needs freeze_gpt_weights=True and compute_dtype=torch.bfloat16")
+        self.gpt.fp8_mx = bool(gpt_fp8)
         self._flat: Optional[FlatParams] = None
         self._synced_version = None
         self._fwd_cache = {}

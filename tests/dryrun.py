@@ -162,6 +162,26 @@ def accesses(name, args):
         dt, B, H, hd, pos, cache, ldc, o, ldo, _sc, _s = a
         es = ES[dt]
         out += [("cache", cache, ((pos + 1) * B - 1) * ldc * es + 3 * H * hd * es), ("out", o, _rows(B, ldo, H * hd, es))]
+    elif name in ("icap_beam_init", "icap_beam_update", "icap_beam_finalize"):
+        b = a[0]._obj
+        R = b.B * b.W
+        out += [("ws", b.ws, _lib.load().icap_beam_workspace_bytes(b.B, b.W, b.T, b.max_len))]
+        if name == "icap_beam_update":
+            es = ES[b.dtype]
+            out += [("top_val", b.top_val, R * b.K * 4), ("top_idx", b.top_idx, R * b.K * 4), ("top_m", b.top_m, R * 4),
+                    ("top_ls", b.top_ls, R * 4), ("x", b.x, R * b.D * es), ("wte", b.wte, b.V * b.D * es),
+                    ("wpe", b.wpe, b.n_positions * b.D * es)]
+        if name == "icap_beam_finalize":
+            out += [("out", a[1], b.B * b.max_len * 8), ("out_len", a[2], b.B * 4)]
+    elif name == "icap_beam_rowtop":
+        dt, R, V, lg, ld, K, tv, ti, tm, tl, _s = a
+        out += [("logits", lg, _rows(R, ld, V, ES[dt])), ("top_val", tv, R * K * 4), ("top_idx", ti, R * K * 4),
+                ("top_m", tm, R * 4), ("top_ls", tl, R * 4)]
+    elif name == "icap_attention_decode_anc":
+        dt, B, H, hd, pos, cache, ldc, anc, o, ldo, _sc, _s = a
+        es = ES[dt]
+        out += [("cache", cache, ((pos + 1) * B - 1) * ldc * es + 3 * H * hd * es), ("anc", anc, (pos + 1) * B * 4),
+                ("out", o, _rows(B, ldo, H * hd, es))]
     elif name == "icap_embedding_scatter_add":
         dt, B, P, L, D, dx, ids, dw, _s = a
         out += [("dx", dx, B * (P + L) * D * ES[dt]), ("ids", ids, B * L * 8), ("dwte", dw, D * 4)]

@@ -170,3 +170,27 @@ def test_gpt2_small_bench_shape_with_clip_in_bounds():
         t.micro_step()
         model.generate(torch.randn(4, 512), max_length=3, temperature=0.0)
         _assert_clean(rec)
+
+
+def test_fp8_gpt_schedule_in_bounds():
+    """BASELINE configs[4]'s fp8 path (gpt_fp8=True): every MX quantise / GEMM of the train step and the forward
+    stays inside live allocations (operands, scales, device row counts of the compact head)."""
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        cfg = GPT2Config(vocab_size=512, n_positions=128, n_embd=128, n_layer=2, n_head=2, eos_token_id=511)
+        gpt = GPT2LMHeadModel(cfg)
+        tok = SimpleNamespace(eos_token_id=511)
+        model = ImageCaptioningModel(TransformerMappingNetwork(64, 128, 5, 4, 2), tokenizer=tok, gpt=gpt,
+                                     compute_dtype=torch.bfloat16, gpt_fp8=True)
+        t = CaptionTrainer(model, 3, 12, num_training_steps=3, dropout=True)
+        t.load_batch(*batch(3, 12))
+        t.micro_step()
+        with torch.no_grad():
+            model.eval()(*[x for x in batch(3, 12)][:1], batch(3, 12)[3], None, None)
+            model.generate(torch.randn(30, 64), max_length=3, temperature=0.0)  # prefill 150 rows: MX products
+            model.generate(torch.randn(40, 64), max_length=3, num_beams=4)  # beam rows 160: MX steps + head
+        _assert_clean(rec)
+        names = [c[0] for c in rec.calls]
+        gemms = [c[1][0]._obj for c in rec.calls if c[0] == "icap_gemm"]
+    assert names.count("icap_quantize_mx") >= 2 * 8 + 2  # 4 fwd + 4 bwd products per layer, LM head fwd + dX
+    assert sum(g.in_dtype == 2 for g in gemms) >= 2 * 8 + 2

@@ -3,7 +3,8 @@
 1. icap_quantize_mx == oracle.mx_quantize bit for bit (element codes as values, scale bytes in the GEMM's layout,
    padded row groups at scale 1.0), bf16 and f32 inputs, zero blocks, wide dynamic range.
 2. icap_gemm with ICAP_FP8_MX operands == fp64 product of the DEQUANTISED operands (the only rounding left is the
-   fp32 accumulation): per-element error <= 1e-5 of sum |a||b|.
+   MFMA's accumulation: the block-scaled MFMA sums a 128-deep step at ~2e-5 of its largest term, measured on the
+   lane-map probe, profiles/r03_mx_probe_check.txt): per-element error <= 1e-4 of sum |a||b|.
 3. The epilogues (bias + gelu_new + aux, residual + dropout, backward dact, beta) and split-K, m_dev behave as on
    bf16 inputs: the fp8 launch equals the bf16 launch run on the dequantised operands (rounded to bf16, which is
    exact for e4m3 values times power-of-two scales in bf16 range) within fp32 accumulation-order noise."""
@@ -66,7 +67,7 @@ def test_gemm_mx_equals_dequantized_product(dev, M, N, K):
     ref = a @ b.t()
     scale = a.abs() @ b.abs().t()
     err = ((C.cpu().double() - ref).abs() / (scale + 1e-30)).max().item()
-    assert err < 1e-5, err
+    assert err < 1e-4, err
 
 
 def test_gemm_mx_epilogues_split_k_and_m_dev(dev):
@@ -94,9 +95,64 @@ def test_gemm_mx_epilogues_split_k_and_m_dev(dev):
         mdev = torch.tensor([100], dtype=torch.int32, device=dev)
         Cm = torch.full((M, N), 7.0, device=dev)
         ops.gemm(a, b, Cm, m_dev=mdev)
-        outs[name] = (C, aux, dZ, Cs, Cb, Cm)
-    for x, y, nm in zip(outs["mx"], outs["bf16"], ("C", "aux", "dZ", "split-K", "beta", "m_dev")):
+        Cd = torch.empty((M, N), device=dev, dtype=torch.float32)  # dropout alone: dropped elements are exactly 0
+        ops.gemm(a, b, Cd, bias=bias, act=L.ACT_GELU_NEW, drop=drop, split_k=1)
+        outs[name] = (C, aux, dZ, Cs, Cb, Cm, Cd)
+    for x, y, nm in zip(outs["mx"], outs["bf16"], ("C", "aux", "dZ", "split-K", "beta", "m_dev", "drop")):
         d = (x.double() - y.double()).abs().max().item() / y.double().abs().max().clamp_min(1e-30).item()
         assert d < 1e-2, (nm, d)  # bf16 outputs: one rounding of fp32 sums in a different order
-    assert torch.equal(outs["mx"][0] == resid, outs["bf16"][0] == resid)  # same dropout positions
+    assert torch.equal(outs["mx"][6] == 0, outs["bf16"][6] == 0)  # same dropout positions
+    assert 0.05 < float((outs["mx"][6] == 0).float().mean()) < 0.15
     assert torch.all(outs["mx"][5][100:] == 7.0)  # rows past m_dev untouched
+
+
+# ------------------------------------------------------------ configs[4] caption model (GPT-2 large) with fp8_mx
+from test_model_gpu import _trainer_steps, build, inputs, load, rel  # noqa: E402
+
+LRG_G = O.GPT2Cfg(n_layer=36, n_embd=1280, n_head=20)
+LRG_M = O.MapperCfg(embed_dim=1024, gpt_dim=1280)
+
+
+def _large_fp8(dev):
+    m = build(LRG_G, LRG_M, torch.bfloat16, dev)
+    m.gpt.fp8_mx = True
+    return m
+
+
+def test_large_forward_fp8(dev):
+    """GPT-2 large + mapper gpt_dim 1280 with every frozen product in MX fp8 vs the reference's fp32 forward
+    (tests/golden/large.npz). Bounds: loss |d| <= 0.1, selected-logit max-rel <= 0.15, argmax agreement >= 70 %
+    (bf16 alone: 5e-2 / 8e-2 / 80 %, test_parity_gpu.py::test_large_forward_bf16)."""
+    g = load("large")
+    ids, mask, labels, emb = inputs(g, dev)
+    model = _large_fp8(dev).eval()
+    core = model.gpt.core(torch.bfloat16)
+    assert core.fp8 and core.layers[0].qw_attn_t.q.dtype == torch.uint8
+    with torch.no_grad():
+        out = model(ids, emb, mask, labels)
+    dl = abs(out.loss.item() - g["loss"][0])
+    rows = torch.from_numpy(g["logit_rows"])
+    r = rel(out.logits[:2][:, rows], g["logits_sel"])
+    agree = float((out.logits.argmax(-1).cpu().numpy() == g["argmax"]).mean())
+    print(f"fp8 large forward: loss |d| {dl:.4f}, logits max-rel {r:.4f}, argmax agreement {agree:.3f}")
+    assert dl < 0.1 and r < 0.15 and agree >= 0.7
+
+
+def test_large_train_fp8(dev):
+    """Two fused train steps (mapper trained, GPT-2 frozen in fp8). Step 1 (before any update) vs the reference's
+    train() loss: |d| <= 0.05. Step 2 and the update vs the bf16 trainer on the same batch (the benchmarked
+    precision; bf16 itself is 0.31 off the fp32 reference at step 2 of this golden: AdamW turns rounding noise on
+    near-zero gradients into full-size steps): loss |d| <= 0.05, mapper-update cosine >= 0.8 (measured 0.941)."""
+    g = load("large")
+    b = inputs(g, dev)
+    m8 = _large_fp8(dev)
+    init = {k: v.detach().clone() for k, v in m8.mapping_network.state_dict().items()}
+    l8, _ = _trainer_steps(m8, b, 2)
+    mb = build(LRG_G, LRG_M, torch.bfloat16, dev)
+    lb, _ = _trainer_steps(mb, b, 2)
+    d = [abs(l8[0] - g["train_losses"][0]), abs(l8[1] - lb[1])]
+    u8 = torch.cat([(v.detach() - init[k]).double().reshape(-1) for k, v in m8.mapping_network.state_dict().items()])
+    ub = torch.cat([(v.detach() - init[k]).double().reshape(-1) for k, v in mb.mapping_network.state_dict().items()])
+    cos = float(torch.nn.functional.cosine_similarity(u8, ub, dim=0))
+    print(f"fp8 large train: losses {l8} (bf16 {lb}, reference {list(g['train_losses'])}), update cosine vs bf16 {cos:.3f}")
+    assert max(d) < 0.05 and cos >= 0.8

@@ -44,7 +44,7 @@ def run(path):
           (f"; first {[(float(X[i]), float(dev[i]), float(ref[i])) for i in bad[:6]]}" if len(bad) else ""))
     for t in range(ntr):
         b = raw[t * rec:(t + 1) * rec]
-        osa, osb = np.frombuffer(b[:8], np.int32)
+        osa, osb = (int(v) for v in np.frombuffer(b[:8], np.int32))
         A = np.frombuffer(b[8:2056], np.uint8).reshape(64, 32)
         B = np.frombuffer(b[2056:4104], np.uint8).reshape(64, 32)
         SA = np.frombuffer(b[4104:4360], np.uint32)
