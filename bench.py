@@ -30,6 +30,7 @@ import torch  # noqa: E402
 
 METRIC = "training images/sec + greedy captions/sec, GPT2-small+CLIP-B/32 at 1/2/4/8 GPU"
 BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+FP8_PEAK_TFLOPS = 5000.0  # dense MX fp8 (block-scaled 16x16x128 f8f6f4: 2x bf16 per clock, same table)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -66,7 +67,7 @@ class GemmTimer:
         return agg
 
 
-def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16):
+def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16, fp8=False):
     """config "small": BASELINE configs[1] (GPT-2 small + CLIP ViT-B/32); "medium": configs[3] (GPT-2 medium +
     CLIP ViT-L/14 encoder on the device, mapper at gpt_dim 1024 / CLIP-L embed 768)."""
     from types import SimpleNamespace
@@ -81,7 +82,7 @@ def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16):
         gpt = GPT2LMHeadModel.random_init(GPT2Config.large(), seed=0)
         mapper = TransformerMappingNetwork.random_init(embed_dim=1024, gpt_dim=1280, seed=0)
         model = ImageCaptioningModel(mapper, tokenizer=SimpleNamespace(eos_token_id=50256), gpt=gpt,
-                                     compute_dtype=dtype).to(dev)
+                                     compute_dtype=dtype, gpt_fp8=fp8).to(dev)
         tower = DINOv3ImageTower.random_init(seed=0).to(dev)
         trainer = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10 ** 6, clip_model=tower,
                                  dropout=dropout, seed=1234)
@@ -95,7 +96,7 @@ def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16):
         mapper = TransformerMappingNetwork.random_init(seed=0)
         tower_cfg = None
     model = ImageCaptioningModel(mapper, tokenizer=SimpleNamespace(eos_token_id=50256), gpt=gpt,
-                                 compute_dtype=dtype).to(dev)
+                                 compute_dtype=dtype, gpt_fp8=fp8).to(dev)
     tower = CLIPVisionTower.random_init(tower_cfg, seed=0).to(dev)
     trainer = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10 ** 6, clip_model=tower, dropout=dropout,
                              seed=1234)
@@ -405,6 +406,74 @@ def launcher_probe():
         torch.distributed.destroy_process_group()
 
 
+def kernel_peak(name: str) -> float:
+    return FP8_PEAK_TFLOPS if "fp8_t" in name else BF16_PEAK_TFLOPS
+
+
+def train_rate(trainer, B, steps, warmup, use_graph, world, dev):
+    """images/s over `steps` graph-replayed steps after `warmup` (barrier + synchronize on both sides, max over
+    ranks), and the GEMM roofline of one eager step (HIP events around every GEMM launch)."""
+    from icap import ops
+
+    dist = world > 1
+    for _ in range(max(warmup, 1)):
+        trainer.micro_step(use_graph=use_graph)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        trainer.micro_step(use_graph=use_graph)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    loss = float(trainer.last_loss.item())
+    timer = GemmTimer()
+    ops.GEMM_TIMER = timer
+    torch.cuda.synchronize()
+    te0 = time.perf_counter()
+    trainer._fwd_bwd(True, trainer.grad_scale())
+    trainer._optimizer()
+    torch.cuda.synchronize()
+    eager_ms = (time.perf_counter() - te0) * 1e3
+    ops.GEMM_TIMER = None
+    agg = timer.summary(os.environ.get("ICAP_GEMM_DETAIL"))
+    dom = max(agg, key=lambda k: agg[k][2])
+    n_l, fl, ms = agg[dom]
+    achieved = fl / (ms * 1e-3) / 1e12
+    return {"el": el, "loss": loss, "images_per_s": world * B * steps / el, "ms_per_step": el / steps * 1e3,
+            "dom": dom, "n_l": n_l, "fl": fl, "ms": ms, "achieved": achieved,
+            "frac": achieved / kernel_peak(dom), "gemm_ms": sum(v[2] for v in agg.values()),
+            "all_fl": sum(v[1] for v in agg.values()), "eager_ms": eager_ms}
+
+
+def batch_sweep(config, batches, dev, world, fp8=False):
+    """SURVEY.md §8(d) perf batch sweep: the same train step at other per-GPU batches (weak-scaling B is a free
+    choice; the reference's is config.yml:32 = 128): images/s and the dominant GEMM's roofline fraction."""
+    out = []
+    for Bs in batches:
+        model, tower, tr = build(Bs, dev, config=config, fp8=fp8)
+        ids, mask, labels, px = synthetic_batch(Bs, 11, dev)
+        tr.load_batch(ids, mask, labels, pixels=px)
+        tr.gws.head_rows_hint = int((labels != -100).sum().item())
+        r = train_rate(tr, Bs, 5, 2, True, world, dev)
+        out.append({"batch_per_gpu": Bs, "images_per_s": round(r["images_per_s"], 1),
+                    "ms_per_step": round(r["ms_per_step"], 3), "dominant_kernel": r["dom"],
+                    "dominant_frac": round(r["frac"], 4), "dominant_tflops": round(r["achieved"], 1),
+                    "all_gemm_ms_per_step": round(r["gemm_ms"], 3)})
+        del model, tower, tr
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return out
+
+
 EDIM = {"small": 512, "medium": 768, "large": 1024}  # image-embedding width per config (CLIP-B/32, CLIP-L/14, DINOv3-L)
 
 
@@ -421,7 +490,11 @@ def main():
     ap.add_argument("--no-decode", action="store_true", help="skip the greedy-decode measurement (PMC passes)")
     ap.add_argument("--config", default="small", choices=["small", "medium", "large"],
                     help="small = BASELINE configs[1] (default, the headline); medium = configs[3]; "
-                         "large = configs[4] (DINOv3 ViT-L/16 + GPT-2 large, beam-4 decode; bf16, fp8 not built)")
+                         "large = configs[4] (DINOv3 ViT-L/16 + GPT-2 large, beam-4 decode)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="configs[4]'s fp8 path: GPT-2's frozen products as MX block-scaled e4m3 GEMMs")
+    ap.add_argument("--sweep", default=None,
+                    help="comma-separated extra per-GPU batches for the batch sweep (default: 256,512 for small)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -441,52 +514,20 @@ def main():
     torch.cuda.set_device(dev)
     B = args.batch
 
-    model, tower, trainer = build(B, dev, config=args.config)
+    if args.fp8 and args.config != "large":
+        raise SystemExit("bench.py: --fp8 is configs[4]'s path (--config large)")
+    model, tower, trainer = build(B, dev, config=args.config, fp8=args.fp8)
     ids, mask, labels, px = synthetic_batch(B, 1 + rank, dev)  # each rank: its own shard of samples
     trainer.load_batch(ids, mask, labels, pixels=px)
     # LM-head target rows of this batch (the device holds the count; the host copy only prices the roofline)
     head_rows = int((labels != -100).sum().item())
     trainer.gws.head_rows_hint = head_rows
     use_graph = not args.no_graph
-    for _ in range(max(args.warmup, 1)):
-        trainer.micro_step(use_graph=use_graph)
-    torch.cuda.synchronize()
-    if dist:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        trainer.micro_step(use_graph=use_graph)
-    torch.cuda.synchronize()
-    if dist:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el = float(t.item())
-    loss = float(trainer.last_loss.item())
-    imgs_per_s = world * B * args.steps / el
-
-    # -- kernel roofline pass: every GEMM launch of one eager step, timed with HIP events ----------------------
-    from icap import ops
-
-    timer = GemmTimer()
-    ops.GEMM_TIMER = timer
-    torch.cuda.synchronize()
-    te0 = time.perf_counter()
-    trainer._fwd_bwd(True, trainer.grad_scale())
-    trainer._optimizer()
-    torch.cuda.synchronize()
-    eager_ms = (time.perf_counter() - te0) * 1e3
-    ops.GEMM_TIMER = None
-    agg = timer.summary(os.environ.get("ICAP_GEMM_DETAIL"))
-    gemm_ms = sum(v[2] for v in agg.values())
-    dom = max(agg, key=lambda k: agg[k][2])
-    n_l, fl, ms = agg[dom]
-    achieved = fl / (ms * 1e-3) / 1e12
-    all_fl = sum(v[1] for v in agg.values())
+    # timed region + the kernel roofline pass (every GEMM launch of one eager step, timed with HIP events)
+    r = train_rate(trainer, B, args.steps, args.warmup, use_graph, world, dev)
+    el, loss, imgs_per_s = r["el"], r["loss"], r["images_per_s"]
+    dom, n_l, fl, ms, achieved = r["dom"], r["n_l"], r["fl"], r["ms"], r["achieved"]
+    gemm_ms, all_fl, eager_ms = r["gemm_ms"], r["all_fl"], r["eager_ms"]
 
     # -- greedy decode throughput ------------------------------------------------------------------------------
     Bd = args.decode_batch
@@ -506,19 +547,27 @@ def main():
     prep = None if args.no_decode else preprocess_rate(dev)
     extract = extraction_child() if (not args.no_decode and args.config == "small" and rank == 0) else None
     parity = parity_mode_rate(B, dev) if (not args.no_decode and args.config == "small" and world == 1) else None
+    sweep_b = [int(x) for x in args.sweep.split(",") if x] if args.sweep is not None else \
+        ([256, 512] if args.config == "small" and not args.no_decode and world == 1 else [])
+    if sweep_b:
+        del model, tower, trainer
+        torch.cuda.empty_cache()
+    sweep = batch_sweep(args.config, sweep_b, dev, world, args.fp8) if sweep_b else None
 
     if rank == 0:
         res = {
             "metric": METRIC, "value": round(imgs_per_s, 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp8 (MX e4m3, GPT-2 products) + bf16" if args.fp8 else "bf16",
             "data": "synthetic (seeded COCO-shaped captions: 13 tokens + EOS, padded to 50; randn 224x224 pixels); "
                     "deterministic random-init weights",
             "config": {"workload": ("train step: CLIP ViT-B/32 fwd (frozen) on 224x224 pixels -> transformer mapper "
                                     "(8 layers, prefix 15, trained) -> GPT-2 small (frozen) fwd + dX bwd, LM head on "
                                     "the target rows + CE, dropout 0.1, clip_grad_norm 1.0 + AdamW + linear LR")
                        if args.config == "small" else
-                       ("BASELINE configs[4] train step (bf16; the fp8 MFMA path is not built): DINOv3 ViT-L/16 fwd "
+                       (f"BASELINE configs[4] train step ({'fp8: every frozen GPT-2 product (fwd, dX, LM head) as an MX block-scaled e4m3 GEMM, the rest bf16' if args.fp8 else 'bf16'}): "
+                        "DINOv3 ViT-L/16 fwd "
                         "(frozen, 4 registers + RoPE, 201 tokens) on 224x224 pixels -> transformer mapper (8 layers, "
                         "gpt_dim 1280, trained) -> GPT-2 large (36 layers, d 1280, frozen) fwd + dX bwd, LM head on "
                         "the target rows + CE, dropout 0.1, clip 1.0 + AdamW; decode: beam-4")
@@ -539,8 +588,9 @@ def main():
             "clip_preprocess": prep,
             "clip_extraction": extract,
             "fp32_parity_mode": parity,
+            "batch_sweep": sweep,
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1),
-                         "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+                         "peak": kernel_peak(dom), "unit": "TFLOP/s", "frac": round(achieved / kernel_peak(dom), 4),
                          "traffic": traffic, "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC: 2 x FETCH_SIZE + WRITE_SIZE)",
                          "traffic_source": traffic_src, "launches_per_step": n_l,
                          "avg_launch_us": round(ms / n_l * 1e3, 2),

@@ -209,16 +209,28 @@ _gemm_ws = {}
 
 def gemm_workspace(device, stream=None) -> Tensor:
     """fp32 split-K scratch of one (device, stream): launches ordered on one stream reuse a buffer safely, and
-    launches on two streams get two buffers, so concurrent split-K GEMMs never overwrite each other's slabs
-    (a GEMM's slabs are written and reduced inside its own stream-ordered launches). A HIP graph captures the
-    buffer of its capture stream; graphs replayed one after another (the trainer's step / segment graphs) share it
-    like eager launches on one stream do."""
+    eager launches on two streams get two buffers, so concurrent split-K GEMMs never overwrite each other's slabs
+    (a GEMM's slabs are written and reduced inside its own stream-ordered launches).
+    Under HIP-graph capture no memory may be allocated (a block of the graph's private pool outlives the graph
+    here and aborts the allocator when that graph is destroyed), so every capture uses one per-device graph
+    buffer, allocated with the device's first eager buffer: graphs replayed one after another (the trainer's step
+    / segment graphs, decode chunks) share it as eager launches on one stream share theirs; two graphs that
+    contain split-K GEMMs must not be replayed concurrently on different streams."""
+    if stream is not None and torch.cuda.is_current_stream_capturing():
+        ws = _gemm_ws.get((device.type, device.index, "graph"))
+        if ws is None:
+            raise L.IcapError("gemm: a split-K workspace is needed inside graph capture; run one eager GEMM on "
+                              "this device first (or pass workspace=)")
+        return ws
     sid = 0 if stream is None else int(stream.cuda_stream)
     key = (device.type, device.index, sid)
     ws = _gemm_ws.get(key)
     if ws is None:
         ws = torch.empty(GEMM_WORKSPACE_BYTES // 4, dtype=torch.float32, device=device)
         _gemm_ws[key] = ws
+        gkey = (device.type, device.index, "graph")
+        if stream is not None and gkey not in _gemm_ws:
+            _gemm_ws[gkey] = torch.empty(GEMM_WORKSPACE_BYTES // 4, dtype=torch.float32, device=device)
     return ws
 
 

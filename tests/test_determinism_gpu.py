@@ -32,8 +32,19 @@ def _snapshot(t):
     return [(n, x.detach().clone()) for n, x in snap if x is not None]
 
 
-def _bits(x):
-    return x.view({2: torch.int16, 4: torch.int32, 8: torch.int64}[x.element_size()])
+def _same(a, b):
+    """Equal values, NaN == NaN (the compact head leaves unused logits rows unwritten: they may hold NaN
+    patterns of earlier allocations, whose payload bits are not a value)."""
+    if not a.is_floating_point():
+        return torch.equal(a, b)
+    return bool(((a == b) | (a.isnan() & b.isnan())).all())
+
+
+def _same(a, b):
+    """Equal values with NaN == NaN: the compact LM head leaves the logits rows past the device's target count
+    unwritten, so they hold whatever an earlier allocation left there (NaN patterns included, which torch.equal
+    never calls equal)."""
+    return bool(((a == b) | (a.isnan() & b.isnan())).all())
 
 
 def _noise(dev, n):
@@ -73,7 +84,11 @@ def test_train_step_bitwise_with_concurrent_stream(dev, B):
         s.synchronize()
         got = _snapshot(t)
         for (name, a), (_, b) in zip(ref, got):
-            if not torch.equal(a, b):
+            if not _same(a, b):
+                diff = ~((a == b) | (a.isnan() & b.isnan()))
+                rows = sorted(set(diff.nonzero()[:, 0].tolist())) if a.dim() > 1 else []
                 d = (a.float() - b.float()).abs()
-                pytest.fail(f"rep {rep}: first differing buffer '{name}': {int((d > 0).sum())} elements, "
-                            f"max |d| {float(d.max()):.3g}")
+                pytest.fail(f"rep {rep}: first differing buffer '{name}': {int(diff.sum())} elements "
+                            f"(NaN before {int(a[diff].isnan().sum())}, now {int(b[diff].isnan().sum())}), rows "
+                            f"{rows[:8]} ({len(rows)}), n_valid {int(t.gws.n_valid.item())}, max finite |d| "
+                            f"{float(d[d.isfinite()].max()) if d.isfinite().any() else 0.0:.3g}")

@@ -431,6 +431,43 @@ def golden_large(workdir):
     print("large beam4", ids.tolist())
 
 
+def golden_bench128(workdir):
+    """The benchmarked shape itself (bench.py / BASELINE configs[1]): B = 128 images, CLIP
+    ViT-B/32 features from seeded 224x224 pixels (HF CLIPModel.get_image_features -> pooler_output, L2-normalised as
+    src/embeddings/clip.py:132-137), COCO-shaped 50-token captions (13 tokens + EOS), S = 65, GPT-2 small frozen +
+    transformer mapper, 2 reference train() steps (src/train.py, lr 1e-4, dropout off). Stored small: the
+    embeddings, the forward loss, the train losses, per-tensor checksums of the trained mapper and every 997th
+    element of each trained tensor (update-direction bounds for the bf16 run)."""
+    from transformers import CLIPConfig, CLIPModel
+
+    gcfg, mcfg = O.GPT2Cfg(), O.MapperCfg()
+    hf = CLIPModel(CLIPConfig())
+    missing, unexpected = hf.load_state_dict(O.clip_vision_state_dict(O.ClipCfg(), seed=0), strict=False)
+    assert not unexpected
+    hf.eval()
+    B = 128
+    px = torch.randn((B, 3, 224, 224), generator=torch.Generator().manual_seed(21))
+    with torch.no_grad():
+        feats = hf.get_image_features(pixel_values=px)
+        feats = getattr(feats, "pooler_output", feats)
+        emb = feats / feats.norm(p=2, dim=-1, keepdim=True)
+    ids, mask, labels, _ = O.synthetic_batch(B, 50, 13, gcfg.vocab_size, gcfg.eos, mcfg.embed_dim, seed=22)
+    torch.manual_seed(0)
+    model, _, _ = build_ref(gcfg, mcfg, seed=0)
+    model.eval()
+    with torch.no_grad():
+        res = model.forward(caption_token_ids=ids, image_embeddings=emb, attention_mask=mask, labels=labels)
+    out = {"pixels_seed": np.array([21]), "batch_seed": np.array([22]), "emb": emb.numpy(),
+           "loss": np.array([res.loss.item()]), "lse_row0": torch.logsumexp(res.logits[0].double(), -1).numpy()}
+    losses = run_ref_train(model, (ids, mask, labels, emb), 2, 1e-4, True, workdir)
+    out["train_losses"] = np.array(losses)
+    for k, v in model.mapping_network.state_dict().items():
+        out["trained_ck." + k] = checksum(v)
+        out["trained_sample." + k] = v.detach().numpy().reshape(-1)[::997].copy()
+    np.savez_compressed(os.path.join(OUT, "bench128.npz"), **out)
+    print("bench128 loss", out["loss"], "train", losses)
+
+
 def golden_ckpt_keys(workdir):
     """Key sets + shapes of the reference's save_parameters() files (src/models.py:489-519) for the transformer
     mapper with GPT-2 frozen / unfrozen and the MLP mapper (GPT-2 small geometry), and of its extraction .pt
@@ -491,6 +528,8 @@ def main():
             golden_medium(work)
         if not only or "large" in only:
             golden_large(work)
+        if not only or "bench128" in only:
+            golden_bench128(work)
         if not only or "ckpt" in only:
             golden_ckpt_keys(work)
     finally:
