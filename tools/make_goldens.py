@@ -436,8 +436,8 @@ def golden_bench128(workdir):
     ViT-B/32 features from seeded 224x224 pixels (HF CLIPModel.get_image_features -> pooler_output, L2-normalised as
     src/embeddings/clip.py:132-137), COCO-shaped 50-token captions (13 tokens + EOS), S = 65, GPT-2 small frozen +
     transformer mapper, 2 reference train() steps (src/train.py, lr 1e-4, dropout off). Stored small: the
-    embeddings, the forward loss, the train losses, per-tensor checksums of the trained mapper and every 997th
-    element of each trained tensor (update-direction bounds for the bf16 run)."""
+    embeddings, the forward loss, the train losses, per-tensor checksums of the trained mapper and each trained
+    tensor whole (<= 20000 elements) or every 997th element (update-direction bounds for the bf16 run)."""
     from transformers import CLIPConfig, CLIPModel
 
     gcfg, mcfg = O.GPT2Cfg(), O.MapperCfg()
@@ -463,7 +463,8 @@ def golden_bench128(workdir):
     out["train_losses"] = np.array(losses)
     for k, v in model.mapping_network.state_dict().items():
         out["trained_ck." + k] = checksum(v)
-        out["trained_sample." + k] = v.detach().numpy().reshape(-1)[::997].copy()
+        a = v.detach().numpy().reshape(-1)
+        out["trained_sample." + k] = a.copy() if a.size <= 20000 else a[::997].copy()
     np.savez_compressed(os.path.join(OUT, "bench128.npz"), **out)
     print("bench128 loss", out["loss"], "train", losses)
 
