@@ -323,7 +323,7 @@ class CaptionTrainer:
         graphs = []
         for _, fn in self._segments(zero, self.grad_scale()):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with ops.graph_capture(g):
                 fn()
             graphs.append(g)
         self.seg_graphs[zero] = graphs
@@ -391,7 +391,7 @@ class CaptionTrainer:
         least one eager step so every kernel and attribute has been initialised)."""
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with ops.graph_capture(g):
             self._fwd_bwd(zero, self.grad_scale())
             if with_opt:
                 self._optimizer()
@@ -401,7 +401,7 @@ class CaptionTrainer:
     def _capture_opt(self):
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with ops.graph_capture(g):
             self._optimizer()
         return g
 

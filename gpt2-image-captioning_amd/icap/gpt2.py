@@ -803,7 +803,7 @@ class BeamRunner:
             self.graphs = []
             for c in range(len(self.bounds)):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with ops.graph_capture(g):
                     self._chunk(c)
                 self.graphs.append(g)
         for c, g in enumerate(self.graphs):
@@ -862,7 +862,7 @@ class DecodeRunner:
             self.graphs = []
             for c in range(len(self.bounds)):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with ops.graph_capture(g):
                     self._chunk(c)
                 self.graphs.append(g)
         steps = 0

@@ -7,7 +7,9 @@ arithmetic itself and none falls back to PyTorch or the CPU.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import gc
 from typing import Optional, Tuple
 
 import torch
@@ -44,6 +46,23 @@ def _stream():
 
 def _rows(t: Tensor) -> int:
     return t.shape[0] if t.dim() >= 1 else 1
+
+
+@contextlib.contextmanager
+def graph_capture(g):
+    """torch.cuda.graph(g) with Python's cyclic garbage collector held off for the capture. The decode / beam
+    runners and their cores reference each other, so dropped ones are freed by the collector, and a collection
+    that runs inside a capture destroys their HIP graphs and frees their memory mid-capture, which the runtime
+    does not allow (the process aborts). Collect first, then capture with the collector disabled."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g):
+            yield g
+    finally:
+        if was:
+            gc.enable()
 
 
 class Dropout:
