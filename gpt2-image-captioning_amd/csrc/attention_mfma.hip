@@ -372,32 +372,48 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
   // chunk partials of a row summed across its CPR consecutive lanes (block size and the loop bound are multiples
   // of CPR, so a row's lanes are active together); otherwise one thread per query after it. Fixed order either way.
   constexpr bool FUSED_DELTA = (CPR & (CPR - 1)) == 0 && CPR <= 64;
-  for (int idx = threadIdx.x; idx < Sp * CPR; idx += blockDim.x) {
-    const int r = idx / CPR, c = idx - r * CPR;
-    uint4 q = make_uint4(0, 0, 0, 0), k = q, v = q, d = q, o = q;
-    if (r < S) {
-      const int64_t row = trow(g, b, r);
-      const bf16_t* src = qkv + row * p.ld_qkv + h * HD + 8 * c;
-      q = *reinterpret_cast<const uint4*>(src);
-      k = *reinterpret_cast<const uint4*>(src + g.D);
-      v = *reinterpret_cast<const uint4*>(src + 2 * g.D);
-      d = *reinterpret_cast<const uint4*>(dout + row * p.ld_dout + h * HD + 8 * c);
-      if (FUSED_DELTA) o = *reinterpret_cast<const uint4*>(outp + row * p.ld_out + h * HD + 8 * c);
+  // Staging in batches of SIT rows-chunks per thread: every global load of a batch is issued before the first LDS
+  // store, so the block waits out one memory round trip per batch instead of one per chunk (hd 64, S = 65: one
+  // batch; it was three dependent round trips).
+  constexpr int SIT = HD == 64 ? 4 : 2;
+  const int nidx = Sp * CPR;
+  for (int base = threadIdx.x; base < nidx; base += SIT * blockDim.x) {
+    uint4 qa[SIT], ka[SIT], va[SIT], da[SIT], oa[SIT];
+#pragma unroll
+    for (int it = 0; it < SIT; ++it) {
+      const int idx = base + it * (int)blockDim.x;
+      const int r = idx / CPR, c = idx - r * CPR;
+      qa[it] = ka[it] = va[it] = da[it] = oa[it] = make_uint4(0, 0, 0, 0);
+      if (idx < nidx && r < S) {
+        const int64_t row = trow(g, b, r);
+        const bf16_t* src = qkv + row * p.ld_qkv + h * HD + 8 * c;
+        qa[it] = *reinterpret_cast<const uint4*>(src);
+        ka[it] = *reinterpret_cast<const uint4*>(src + g.D);
+        va[it] = *reinterpret_cast<const uint4*>(src + 2 * g.D);
+        da[it] = *reinterpret_cast<const uint4*>(dout + row * p.ld_dout + h * HD + 8 * c);
+        if (FUSED_DELTA) oa[it] = *reinterpret_cast<const uint4*>(outp + row * p.ld_out + h * HD + 8 * c);
+      }
     }
-    *reinterpret_cast<uint4*>(Qs + r * LDR + 8 * c) = q;
-    *reinterpret_cast<uint4*>(Ks + r * LDR + 8 * c) = k;
-    if (r < g.Sp16) *reinterpret_cast<uint4*>(Vs + r * LDR + 8 * c) = v;
-    *reinterpret_cast<uint4*>(dOs + r * LDR + 8 * c) = d;
-    if constexpr (FUSED_DELTA) {
-      const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, ow[4] = {o.x, o.y, o.z, o.w};
-      float part = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        part += __uint_as_float(dw[e] << 16) * __uint_as_float(ow[e] << 16) +
-                __uint_as_float(dw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+    for (int it = 0; it < SIT; ++it) {
+      const int idx = base + it * (int)blockDim.x;
+      if (idx >= nidx) break;  // uniform over a row's CPR lanes (nidx and blockDim are multiples of CPR)
+      const int r = idx / CPR, c = idx - r * CPR;
+      *reinterpret_cast<uint4*>(Qs + r * LDR + 8 * c) = qa[it];
+      *reinterpret_cast<uint4*>(Ks + r * LDR + 8 * c) = ka[it];
+      if (r < g.Sp16) *reinterpret_cast<uint4*>(Vs + r * LDR + 8 * c) = va[it];
+      *reinterpret_cast<uint4*>(dOs + r * LDR + 8 * c) = da[it];
+      if constexpr (FUSED_DELTA) {
+        const uint32_t dw[4] = {da[it].x, da[it].y, da[it].z, da[it].w}, ow[4] = {oa[it].x, oa[it].y, oa[it].z, oa[it].w};
+        float part = 0.f;
 #pragma unroll
-      for (int off = 1; off < CPR; off <<= 1) part += __shfl_xor(part, off, 64);
-      if (c == 0 && r < S) delta_s[r] = part;
+        for (int e = 0; e < 4; ++e)
+          part += __uint_as_float(dw[e] << 16) * __uint_as_float(ow[e] << 16) +
+                  __uint_as_float(dw[e] & 0xffff0000u) * __uint_as_float(ow[e] & 0xffff0000u);
+#pragma unroll
+        for (int off = 1; off < CPR; off <<= 1) part += __shfl_xor(part, off, 64);
+        if (c == 0 && r < S) delta_s[r] = part;
+      }
     }
   }
   if constexpr (!FUSED_DELTA) {

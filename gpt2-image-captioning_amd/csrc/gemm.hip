@@ -69,7 +69,11 @@ __device__ __forceinline__ uint4 kout_frag(const char* img, int r0, int c0, int 
 // columns, 256-byte LDS rows in the T10 (b) XOR image (cdna_hip_programming.md T10), written by LDS-DMA with the
 // swizzle on the source address; fragments come from ds_read_b64_tr_b16 pairs (k order {4g..4g+3, 16+4g..},
 // the same on both operands, so the contraction is unchanged). bf16 inputs, 128 x 128 tiles only.
-template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false>
+// ACT: false for launches with no activation (act == dact == NONE: most of the step's products): the epilogue's
+// activation code is then not compiled into the kernel at all. Measured (profiles/r03_k768_counters.txt): with it
+// present, the plain 8320 x 2304 x 768 product ran 53.7 vs 45.0 us — the same memory instructions, +7 % VALU and
+// +22 % SQ_WAIT_ANY (the larger function scheduled its main loop worse), SQ_WAIT_INST_ANY +1 % (not instruction fetch).
+template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, bool ACT = true>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
                                                                   int nk_split, uint32_t drop_thresh, float inv_keep) {
   static_assert(!KOUT || (sizeof(TI) == 2 && 16 * WM * TM == 128 && 16 * WN * TN == 128),
@@ -349,7 +353,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   };
   if constexpr (std::is_same<TC, bf16_t>::value) {
     if (splits == 1) {
-      if (p.dact != ICAP_ACT_NONE) {
+      if (ACT && p.dact != ICAP_ACT_NONE) {
         esrc = reinterpret_cast<const bf16_t*>(p.dact_src);
         eld = p.ld_dact;
       } else if (p.resid) {
@@ -387,7 +391,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
           if (col + 4 * q < N)
             *reinterpret_cast<float4*>(slab + row * N + col + 4 * q) = *reinterpret_cast<const float4*>(x + 4 * q);
       } else {
-        epiw<TC, EW>(p, row, col, x, biasw, fullw, seed, drop_thresh, inv_keep, pq);
+        epiw<TC, EW, ACT>(p, row, col, x, biasw, fullw, seed, drop_thresh, inv_keep, pq);
       }
     }
   };
@@ -829,6 +833,7 @@ struct GemmPlan {
   int sku = 3;           // skinny: k-steps in flight per wave
   int variant = 0;       // tile kernel (see ICAP_GEMM_LAUNCH)
   int splits = 1, nk_split = 0, tiles_n = 0;
+  bool act = true;       // tile kernels: the instantiation with the activation epilogue compiled in
   dim3 grid, block;
   uint32_t thr = 0;
   float inv_keep = 1.f;
@@ -949,21 +954,22 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   }
   if (p.trans_ab) pl.variant = nk_split > 16 ? 14 : 15;  // K-outer forms of variants 0 / 4
   pl.tiles_n = (int)tiles_n;
+  pl.act = splits == 1 && (p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE);
   pl.block = dim3(GNT);
   pl.grid = dim3((unsigned)(tiles * splits));
   return ICAP_OK;
 }
 
-// "TI, TC, template ints" of each tile variant (keep in sync with the launch switch below)
+// "TI, TC, template ints" of each tile variant (keep in sync with the launch switch below); %%s = ACT
 static const char* variant_kernel(int v) {
   switch (v) {
-    case 0: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, false>";
-    case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, false>";
-    case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4, false>";
-    case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2, false>";
-    case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2, false>";
-    case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true>";
-    default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true>";
+    case 0: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, false, %s>";
+    case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, false, %s>";
+    case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4, false, %s>";
+    case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2, false, %s>";
+    case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2, false, %s>";
+    case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true, %s>";
+    default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %s>";
   }
 }
 
@@ -982,7 +988,7 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
   if (pl.skinny) snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2, %d>", pl.nt, pl.sku);
   else snprintf(fmt, sizeof fmt, "%s", variant_kernel(pl.variant));
   char inner[128];
-  snprintf(inner, sizeof inner, fmt, ti, tc);
+  snprintf(inner, sizeof inner, fmt, ti, tc, pl.act ? "true" : "false");
   snprintf(buf, sizeof buf, "icap::%s", inner);
   return buf;
 }
@@ -1037,42 +1043,48 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const dim3 grid = pl.grid, block = pl.block;
   const int sp = pl.splits, nks = pl.nk_split, tn = pl.tiles_n;
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
-#define ICAP_GEMM_LAUNCH(TI, TC)                                                                               \
-  switch (pl.variant) {                                                                                        \
-    case 0: hipLaunchKernelGGL((gemm_kernel<TI, TC, 2, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    case 4: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 3, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
-    default: hipLaunchKernelGGL((gemm_kernel<TI, TC, 1, 4, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); break; \
+#define ICAP_GK(TI, TC, NST, MINB, TM_, TN_, KOUT)                                                              \
+  do {                                                                                                       \
+    if (pl.act) hipLaunchKernelGGL((gemm_kernel<TI, TC, NST, MINB, 2, 2, TM_, TN_, KOUT, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
+    else hipLaunchKernelGGL((gemm_kernel<TI, TC, NST, MINB, 2, 2, TM_, TN_, KOUT, false>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
+  } while (0)
+#define ICAP_GEMM_LAUNCH(TI, TC)                                    \
+  switch (pl.variant) {                                             \
+    case 0: ICAP_GK(TI, TC, 2, 2, 4, 4, false); break;              \
+    case 4: ICAP_GK(TI, TC, 1, 3, 4, 4, false); break;              \
+    default: ICAP_GK(TI, TC, 1, 4, 4, 4, false); break;             \
   }
   if (pl.variant == 14 || pl.variant == 15) {  // K-outer operands (bf16 inputs only)
     if (p.c_dtype == ICAP_BF16) {
-      if (pl.variant == 14) hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 2, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 1, 3, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      if (pl.variant == 14) ICAP_GK(bf16_t, bf16_t, 2, 2, 4, 4, true);
+      else ICAP_GK(bf16_t, bf16_t, 1, 3, 4, 4, true);
     } else {
-      if (pl.variant == 14) hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 2, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 1, 3, 2, 2, 4, 4, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      if (pl.variant == 14) ICAP_GK(bf16_t, float, 2, 2, 4, 4, true);
+      else ICAP_GK(bf16_t, float, 1, 3, 4, 4, true);
     }
   } else if (pl.variant == 12 || pl.variant == 13) {  // 128 x 64 (bf16 inputs only)
     if (p.c_dtype == ICAP_BF16) {
-      if (pl.variant == 12) hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 2, 3, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, 1, 4, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      if (pl.variant == 12) ICAP_GK(bf16_t, bf16_t, 2, 3, 4, 2, false);
+      else ICAP_GK(bf16_t, bf16_t, 1, 4, 4, 2, false);
     } else {
-      if (pl.variant == 12) hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 2, 3, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm_kernel<bf16_t, float, 1, 4, 2, 2, 4, 2>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      if (pl.variant == 12) ICAP_GK(bf16_t, float, 2, 3, 4, 2, false);
+      else ICAP_GK(bf16_t, float, 1, 4, 4, 2, false);
     }
   } else if (p.in_dtype == ICAP_BF16) {
     if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(bf16_t, bf16_t) } else { ICAP_GEMM_LAUNCH(bf16_t, float) }
   } else if (p.in_dtype == ICAP_FP8_MX) {  // variants 0 / 4 only (gemm_plan)
     if (p.c_dtype == ICAP_BF16) {
-      if (pl.variant == 0) hipLaunchKernelGGL((gemm_kernel<fp8_t, bf16_t, 2, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm_kernel<fp8_t, bf16_t, 1, 3, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      if (pl.variant == 0) ICAP_GK(fp8_t, bf16_t, 2, 2, 4, 4, false);
+      else ICAP_GK(fp8_t, bf16_t, 1, 3, 4, 4, false);
     } else {
-      if (pl.variant == 0) hipLaunchKernelGGL((gemm_kernel<fp8_t, float, 2, 2, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
-      else hipLaunchKernelGGL((gemm_kernel<fp8_t, float, 1, 3, 2, 2, 4, 4>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep);
+      if (pl.variant == 0) ICAP_GK(fp8_t, float, 2, 2, 4, 4, false);
+      else ICAP_GK(fp8_t, float, 1, 3, 4, 4, false);
     }
   } else {
     if (p.c_dtype == ICAP_BF16) { ICAP_GEMM_LAUNCH(float, bf16_t) } else { ICAP_GEMM_LAUNCH(float, float) }
   }
 #undef ICAP_GEMM_LAUNCH
+#undef ICAP_GK
   if (sp > 1) {
     if (p.c_dtype == ICAP_BF16)
       hipLaunchKernelGGL((gemm_splitk_reduce<bf16_t>), rgrid, dim3(256), 0, s, p, sp, thr, inv_keep);

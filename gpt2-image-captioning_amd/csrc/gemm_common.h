@@ -192,13 +192,15 @@ __device__ __forceinline__ void epi_bwd_math(const icap_gemm_args& p, float x[W]
       for (int e = 0; e < W; ++e) x[e] = y[e] * act_bwd(ICAP_ACT_NONE, a[e]);
   }
 }
-// forward form, first half: x = act(alpha * acc + bias); a = the aux value (pre-activation, or tanh output)
-template <int W>
+// forward form, first half: x = act(alpha * acc + bias); a = the aux value (pre-activation, or tanh output).
+// ACT = false: an instantiation for launches without an activation (the host guarantees act == dact == NONE), so
+// none of the activation code is compiled into that kernel (see gemm_kernel's ACT parameter).
+template <int W, bool ACT = true>
 __device__ __forceinline__ void epi_fwd_act(const icap_gemm_args& p, float x[W], const float biasw[W], float a[W]) {
 #pragma clang fp contract(off)
 #pragma unroll
   for (int e = 0; e < W; ++e) x[e] = __builtin_fmaf(p.alpha, x[e], biasw[e]);
-  if (__builtin_expect(p.act == ICAP_ACT_NONE, 1)) {  // no activation: keep this path short and first
+  if (!ACT || __builtin_expect(p.act == ICAP_ACT_NONE, 1)) {  // no activation: keep this path short and first
     if (p.aux) {
 #pragma unroll
       for (int e = 0; e < W; ++e) a[e] = x[e];
@@ -244,7 +246,7 @@ __device__ __forceinline__ void epi_fwd_tail(float x[W], const float r[W], bool 
 // W-wide vector access is used per operand where its leading dimension and base pointer are W-aligned.
 // pre: optional prefetched raw bf16 vector of the epilogue's input operand at (row, col..) — dact_src in the
 // backward form, resid in the forward form — loaded by the caller ahead of the LDS staging (fullw rows only).
-template <typename TC, int W>
+template <typename TC, int W, bool ACT = true>
 __device__ __forceinline__ void epiw(const icap_gemm_args& p, int64_t row, int64_t col, float x[W],
                                      const float biasw[W], bool fullw, uint64_t seed, uint32_t drop_thresh,
                                      float inv_keep, const typename rawbf<W>::T* pre = nullptr) {
@@ -260,13 +262,13 @@ __device__ __forceinline__ void epiw(const icap_gemm_args& p, int64_t row, int64
   constexpr uintptr_t VA = (W * sizeof(TC) > 16 ? 16 : W * sizeof(TC)) - 1;
   auto vok = [&](int64_t ld, const void* ptr) { return (ld % W) == 0 && (reinterpret_cast<uintptr_t>(ptr) & VA) == 0; };
   fullw = fullw && vok(p.ldc, C);
-  if (p.dact != ICAP_ACT_NONE) {
+  if (ACT && p.dact != ICAP_ACT_NONE) {
     if (pre) unpack_bf16(*pre, a);
     else if (fullw && vok(p.ld_dact, dsrc)) vecio<TC, W>::ld(dsrc + row * p.ld_dact + col, a);
     else for (int e = 0; e < W; ++e) a[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
     epi_bwd_math<W>(p, x, a, seed, didx, drop_thresh, inv_keep);
   } else {
-    epi_fwd_act<W>(p, x, biasw, a);
+    epi_fwd_act<W, ACT>(p, x, biasw, a);
     if (aux) {
       if (fullw && vok(p.ldaux, aux)) vecio<TC, W>::st(aux + row * p.ldaux + col, a);
       else for (int e = 0; e < W; ++e) if (col + e < N) io<TC>::st(aux + row * p.ldaux + col + e, a[e]);

@@ -148,8 +148,9 @@ class IcapError(RuntimeError):
     pass
 
 
-def load(path: str = LIB_PATH) -> C.CDLL:
-    """Load (once) and bind the library; raises if it is missing."""
+def load(path: str = LIB_PATH, strict: bool = True) -> C.CDLL:
+    """Load (once) and bind the library; raises if it is missing. strict=False (A/B measurement tools loading an
+    older build) skips entry points the build does not export."""
     global _lib
     if _lib is not None:
         return _lib
@@ -160,6 +161,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         )
     lib = C.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if not strict and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -30,7 +30,7 @@ def timeit(fn, reps=20):
 
 def main():
     if os.environ.get("ICAP_LIB"):
-        L.load(os.environ["ICAP_LIB"])
+        L.load(os.environ["ICAP_LIB"], strict=False)
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(0)
     for (B, S, H, hd, causal) in [(128, 65, 12, 64, True), (128, 25, 8, 96, False)]:

@@ -46,7 +46,7 @@ SHAPES = [
 
 def main():
     if os.environ.get("ICAP_LIB"):  # A/B against another build of the library
-        L.load(os.environ["ICAP_LIB"])
+        L.load(os.environ["ICAP_LIB"], strict=False)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     reps = int(os.environ.get("REPS", "20"))
