@@ -67,7 +67,15 @@ class GemmTimer:
         return agg
 
 
-def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16, fp8=False):
+def live_rows(labels, P):
+    """Host copy of the packed token-row count icap_caption_pack computes on the device (roofline pricing and the
+    GEMM kernel choice): per caption max(P, P + last caption index with a target)."""
+    from icap.engine import live_rows as lr
+
+    return lr(labels, P)
+
+
+def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16, fp8=False, pack=None):
     """config "small": BASELINE configs[1] (GPT-2 small + CLIP ViT-B/32); "medium": configs[3] (GPT-2 medium +
     CLIP ViT-L/14 encoder on the device, mapper at gpt_dim 1024 / CLIP-L embed 768)."""
     from types import SimpleNamespace
@@ -85,7 +93,7 @@ def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16, fp8=False)
                                      compute_dtype=dtype, gpt_fp8=fp8).to(dev)
         tower = DINOv3ImageTower.random_init(seed=0).to(dev)
         trainer = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10 ** 6, clip_model=tower,
-                                 dropout=dropout, seed=1234)
+                                 dropout=dropout, seed=1234, pack_rows=pack)
         return model, tower, trainer
     if config == "medium":
         gpt = GPT2LMHeadModel.random_init(GPT2Config.medium(), seed=0)
@@ -99,7 +107,7 @@ def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16, fp8=False)
                                  compute_dtype=dtype, gpt_fp8=fp8).to(dev)
     tower = CLIPVisionTower.random_init(tower_cfg, seed=0).to(dev)
     trainer = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10 ** 6, clip_model=tower, dropout=dropout,
-                             seed=1234)
+                             seed=1234, pack_rows=pack)
     return model, tower, trainer
 
 
@@ -454,6 +462,22 @@ def train_rate(trainer, B, steps, warmup, use_graph, world, dev):
             "all_fl": sum(v[1] for v in agg.values()), "eager_ms": eager_ms}
 
 
+def padded_rate(config, B, dev, world, fp8=False, steps=10):
+    """The same step with the packed token rows off (ICAP_PACK=0: every block runs on all B x 65 rows of the padded
+    grid, as the reference computes them): images/s and the dominant GEMM's roofline fraction, for comparison."""
+    model, tower, tr = build(B, dev, config=config, fp8=fp8, pack=False)
+    ids, mask, labels, px = synthetic_batch(B, 1, dev)
+    tr.load_batch(ids, mask, labels, pixels=px)
+    tr.gws.head_rows_hint = int((labels != -100).sum().item())
+    r = train_rate(tr, B, steps, 3, True, world, dev)
+    del model, tower, tr
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return {"images_per_s": round(r["images_per_s"], 1), "ms_per_step": round(r["ms_per_step"], 3),
+            "token_rows_per_step": B * 65, "dominant_kernel": r["dom"], "dominant_frac": round(r["frac"], 4),
+            "all_gemm_ms_per_step": round(r["gemm_ms"], 3)}
+
+
 def batch_sweep(config, batches, dev, world, fp8=False):
     """SURVEY.md §8(d) perf batch sweep: the same train step at other per-GPU batches (weak-scaling B is a free
     choice; the reference's is config.yml:32 = 128): images/s and the dominant GEMM's roofline fraction."""
@@ -463,6 +487,7 @@ def batch_sweep(config, batches, dev, world, fp8=False):
         ids, mask, labels, px = synthetic_batch(Bs, 11, dev)
         tr.load_batch(ids, mask, labels, pixels=px)
         tr.gws.head_rows_hint = int((labels != -100).sum().item())
+        tr.gws.live_rows_hint = live_rows(labels, tr.P)
         r = train_rate(tr, Bs, 5, 2, True, world, dev)
         out.append({"batch_per_gpu": Bs, "images_per_s": round(r["images_per_s"], 1),
                     "ms_per_step": round(r["ms_per_step"], 3), "dominant_kernel": r["dom"],
@@ -522,6 +547,9 @@ def main():
     # LM-head target rows of this batch (the device holds the count; the host copy only prices the roofline)
     head_rows = int((labels != -100).sum().item())
     trainer.gws.head_rows_hint = head_rows
+    packed = bool(trainer.gws.pack)
+    token_rows = live_rows(labels, trainer.P) if packed else B * trainer.gws.S
+    trainer.gws.live_rows_hint = token_rows if packed else None
     use_graph = not args.no_graph
     # timed region + the kernel roofline pass (every GEMM launch of one eager step, timed with HIP events)
     r = train_rate(trainer, B, args.steps, args.warmup, use_graph, world, dev)
@@ -549,9 +577,11 @@ def main():
     parity = parity_mode_rate(B, dev) if (not args.no_decode and args.config == "small" and world == 1) else None
     sweep_b = [int(x) for x in args.sweep.split(",") if x] if args.sweep is not None else \
         ([256, 512] if args.config == "small" and not args.no_decode and world == 1 else [])
-    if sweep_b:
+    want_padded = packed and not args.no_decode and world == 1
+    if sweep_b or want_padded:
         del model, tower, trainer
         torch.cuda.empty_cache()
+    padded = padded_rate(args.config, B, dev, world, args.fp8) if want_padded else None
     sweep = batch_sweep(args.config, sweep_b, dev, world, args.fp8) if sweep_b else None
 
     if rank == 0:
@@ -562,6 +592,11 @@ def main():
             "dtype": "fp8 (MX e4m3, GPT-2 products) + bf16" if args.fp8 else "bf16",
             "data": "synthetic (seeded COCO-shaped captions: 13 tokens + EOS, padded to 50; randn 224x224 pixels); "
                     "deterministic random-init weights",
+            "packed_rows": ({"token_rows_per_step": token_rows, "padded_rows": B * 65,
+                             "note": "GPT-2 blocks run on each caption's live rows (prefix + positions up to its last "
+                                     "loss target, icap_caption_pack); the dead tail of the padded grid feeds no loss "
+                                     "term under the causal mask (loss / gradients unchanged: tests/test_pack_gpu.py)",
+                             "padded_step": padded} if packed else None),
             "config": {"workload": ("train step: CLIP ViT-B/32 fwd (frozen) on 224x224 pixels -> transformer mapper "
                                     "(8 layers, prefix 15, trained) -> GPT-2 small (frozen) fwd + dX bwd, LM head on "
                                     "the target rows + CE, dropout 0.1, clip_grad_norm 1.0 + AdamW + linear LR")

@@ -14,12 +14,29 @@
 
 namespace icap {
 
+// S: tokens of this block's sequence (seq_len[b] for packed sequences); Sst: the launch's S (lse / dropout
+// numbering); base / kmb: row of token 0 and its key-mask index (attn_localize)
 struct AttnGeom {
   int S, H, hd, D;
   int64_t rsb, rss;  // row strides (in rows) for batch and sequence
+  int Sst;
+  int64_t base, kmb;
 };
 
-__device__ __forceinline__ int64_t tok_row(const AttnGeom& g, int b, int s) { return (int64_t)b * g.rsb + (int64_t)s * g.rss; }
+__device__ __forceinline__ int64_t tok_row(const AttnGeom& g, int b, int s) { return g.base + (int64_t)s * g.rss; }
+
+__device__ __forceinline__ bool attn_localize(AttnGeom& g, const icap_attn_args& p, int b) {
+  if (p.seq_len) {
+    const int n = p.seq_len[b];
+    g.S = n < g.Sst ? n : g.Sst;
+    g.base = p.seq_off[b];
+    g.kmb = p.seq_off[b];
+  } else {
+    g.base = (int64_t)b * g.rsb;
+    g.kmb = (int64_t)b * g.Sst;
+  }
+  return g.S > 0;
+}
 
 template <typename T>
 __device__ __forceinline__ void stage_head(const T* src, int64_t ld, int col0, const AttnGeom& g, int b,
@@ -34,9 +51,9 @@ __device__ __forceinline__ void stage_head(const T* src, int64_t ld, int col0, c
   }
 }
 
-__device__ __forceinline__ bool allowed(int causal, const int32_t* key_mask, int b, int S, int i, int j) {
+__device__ __forceinline__ bool allowed(int causal, const int32_t* key_mask, int64_t kmb, int i, int j) {
   if (causal && j > i) return false;
-  if (key_mask && key_mask[(int64_t)b * S + j] == 0) return false;
+  if (key_mask && key_mask[kmb + j] == 0) return false;
   return true;
 }
 
@@ -48,8 +65,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeo
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int bh = blockIdx.x;
   const int b = bh / g.H, h = bh - b * g.H;
-  const int S = g.S, hd = g.hd, ldp = hd + 1;
+  if (!attn_localize(g, p, b)) return;
+  const int S = g.S, SS = g.Sst, hd = g.hd, ldp = hd + 1;
   const int q0 = blockIdx.y * QT, nq = min(QT, S - q0);
+  if (nq <= 0) return;
   float* Ks = sm;
   float* Vs = Ks + S * ldp;
   float* Qs = Vs + S * ldp;
@@ -72,7 +91,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeo
   for (int idx = threadIdx.x; idx < nq * S; idx += blockDim.x) {
     const int il = idx / S, j = idx - il * S;
     float s = -INFINITY;
-    if (allowed(p.causal, p.key_mask, b, S, q0 + il, j)) {
+    if (allowed(p.causal, p.key_mask, g.kmb, q0 + il, j)) {
       const float* q = Qs + il * ldp;
       const float* k = Ks + j * ldp;
       float a0 = 0.f, a1 = 0.f;
@@ -87,7 +106,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeo
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  const uint64_t drop_base = p.offset + (uint64_t)bh * S * S;
+  const uint64_t drop_base = p.offset + (uint64_t)bh * SS * SS;
   const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
   for (int il = wv; il < nq; il += nwv) {
     const int i = q0 + il;
@@ -101,10 +120,10 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(icap_attn_args p, AttnGeo
     const float inv = l > 0.f ? 1.f / l : 0.f;
     for (int j = lane; j < S; j += 64) {
       float pv = (m == -INFINITY) ? 0.f : __expf(row[j] - m) * inv;
-      if (thr) pv *= drop_scale(seed, drop_base + (uint64_t)i * S + j, thr, inv_keep);
+      if (thr) pv *= drop_scale(seed, drop_base + (uint64_t)i * SS + j, thr, inv_keep);
       row[j] = pv;
     }
-    if (lane == 0 && p.lse) p.lse[(int64_t)bh * S + i] = (l > 0.f) ? m + logf(l) : -INFINITY;
+    if (lane == 0 && p.lse) p.lse[(int64_t)bh * SS + i] = (l > 0.f) ? m + logf(l) : -INFINITY;
   }
   __syncthreads();
 
@@ -128,7 +147,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(icap_attn_args p, AttnGeo
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int bh = blockIdx.x;
   const int b = bh / g.H, h = bh - b * g.H;
-  const int S = g.S, hd = g.hd, ldp = hd + 1;
+  if (!attn_localize(g, p, b)) return;
+  const int S = g.S, SS = g.Sst, hd = g.hd, ldp = hd + 1;
   float* Qs = sm;
   float* Ks = Qs + S * ldp;
   float* Vs = Ks + S * ldp;
@@ -145,8 +165,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(icap_attn_args p, AttnGeo
   for (int idx = threadIdx.x; idx < S * S; idx += blockDim.x) {
     const int i = idx / S, j = idx - i * S;
     float pv = 0.f, dp = 0.f;
-    const float lse = p.lse[(int64_t)bh * S + i];
-    if (allowed(p.causal, p.key_mask, b, S, i, j) && lse != -INFINITY) {
+    const float lse = p.lse[(int64_t)bh * SS + i];
+    if (allowed(p.causal, p.key_mask, g.kmb, i, j) && lse != -INFINITY) {
       const float* q = Qs + i * ldp;
       const float* k = Ks + j * ldp;
       const float* o = dOs + i * ldp;
@@ -167,7 +187,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(icap_attn_args p, AttnGeo
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  const uint64_t drop_base = p.offset + (uint64_t)bh * S * S;
+  const uint64_t drop_base = p.offset + (uint64_t)bh * SS * SS;
   const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
   for (int i = wv; i < S; i += nwv) {
     float* prow = P + i * S;
@@ -175,7 +195,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(icap_attn_args p, AttnGeo
     float delta = 0.f;
     for (int j = lane; j < S; j += 64) {
       float dp = drow[j];
-      if (thr) dp *= drop_scale(seed, drop_base + (uint64_t)i * S + j, thr, inv_keep);
+      if (thr) dp *= drop_scale(seed, drop_base + (uint64_t)i * SS + j, thr, inv_keep);
       drow[j] = dp;
       delta += prow[j] * dp;
     }
@@ -183,7 +203,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(icap_attn_args p, AttnGeo
     for (int j = lane; j < S; j += 64) {
       const float pv = prow[j];
       drow[j] = pv * (drow[j] - delta);
-      if (thr) prow[j] = pv * drop_scale(seed, drop_base + (uint64_t)i * S + j, thr, inv_keep);
+      if (thr) prow[j] = pv * drop_scale(seed, drop_base + (uint64_t)i * SS + j, thr, inv_keep);
     }
   }
   __syncthreads();
@@ -388,6 +408,8 @@ static int check_attn(const icap_attn_args* a, bool bwd) {
   ICAP_REQUIRE(a->qkv && (bwd ? (a->dout && a->dqkv && a->lse) : (a->out != nullptr)), "icap_attention: null pointer");
   ICAP_REQUIRE(a->ld_qkv % 4 == 0, "icap_attention: ld_qkv must be a multiple of 4");
   ICAP_REQUIRE(a->drop_p >= 0.f && a->drop_p < 1.f, "icap_attention: drop_p out of range");
+  ICAP_REQUIRE((a->seq_off == nullptr) == (a->seq_len == nullptr), "icap_attention: seq_off and seq_len go together");
+  ICAP_REQUIRE(a->seq_off == nullptr || a->row_stride_s == 1, "icap_attention: packed sequences need row_stride_s 1");
 
   return ICAP_OK;
 }
@@ -400,7 +422,7 @@ extern "C" int icap_attention_fwd(const icap_attn_args* a, void* stream) {
   int rc = check_attn(a, false);
   if (rc) return rc;
   if (a->B == 0) return ICAP_OK;
-  AttnGeom g{a->S, a->H, a->hd, a->H * a->hd, a->row_stride_b, a->row_stride_s};
+  AttnGeom g{a->S, a->H, a->hd, a->H * a->hd, a->row_stride_b, a->row_stride_s, a->S, 0, 0};
   const uint32_t thr = a->drop_p > 0.f ? drop_threshold(a->drop_p) : 0u;
   const float inv_keep = a->drop_p > 0.f ? 1.f / (1.f - a->drop_p) : 1.f;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -423,7 +445,7 @@ extern "C" int icap_attention_bwd(const icap_attn_args* a, void* stream) {
   int rc = check_attn(a, true);
   if (rc) return rc;
   if (a->B == 0) return ICAP_OK;
-  AttnGeom g{a->S, a->H, a->hd, a->H * a->hd, a->row_stride_b, a->row_stride_s};
+  AttnGeom g{a->S, a->H, a->hd, a->H * a->hd, a->row_stride_b, a->row_stride_s, a->S, 0, 0};
   const uint32_t thr = a->drop_p > 0.f ? drop_threshold(a->drop_p) : 0u;
   const float inv_keep = a->drop_p > 0.f ? 1.f / (1.f - a->drop_p) : 1.f;
   const size_t lds = bwd_lds(a->S, a->hd);

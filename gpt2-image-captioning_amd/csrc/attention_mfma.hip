@@ -25,12 +25,33 @@ namespace amfma {
 
 constexpr int MAXKT = 8;  // key tiles of 16 -> S <= 128
 
+// S: tokens of this block's sequence (the launch's S, or seq_len[b] for packed sequences); Sst: the launch's S,
+// the stride of the lse [B, H, S] and dropout [B, H, S, S] numbering; base / kmb: row of token 0 and its key-mask
+// index (localize)
 struct Geo {
   int S, H, hd, D, Sp16, Sp32, ldT;
   int64_t rsb, rss;
+  int Sst;
+  int64_t base, kmb;
 };
 
-__device__ __forceinline__ int64_t trow(const Geo& g, int b, int s) { return (int64_t)b * g.rsb + (int64_t)s * g.rss; }
+__device__ __forceinline__ int64_t trow(const Geo& g, int b, int s) { return g.base + (int64_t)s * g.rss; }
+
+// per-block sequence geometry (icap_attn_args.seq_off / seq_len: packed rows); false: empty sequence
+__device__ __forceinline__ bool localize(Geo& g, const icap_attn_args& p, int b) {
+  if (p.seq_len) {
+    const int n = p.seq_len[b];
+    g.S = n < g.Sst ? n : g.Sst;
+    g.base = p.seq_off[b];
+    g.kmb = p.seq_off[b];
+    g.Sp16 = (g.S + 15) & ~15;
+    g.Sp32 = (g.S + 31) & ~31;
+  } else {
+    g.base = (int64_t)b * g.rsb;
+    g.kmb = (int64_t)b * g.Sst;
+  }
+  return g.S > 0;
+}
 
 __device__ __forceinline__ f32x4_t mfma(const uint4& a, const uint4& b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -70,7 +91,7 @@ __device__ __forceinline__ void stage_T(bf16_t* dst, int ld, const bf16_t* src, 
 __device__ __forceinline__ bool key_ok(int causal, const int32_t* km, const Geo& g, int b, int q, int key) {
   if (key >= g.S) return false;
   if (causal && key > q) return false;
-  if (km && km[(int64_t)b * g.S + key] == 0) return false;
+  if (km && km[g.kmb + key] == 0) return false;
   return true;
 }
 
@@ -97,6 +118,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(icap_attn_args p, Geo g, uint3
   constexpr int NDT = HD / 16;   // d tiles of O
   const int bh = blockIdx.x;
   const int b = bh / g.H, h = bh - b * g.H;
+  if (!localize(g, p, b)) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ldT = g.ldT;
   bf16_t* Vt = sm;                                   // [HD][ldT]
@@ -106,7 +128,7 @@ __global__ __launch_bounds__(256) void fwd_kernel(icap_attn_args p, Geo g, uint3
   for (int i = lane; i < 16 * ldT; i += 64) Pw[i] = 0;
   __syncthreads();
   const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
-  const uint64_t dbase = p.offset + (uint64_t)bh * g.S * g.S;
+  const uint64_t dbase = p.offset + (uint64_t)bh * g.Sst * g.Sst;
   const int nkt = g.Sp16 >> 4, nqt = g.Sp16 >> 4, nks2 = g.Sp32 >> 5;
   const int fr = lane & 15, fg = lane >> 4;
   bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
@@ -150,13 +172,13 @@ __global__ __launch_bounds__(256) void fwd_kernel(icap_attn_args p, Geo g, uint3
       }
       l = row16_sum(l);
       const float inv = l > 0.f ? 1.f / l : 0.f;
-      if (fr == 0 && q < g.S && p.lse) p.lse[(int64_t)bh * g.S + q] = l > 0.f ? m + logf(l) : -INFINITY;
+      if (fr == 0 && q < g.S && p.lse) p.lse[(int64_t)bh * g.Sst + q] = l > 0.f ? m + logf(l) : -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < MAXKT; ++kt) {
         if (kt < nkt) {
           const int key = kt * 16 + fr;
           float pv = s[kt][v] * inv;
-          if (thr && q < g.S && key < g.S) pv *= drop_scale(seed, dbase + (uint64_t)q * g.S + key, thr, inv_keep);
+          if (thr && q < g.S && key < g.S) pv *= drop_scale(seed, dbase + (uint64_t)q * g.Sst + key, thr, inv_keep);
           Pw[(fg * 4 + v) * ldT + key] = f2bf(pv);
         }
       }
@@ -184,6 +206,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(icap_attn_args p, Geo g, uint3
   constexpr int NDT = HD / 16;
   const int bh = blockIdx.x;
   const int b = bh / g.H, h = bh - b * g.H;
+  if (!localize(g, p, b)) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int ldT = g.ldT;
   bf16_t* Kt = sm;                        // [HD][ldT]   K^T  (dQ B operand)
@@ -205,7 +228,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(icap_attn_args p, Geo g, uint3
   }
   __syncthreads();
   const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
-  const uint64_t dbase = p.offset + (uint64_t)bh * g.S * g.S;
+  const uint64_t dbase = p.offset + (uint64_t)bh * g.Sst * g.Sst;
   const int nkt = g.Sp16 >> 4, nqt = g.Sp16 >> 4, nks2 = g.Sp32 >> 5;
   const int fr = lane & 15, fg = lane >> 4;
   bf16_t* dqkv = reinterpret_cast<bf16_t*>(p.dqkv);
@@ -232,7 +255,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(icap_attn_args p, Geo g, uint3
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int q = qt * 16 + fg * 4 + v;
-      const float lse = q < g.S ? p.lse[(int64_t)bh * g.S + q] : -INFINITY;
+      const float lse = q < g.S ? p.lse[(int64_t)bh * g.Sst + q] : -INFINITY;
       float delta = 0.f;
 #pragma unroll
       for (int kt = 0; kt < MAXKT; ++kt) {
@@ -244,7 +267,7 @@ __global__ __launch_bounds__(256) void bwd_kernel(icap_attn_args p, Geo g, uint3
           float d = dp[kt][v];
           float pd = pv;
           if (thr && q < g.S && key < g.S) {
-            const float ms = drop_scale(seed, dbase + (uint64_t)q * g.S + key, thr, inv_keep);
+            const float ms = drop_scale(seed, dbase + (uint64_t)q * g.Sst + key, thr, inv_keep);
             d *= ms;
             pd *= ms;
           }
@@ -346,9 +369,10 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
   constexpr int NKS = HD / 32;  // 32-deep k steps over the head dim
   constexpr int NDT = HD / 16;  // 16-wide head-dim tiles of the outputs
   constexpr int CPR = HD / 8;   // 16-byte chunks per row
-  const int Sp = g.Sp32, S = g.S;
   const int bh = blockIdx.x;
   const int b = bh / g.H, h = bh - b * g.H;
+  if (!localize(g, p, b)) return;
+  const int Sp = g.Sp32, S = g.S, SS = g.Sst;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int nt = g.Sp16 >> 4;
@@ -363,9 +387,9 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
   const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
   const bf16_t* outp = reinterpret_cast<const bf16_t*>(p.out);
   for (int r = threadIdx.x; r < Sp; r += blockDim.x) {
-    lse_s[r] = r < S ? p.lse[(int64_t)bh * S + r] : -INFINITY;
+    lse_s[r] = r < S ? p.lse[(int64_t)bh * SS + r] : -INFINITY;
     delta_s[r] = 0.f;
-    kok_s[r] = (r < S && (p.key_mask == nullptr || p.key_mask[(int64_t)b * S + r] != 0)) ? 1 : 0;
+    kok_s[r] = (r < S && (p.key_mask == nullptr || p.key_mask[g.kmb + r] != 0)) ? 1 : 0;
   }
   __syncthreads();
   // CPR a power of two (HD 64 / 128): delta[q] = sum_d dO[q][d] O[q][d] fused into the staging loop, the CPR
@@ -438,7 +462,7 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
   __syncthreads();
   auto kok = [&](int q, int key) { return kok_s[key] && !(p.causal && key > q); };
   const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
-  const uint64_t dbase = p.offset + (uint64_t)bh * S * S;
+  const uint64_t dbase = p.offset + (uint64_t)bh * SS * SS;
   bf16_t* dqkv = reinterpret_cast<bf16_t*>(p.dqkv);
   const int npair = Sp >> 5;
   if (wave < nt) {
@@ -473,7 +497,7 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
           float pv = 0.f;
           if (lse != -INFINITY && kok(q, key)) pv = __expf(sc[v] * p.scale - lse);
           float ms = 1.f;
-          if (thr && q < S && key < S) ms = drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
+          if (thr && q < S && key < S) ms = drop_scale(seed, dbase + (uint64_t)q * SS + key, thr, inv_keep);
           pd[sub * 4 + v] = pv * ms;
           ds[sub * 4 + v] = pv * (dp[v] * ms - delta_s[q]);
         }
@@ -535,7 +559,7 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
           float pv = 0.f;
           if (lse != -INFINITY && kok(q, key)) pv = __expf(st[v] * p.scale - lse);
           float ms = 1.f;
-          if (thr && q < S && key < S) ms = drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
+          if (thr && q < S && key < S) ms = drop_scale(seed, dbase + (uint64_t)q * SS + key, thr, inv_keep);
           ds[sub * 4 + v] = pv * (dpt[v] * ms - de);
         }
       }
@@ -566,9 +590,10 @@ __global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint
   constexpr int NKS = HD / 32;
   constexpr int NDT = HD / 16;
   constexpr int CPR = HD / 8;
-  const int Sp = g.Sp32, S = g.S;
   const int bh = blockIdx.x;
   const int b = bh / g.H, h = bh - b * g.H;
+  if (!localize(g, p, b)) return;
+  const int Sp = g.Sp32, S = g.S, SS = g.Sst;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   bf16_t* Ks = sm;
@@ -587,6 +612,7 @@ __global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint
   }
   __syncthreads();
   const int qt = wave;
+  if (qt * 16 >= S) return;  // (packed sequences shorter than the launch's S; no barrier follows)
   const int q = qt * 16 + fr;
   // Q fragments of this query tile straight from HBM/L2 (B operand: rows = queries)
   uint4 qf[NKS];
@@ -631,9 +657,9 @@ __global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint
   l += __shfl_xor(l, 16, 64);
   l += __shfl_xor(l, 32, 64);
   const float inv = l > 0.f ? 1.f / l : 0.f;
-  if (fg == 0 && q < S && p.lse) p.lse[(int64_t)bh * S + q] = l > 0.f ? m + logf(l) : -INFINITY;
+  if (fg == 0 && q < S && p.lse) p.lse[(int64_t)bh * SS + q] = l > 0.f ? m + logf(l) : -INFINITY;
   const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
-  const uint64_t dbase = p.offset + (uint64_t)bh * S * S;
+  const uint64_t dbase = p.offset + (uint64_t)bh * SS * SS;
   f32x4_t o[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) o[dt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
@@ -647,7 +673,7 @@ __global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint
         for (int v = 0; v < 4; ++v) {
           const int key = (2 * kp + sub) * 16 + 4 * fg + v;
           float x = st[2 * kp + sub][v] * inv;
-          if (thr && q < S && key < S) x *= drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
+          if (thr && q < S && key < S) x *= drop_scale(seed, dbase + (uint64_t)q * SS + key, thr, inv_keep);
           pv[sub * 4 + v] = x;
         }
       uint4 xp;
@@ -676,9 +702,10 @@ __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void fwd3_kernel(icap_attn_a
   constexpr int NKS = HD / 32;
   constexpr int NDT = HD / 16;
   constexpr int CPR = HD / 8;
-  const int Sp = g.Sp32, S = g.S;
   const int bh = blockIdx.x;
   const int b = bh / g.H, h = bh - b * g.H;
+  if (!localize(g, p, b)) return;
+  const int Sp = g.Sp32, S = g.S, SS = g.Sst;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   bf16_t* Ks = sm;
@@ -699,7 +726,7 @@ __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void fwd3_kernel(icap_attn_a
   const int nqt = g.Sp16 >> 4;
   const int nkt = Sp >> 4;  // key tiles incl. the zero rows up to Sp32 (pairs stay whole)
   const uint64_t seed = thr ? eff_seed(p.seed, p.seed_ptr) : 0ull;
-  const uint64_t dbase = p.offset + (uint64_t)bh * S * S;
+  const uint64_t dbase = p.offset + (uint64_t)bh * SS * SS;
   for (int qt = wave; qt < nqt; qt += nw) {
     const int q = qt * 16 + fr;
     uint4 qf[NKS];
@@ -749,7 +776,7 @@ __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void fwd3_kernel(icap_attn_a
               const int key = (c0 + 2 * kp + sub) * 16 + 4 * fg + v;
               float e = (m == -INFINITY) ? 0.f : __expf(st[2 * kp + sub][v] - m);
               l += e;
-              if (thr && q < S && key < S) e *= drop_scale(seed, dbase + (uint64_t)q * S + key, thr, inv_keep);
+              if (thr && q < S && key < S) e *= drop_scale(seed, dbase + (uint64_t)q * SS + key, thr, inv_keep);
               pv[sub * 4 + v] = e;
             }
           uint4 xp;
@@ -762,7 +789,7 @@ __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void fwd3_kernel(icap_attn_a
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     const float inv = l > 0.f ? 1.f / l : 0.f;
-    if (fg == 0 && q < S && p.lse) p.lse[(int64_t)bh * S + q] = l > 0.f ? m + logf(l) : -INFINITY;
+    if (fg == 0 && q < S && p.lse) p.lse[(int64_t)bh * SS + q] = l > 0.f ? m + logf(l) : -INFINITY;
     if (q < S) {
       bf16_t* rowp = reinterpret_cast<bf16_t*>(p.out) + trow(g, b, q) * p.ld_out + h * HD;
 #pragma unroll
@@ -782,6 +809,7 @@ amfma::Geo mfma_geo(const icap_attn_args* a) {
   g.S = a->S; g.H = a->H; g.hd = a->hd; g.D = a->H * a->hd;
   g.Sp16 = rup(a->S, 16); g.Sp32 = rup(a->S, 32); g.ldT = g.Sp32 + 8;
   g.rsb = a->row_stride_b; g.rss = a->row_stride_s;
+  g.Sst = a->S; g.base = 0; g.kmb = 0;
   return g;
 }
 

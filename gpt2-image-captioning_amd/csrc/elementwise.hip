@@ -30,14 +30,20 @@ template <typename T>
 __global__ void gpt2_embed_kernel(int B, int P, int L, int D, const T* __restrict__ prefix, int64_t pbs,
                                   const T* __restrict__ wte, const T* __restrict__ wpe,
                                   const int64_t* __restrict__ ids, T* __restrict__ x, uint32_t thr,
-                                  float inv_keep, uint64_t seed0, const uint64_t* seed_ptr, uint64_t offset) {
+                                  float inv_keep, uint64_t seed0, const uint64_t* seed_ptr, uint64_t offset,
+                                  const int32_t* __restrict__ seq_off, const int32_t* __restrict__ seq_len) {
   const int S = P + L, D4 = D >> 2;
   const uint64_t seed = thr ? eff_seed(seed0, seed_ptr) : 0ull;
   const int64_t total = (int64_t)B * S * D4;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = i / D4;
-    const int c = (int)(i - row * D4) * 4;
-    const int b = (int)(row / S), t = (int)(row - (int64_t)b * S);
+    const int64_t prow = i / D4;  // padded (b, t) index
+    const int c = (int)(i - prow * D4) * 4;
+    const int b = (int)(prow / S), t = (int)(prow - (int64_t)b * S);
+    int64_t row = prow;  // destination row
+    if (seq_off) {       // packed: only the live prefix of the sequence, at its packed rows
+      if (t >= seq_len[b]) continue;
+      row = (int64_t)seq_off[b] + t;
+    }
     float v[4], w[4];
     if (t < P) io<T>::ld4(prefix + (int64_t)b * pbs + (int64_t)t * D + c, v);
     else io<T>::ld4(wte + ids[(int64_t)b * L + (t - P)] * D + c, v);
@@ -117,6 +123,126 @@ __global__ __launch_bounds__(1024) void caption_prep_kernel(int B, int P, int L,
     }
   }
   if (threadIdx.x == 0 && n_valid) *n_valid = tot;
+}
+
+// Packed token rows (icap_caption_pack): one 1024-thread block. Phase 1: per-sequence live length (the last
+// position whose shifted label is a target, at least the P prefix rows) and an exclusive scan of the lengths
+// (threads own contiguous sequences). Phase 2: the per-row arrays over the packed rows (threads own contiguous
+// rows) and the target compaction, an exclusive scan over the same contiguous ownership as caption_prep_kernel,
+// so the compacted rows keep row order — the order caption_prep_kernel gives them in the padded layout.
+__device__ __forceinline__ int block_excl_scan1024(int cnt, int* wsum, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  __syncthreads();  // wsum reuse
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int woff = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    woff += k < w ? wsum[k] : 0;
+    tot += wsum[k];
+  }
+  total = tot;
+  return woff + incl - cnt;
+}
+
+__global__ __launch_bounds__(1024) void caption_pack_kernel(int B, int P, int L, const int64_t* __restrict__ mask,
+                                                           const int64_t* __restrict__ labels, int32_t* seq_off,
+                                                           int32_t* seq_len, int32_t* m_live, int32_t* key_mask,
+                                                           int32_t* lab_shift, int32_t* n_valid, int32_t* row_slot,
+                                                           int32_t* lab_c) {
+  __shared__ int wsum[16];
+  const int S = P + L, n = B * S;
+  auto label_at = [&](int b, int t) {  // shifted label of position t of sequence b
+    const int tn = t + 1;
+    return (tn < S && tn >= P && labels) ? (int)labels[(int64_t)b * L + tn - P] : -100;
+  };
+  // phase 1: lengths + offsets
+  const int bper = (B + 1023) / 1024;
+  const int b0 = threadIdx.x * bper < B ? threadIdx.x * bper : B;
+  const int b1 = b0 + bper < B ? b0 + bper : B;
+  int cnt = 0;
+  for (int b = b0; b < b1; ++b) {
+    int len = P;
+    for (int t = S - 1; t >= P; --t)
+      if (label_at(b, t) != -100) { len = t + 1; break; }
+    seq_len[b] = len;
+    cnt += len;
+  }
+  int mtot = 0;
+  int off = block_excl_scan1024(cnt, wsum, mtot);
+  for (int b = b0; b < b1; ++b) {
+    seq_off[b] = off;
+    off += seq_len[b];
+  }
+  if (threadIdx.x == 0) *m_live = mtot;
+  __syncthreads();  // seq_off / seq_len visible to the whole block
+  // phase 2: per packed row
+  const int per = (n + 1023) / 1024;
+  const int i0 = threadIdx.x * per < n ? threadIdx.x * per : n;
+  const int i1 = i0 + per < n ? i0 + per : n;
+  // sequence of the first row this thread owns (binary search over the offsets)
+  int bb = 0;
+  if (i0 < mtot) {
+    int lo = 0, hi = B - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (seq_off[mid] <= i0) lo = mid; else hi = mid - 1;
+    }
+    bb = lo;
+  }
+  int tcnt = 0;
+  {
+    int b = bb;
+    for (int i = i0; i < i1; ++i) {
+      int lab = -100, km = 0;
+      if (i < mtot) {
+        while (i >= seq_off[b] + seq_len[b]) ++b;  // skips empty sequences too
+        const int t = i - seq_off[b];
+        km = (t < P || mask == nullptr) ? 1 : (mask[(int64_t)b * L + t - P] != 0 ? 1 : 0);
+        lab = label_at(b, t);
+      }
+      key_mask[i] = km;
+      lab_shift[i] = lab;
+      tcnt += lab != -100 ? 1 : 0;
+    }
+  }
+  int tot = 0;
+  const int slot0 = block_excl_scan1024(tcnt, wsum, tot);
+  if (row_slot) {
+    int slot = slot0;
+    for (int i = i0; i < i1; ++i) {
+      const int lab = lab_shift[i];
+      if (lab != -100) {
+        row_slot[i] = slot;
+        if (lab_c) lab_c[slot] = lab;
+        ++slot;
+      } else {
+        row_slot[i] = -1;
+      }
+    }
+  }
+  if (threadIdx.x == 0 && n_valid) *n_valid = tot;
+}
+
+template <typename T>
+__global__ void rows_unpack_kernel(int B, int P, int D, const T* __restrict__ src, const int32_t* __restrict__ seq_off,
+                                   const int32_t* __restrict__ seq_len, T* __restrict__ dst, int64_t dbs) {
+  const int D4 = D >> 2;
+  const int64_t total = (int64_t)B * P * D4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / D4;
+    const int c = (int)(i - r * D4) * 4;
+    const int b = (int)(r / P), t = (int)(r - (int64_t)b * P);
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (t < seq_len[b]) io<T>::ld4(src + ((int64_t)seq_off[b] + t) * D + c, v);
+    io<T>::st4(dst + (int64_t)b * dbs + (int64_t)t * D + c, v);
+  }
 }
 
 // ---------------------------------------------------------------- cross entropy
@@ -911,11 +1037,6 @@ __global__ __launch_bounds__(512) void topp_sample_kernel(int64_t V, const T* __
       c = block_sum(c, sbuf[ci]); ci ^= 1;
       const uint64_t qs = kstar;
       const uint64_t ntie = (thr - a) / qs + 1;
-#ifdef ICAP_TOPP_DEBUG
-      if (tid == 0)
-        printf("row %d a %llu c %llu qs %llu thr %llu ntie %llu\n", b, (unsigned long long)a,
-               (unsigned long long)c, (unsigned long long)qs, (unsigned long long)thr, (unsigned long long)ntie);
-#endif
       if (ntie < c) {  // keep the ntie lowest indices of the tie group: jt = min{J : count(tie, j < J) >= ntie}
         uint32_t jlo = 1, jhi = (uint32_t)V;
         while (jlo < jhi) {
@@ -958,11 +1079,6 @@ __global__ __launch_bounds__(512) void topp_sample_kernel(int64_t V, const T* __
     ci ^= 1;
     if (s > target) jhi = mid; else jlo = mid + 1;
   }
-#ifdef ICAP_TOPP_DEBUG
-  if (tid == 0)
-    printf("row %d z %.9g kstar %08x jt %u tot %llu u %u target %llu -> %u\n", b, z, kstar, jt,
-           (unsigned long long)tot, u, (unsigned long long)target, jlo - 1);
-#endif
   if (tid == 0) out[b] = tot ? (int64_t)(jlo - 1) : 0;
 }
 
@@ -990,8 +1106,9 @@ using namespace icap;
 extern "C" int icap_gpt2_embed(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D, const void* prefix,
                                int64_t prefix_bstride, const void* wte, const void* wpe, const int64_t* ids, void* x,
                                float drop_p, uint64_t seed, uint64_t offset, const uint64_t* seed_ptr,
-                               void* stream) {
+                               const int32_t* seq_off, const int32_t* seq_len, void* stream) {
   ICAP_REQUIRE(D % 4 == 0 && B >= 0 && P >= 0 && L >= 0, "icap_gpt2_embed: bad geometry");
+  ICAP_REQUIRE((seq_off == nullptr) == (seq_len == nullptr), "icap_gpt2_embed: seq_off and seq_len go together");
   ICAP_REQUIRE(x && wpe && (P == 0 || prefix) && (L == 0 || (wte && ids)), "icap_gpt2_embed: null pointer");
   ICAP_REQUIRE(prefix_bstride % 4 == 0, "icap_gpt2_embed: prefix_bstride must be a multiple of 4");
   const int64_t n = (int64_t)B * (P + L) * (D / 4);
@@ -1001,11 +1118,11 @@ extern "C" int icap_gpt2_embed(int32_t dtype, int32_t B, int32_t P, int32_t L, i
   if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(gpt2_embed_kernel<bf16_t>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B, P, L, D,
                        (const bf16_t*)prefix, prefix_bstride, (const bf16_t*)wte, (const bf16_t*)wpe, ids, (bf16_t*)x,
-                       thr, ik, seed, seed_ptr, offset);
+                       thr, ik, seed, seed_ptr, offset, seq_off, seq_len);
   else
     hipLaunchKernelGGL(gpt2_embed_kernel<float>, dim3(nblk(n, 256, 8192)), dim3(256), 0, S_(stream), B, P, L, D,
                        (const float*)prefix, prefix_bstride, (const float*)wte, (const float*)wpe, ids, (float*)x,
-                       thr, ik, seed, seed_ptr, offset);
+                       thr, ik, seed, seed_ptr, offset, seq_off, seq_len);
   return check_launch("icap_gpt2_embed");
 }
 
@@ -1018,6 +1135,34 @@ extern "C" int icap_caption_prep(int32_t B, int32_t P, int32_t L, const int64_t*
   hipLaunchKernelGGL(caption_prep_kernel, dim3(1), dim3(1024), 0, S_(stream), B, P, L, mask, labels, key_mask,
                      labels_shift, n_valid, row_slot, labels_compact);
   return check_launch("icap_caption_prep");
+}
+
+extern "C" int icap_caption_pack(int32_t B, int32_t P, int32_t L, const int64_t* mask, const int64_t* labels,
+                                 int32_t* seq_off, int32_t* seq_len, int32_t* m_live, int32_t* key_mask,
+                                 int32_t* labels_shift, int32_t* n_valid, int32_t* row_slot, int32_t* labels_compact,
+                                 void* stream) {
+  ICAP_REQUIRE(B >= 1 && P >= 0 && L >= 0, "icap_caption_pack: bad geometry");
+  ICAP_REQUIRE((int64_t)B * (P + L) < (1ll << 30), "icap_caption_pack: too many rows");
+  ICAP_REQUIRE(seq_off && seq_len && m_live && key_mask && labels_shift, "icap_caption_pack: null pointer");
+  ICAP_REQUIRE((row_slot == nullptr) == (labels_compact == nullptr), "icap_caption_pack: row_slot and labels_compact go together");
+  hipLaunchKernelGGL(caption_pack_kernel, dim3(1), dim3(1024), 0, S_(stream), B, P, L, mask, labels, seq_off, seq_len,
+                     m_live, key_mask, labels_shift, n_valid, row_slot, labels_compact);
+  return check_launch("icap_caption_pack");
+}
+
+extern "C" int icap_rows_unpack(int32_t dtype, int32_t B, int32_t P, int32_t D, const void* src, const int32_t* seq_off,
+                                const int32_t* seq_len, void* dst, int64_t dst_bstride, void* stream) {
+  ICAP_REQUIRE(B >= 0 && P >= 0 && D > 0 && D % 4 == 0 && dst_bstride % 4 == 0, "icap_rows_unpack: bad geometry");
+  ICAP_REQUIRE(src && seq_off && seq_len && dst, "icap_rows_unpack: null pointer");
+  const int64_t n = (int64_t)B * P * (D / 4);
+  if (n == 0) return ICAP_OK;
+  if (dtype == ICAP_BF16)
+    hipLaunchKernelGGL(rows_unpack_kernel<bf16_t>, dim3(nblk(n, 256, 4096)), dim3(256), 0, S_(stream), B, P, D,
+                       (const bf16_t*)src, seq_off, seq_len, (bf16_t*)dst, dst_bstride);
+  else
+    hipLaunchKernelGGL(rows_unpack_kernel<float>, dim3(nblk(n, 256, 4096)), dim3(256), 0, S_(stream), B, P, D,
+                       (const float*)src, seq_off, seq_len, (float*)dst, dst_bstride);
+  return check_launch("icap_rows_unpack");
 }
 
 extern "C" size_t icap_cross_entropy_workspace_bytes(int64_t rows) {

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   constexpr int NW = WM * WN;
   constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
   constexpr int STB = (BM + BN) * GROWB;    // bytes per stage
-  constexpr int EPR = NST == 2 ? 32 : 16;   // rows per LDS-staged epilogue pass
+  constexpr int EPR = NST >= 2 ? 32 : 16;   // rows per LDS-staged epilogue pass
   constexpr int ELD = 16 * TN + 4;          // fp32 row stride of the epilogue staging tile
   static_assert(NW * EPR * ELD * 4 <= NST * STB, "epilogue staging must fit the stage buffers");
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "each wave stages whole 8-row DMA pieces");
@@ -101,22 +101,25 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave - wm * WN;
 
-  // bijective XCD-aware remap: blocks sharing an XCD get consecutive tiles
-  // (consecutive tiles share the A row panel).
-  const int bid = blockIdx.x, nwg = gridDim.x;
+  const int64_t M = p.M, N = p.N, K = p.K;
+  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;  // device row count
+  // bijective XCD-aware remap over the LIVE blocks: blocks sharing an XCD get consecutive tiles (consecutive
+  // tiles share the A row panel). With a device row count the grid is sized for M but only the first
+  // nlive = (row tiles of Mv) x tiles_n x splits blocks work: they are the lowest block ids, which the dispatcher
+  // hands out first and round-robin over the XCDs, so the live tiles land one per CU before any CU takes a second
+  // (the dead blocks exit at once), and the remap over nlive keeps every XCD's share contiguous.
+  const int bid = blockIdx.x;
+  const int tiles_m = (int)(gridDim.x / splits) / tiles_n;
+  const int tiles_mv = p.m_dev ? (int)((Mv + BM - 1) / BM) : tiles_m;
+  const int nwg = tiles_mv * tiles_n * splits;
+  if (bid >= nwg) return;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   // split-K: split-major order, so the blocks of one split (same K range) sit together on an XCD
-  const int tiles = (int)(gridDim.x / splits);
+  const int tiles = tiles_mv * tiles_n;
   const int split = wgid / tiles, tile = wgid - split * tiles;
-  // row tiles fastest when the row count is device-side: the live tiles (low rows) then spread over every XCD
-  const int tiles_m = tiles / tiles_n;
-  const int tm = p.m_dev ? tile % tiles_m : tile / tiles_n;
-  const int tn = p.m_dev ? tile / tiles_m : tile - tm * tiles_n;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-
-  const int64_t M = p.M, N = p.N, K = p.K;
-  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;  // device row count
   if (m0 >= Mv) return;
   // tile-relative buffer descriptors: rows past M / N fall beyond num_records and load zeros
   // (K-outer: k-rows past K do; columns past M / N read neighbouring data that only reaches unstored outputs)
@@ -262,7 +265,73 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     }
   };
 
-  if (NST == 2) {
+  if constexpr (NST == 4) {
+    // Deep ring for launches with about one tile per CU and long K (the packed step's N = 768 products): 4 LDS
+    // stages (128 KiB, one block per CU), stages kt+1..kt+2 in flight while stage kt is read and stage kt+3 is
+    // issued, so three DMA round trips overlap each stage's MFMAs (the double-buffered loop leaves one: at one block
+    // per CU it waited ~0.6 of every k-step on the DMA). The fragment reads are inline asm (hipcc would otherwise
+    // drain the DMA queue, vmcnt(0), in front of every LDS read), retired by counted lgkmcnt waits tied to their
+    // registers; the DMA waits are counted vmcnt (never 0 in the steady state) and the barriers raw s_barrier
+    // (cdna_hip_programming.md "Pipelining across barriers", T3+T4).
+    //   RAW: stage kt is read after this wave's vmcnt wait for it and a barrier every wave passed after its own.
+    //   WAR: stage kt+3 is written into the slot read in iteration kt-1, whose reads every wave retired (lgkmcnt)
+    //        before that iteration's MFMAs, i.e. before the barrier of iteration kt.
+    static_assert(!KOUT && !MX && sizeof(TI) == 2 && TM == 4 && TN == 4 && APW + BPW == 8,
+                  "ring: bf16 row-major operands, 128 x 128 tiles of 4 waves");
+    typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+    const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>(smem);
+    uint32_t la[2], lb[2];  // byte offsets in a stage of this lane's fragment rows (A row / B row + 16 i)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint32_t sw = (uint32_t)(((ks * 4 + fg) ^ (fr & 7)) << 4);
+      la[ks] = (uint32_t)((wm * 16 * TM + fr) * GROWB) + sw;
+      lb[ks] = (uint32_t)(BM * GROWB + (wn * 16 * TN + fr) * GROWB) + sw;
+    }
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+      if (s < nk) load_stage(kbase + (int64_t)s * BKE, s);
+#define ICAP_RING_RD(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
+    for (int kt = 0; kt < nk; ++kt) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");      // stages kt+1, kt+2 stay in flight
+      else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 3 < nk) load_stage(kbase + (int64_t)(kt + 3) * BKE, (kt + 3) & 3);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t sb = sbase + (uint32_t)((kt & 3) * STB);
+      u32x4_t fa0[4], fb0[4], fa1[4], fb1[4];
+      {
+        const uint32_t a0 = sb + la[0], b0 = sb + lb[0], a1 = sb + la[1], b1 = sb + lb[1];
+        ICAP_RING_RD(fa0[0], a0, 0); ICAP_RING_RD(fa0[1], a0, 2048); ICAP_RING_RD(fa0[2], a0, 4096); ICAP_RING_RD(fa0[3], a0, 6144);
+        ICAP_RING_RD(fb0[0], b0, 0); ICAP_RING_RD(fb0[1], b0, 2048); ICAP_RING_RD(fb0[2], b0, 4096); ICAP_RING_RD(fb0[3], b0, 6144);
+        ICAP_RING_RD(fa1[0], a1, 0); ICAP_RING_RD(fa1[1], a1, 2048); ICAP_RING_RD(fa1[2], a1, 4096); ICAP_RING_RD(fa1[3], a1, 6144);
+        ICAP_RING_RD(fb1[0], b1, 0); ICAP_RING_RD(fb1[1], b1, 2048); ICAP_RING_RD(fb1[2], b1, 4096); ICAP_RING_RD(fb1[3], b1, 6144);
+      }
+      asm volatile("s_waitcnt lgkmcnt(8)"
+                   : "+v"(fa0[0]), "+v"(fa0[1]), "+v"(fa0[2]), "+v"(fa0[3]), "+v"(fb0[0]), "+v"(fb0[1]), "+v"(fb0[2]),
+                     "+v"(fb0[3]));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          mfma_chunk<TI>(acc[i][j], __builtin_bit_cast(uint4, fa0[i]), __builtin_bit_cast(uint4, fb0[j]));
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(fa1[0]), "+v"(fa1[1]), "+v"(fa1[2]), "+v"(fa1[3]), "+v"(fb1[0]), "+v"(fb1[1]), "+v"(fb1[2]),
+                     "+v"(fb1[3]));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          mfma_chunk<TI>(acc[i][j], __builtin_bit_cast(uint4, fa1[i]), __builtin_bit_cast(uint4, fb1[j]));
+    }
+#undef ICAP_RING_RD
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();  // (no DMA outstanding) every wave is done reading the ring before the epilogue reuses it
+  } else if (NST == 2) {
     load_stage(kbase, 0);
     load_scales(kt0, sca_cur, scb_cur);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -946,6 +1015,13 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   pl.splits = (int)splits;
   pl.nk_split = (int)nk_split;
   pl.variant = gemm_variant(p, nk_split);
+  // Long K over about one 128 x 128 tile per CU (the packed step's N = 768 products: M_live ~ 3600 -> 168 tiles):
+  // the 4-stage ring at one block per CU (the double-buffered loop at 2 blocks per CU only pays when a CU holds two
+  // tiles). With a device row count the choice follows the expected count (m_hint).
+  const int64_t m_plan = (p.m_dev && p.m_hint > 0 && p.m_hint < p.M) ? p.m_hint : p.M;
+  const int64_t tiles_plan = ((m_plan + GBM - 1) / GBM) * tiles_n;
+  if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 && nk_split > 16 && tiles_plan * 4 <= (int64_t)device_cus() * 5)
+    pl.variant = 16;
   if (mx && pl.variant == 5) pl.variant = 4;  // MX at 4 blocks / CU (128 VGPRs) spills: 3 blocks / CU
   if (narrow) {
     tiles_n = (p.N + 63) / 64;
@@ -969,6 +1045,7 @@ static const char* variant_kernel(int v) {
     case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2, false, %s>";
     case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2, false, %s>";
     case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true, %s>";
+    case 16: return "gemm_kernel<%s, %s, 4, 1, 2, 2, 4, 4, false, %s>";
     default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %s>";
   }
 }
@@ -1062,6 +1139,9 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
       if (pl.variant == 14) ICAP_GK(bf16_t, float, 2, 2, 4, 4, true);
       else ICAP_GK(bf16_t, float, 1, 3, 4, 4, true);
     }
+  } else if (pl.variant == 16) {  // 4-stage ring (bf16 inputs only)
+    if (p.c_dtype == ICAP_BF16) ICAP_GK(bf16_t, bf16_t, 4, 1, 4, 4, false);
+    else ICAP_GK(bf16_t, float, 4, 1, 4, 4, false);
   } else if (pl.variant == 12 || pl.variant == 13) {  // 128 x 64 (bf16 inputs only)
     if (p.c_dtype == ICAP_BF16) {
       if (pl.variant == 12) ICAP_GK(bf16_t, bf16_t, 2, 3, 4, 2, false);

@@ -13,7 +13,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int64_t rows, int D, const 
                                                     const float* __restrict__ gamma,
                                                     const float* __restrict__ beta, float eps,
                                                     T* __restrict__ y, int64_t ldy, float* mean_out,
-                                                    float* rstd_out, const int32_t* __restrict__ y_rowmap) {
+                                                    float* rstd_out, const int32_t* __restrict__ y_rowmap,
+                                                    const int32_t* __restrict__ rows_dev) {
+  if (rows_dev && (int64_t)*rows_dev < rows) rows = *rows_dev;
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   const int D4 = D >> 2;
@@ -77,7 +79,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t rows, int D, const 
                                                     uint32_t thr, float inv_keep, uint64_t seed0,
                                                     const uint64_t* seed_ptr, uint64_t offset,
                                                     float* __restrict__ partial,
-                                                    const int32_t* __restrict__ dy_rowmap) {
+                                                    const int32_t* __restrict__ dy_rowmap,
+                                                    const int32_t* __restrict__ rows_dev) {
+  if (rows_dev && (int64_t)*rows_dev < rows) rows = *rows_dev;
   __shared__ float red[4][2][LN_MAXV * 256];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -216,7 +220,9 @@ __global__ __launch_bounds__(256) void ln_fwd8_kernel(int64_t rows, int D, const
                                                      const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps,
                                                      T* __restrict__ y, int64_t ldy, float* mean_out,
-                                                     float* rstd_out, const int32_t* __restrict__ y_rowmap) {
+                                                     float* rstd_out, const int32_t* __restrict__ y_rowmap,
+                                                    const int32_t* __restrict__ rows_dev) {
+  if (rows_dev && (int64_t)*rows_dev < rows) rows = *rows_dev;
   const int hl = threadIdx.x & 31;
   const int64_t nr = (int64_t)gridDim.x * 8;
   const int D8 = D >> 3;
@@ -279,7 +285,9 @@ __global__ __launch_bounds__(256) void ln_bwd8_kernel(int64_t rows, int D, const
                                                      uint32_t thr, float inv_keep, uint64_t seed0,
                                                      const uint64_t* seed_ptr, uint64_t offset,
                                                      float* __restrict__ partial,
-                                                     const int32_t* __restrict__ dy_rowmap) {
+                                                     const int32_t* __restrict__ dy_rowmap,
+                                                    const int32_t* __restrict__ rows_dev) {
+  if (rows_dev && (int64_t)*rows_dev < rows) rows = *rows_dev;
   __shared__ float red[PARAMS ? 4 : 1][2][PARAMS ? LN8_MAXC * 256 : 1];  // [wave][dgamma|dbeta][column]
   const int hl = threadIdx.x & 31;
   const int wv = threadIdx.x >> 6;
@@ -411,7 +419,8 @@ static int ln_blocks(int64_t rows, int cap) {
 
 extern "C" int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
                                   const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
-                                  float* mean, float* rstd, const int32_t* y_rowmap, void* stream) {
+                                  float* mean, float* rstd, const int32_t* y_rowmap, const int32_t* rows_dev,
+                                  void* stream) {
   ICAP_REQUIRE(x && y && gamma && beta, "icap_layernorm_fwd: null pointer");
   ICAP_REQUIRE(D > 0 && D % 4 == 0 && (D <= 4 * 64 * LN_MAXV || (D <= LN8_DMAX && ln8_ok(dtype, D, x, ldx) &&
                                                                ln8_ok(dtype, D, y, ldy))),
@@ -423,7 +432,7 @@ extern "C" int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const 
     const int nb8 = ln_blocks8(rows, 4096);
 #define ICAP_LN_FWD8(T, NC)                                                                                    \
   hipLaunchKernelGGL((ln_fwd8_kernel<T, NC>), dim3(nb8), dim3(256), 0, s, rows, (int)D, (const T*)x, ldx, gamma, \
-                     beta, eps, (T*)y, ldy, mean, rstd, y_rowmap)
+                     beta, eps, (T*)y, ldy, mean, rstd, y_rowmap, rows_dev)
     if (dtype == ICAP_BF16) {
       if (D <= 768) ICAP_LN_FWD8(bf16_t, 3); else if (D <= 1024) ICAP_LN_FWD8(bf16_t, 4);
       else if (D <= 1280) ICAP_LN_FWD8(bf16_t, 5); else ICAP_LN_FWD8(bf16_t, 6);
@@ -437,10 +446,10 @@ extern "C" int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const 
   const int nb = ln_blocks(rows, 4096);
   if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, rows, (int)D,
-                       (const bf16_t*)x, ldx, gamma, beta, eps, (bf16_t*)y, ldy, mean, rstd, y_rowmap);
+                       (const bf16_t*)x, ldx, gamma, beta, eps, (bf16_t*)y, ldy, mean, rstd, y_rowmap, rows_dev);
   else
     hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const float*)x,
-                       ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd, y_rowmap);
+                       ldx, gamma, beta, eps, (float*)y, ldy, mean, rstd, y_rowmap, rows_dev);
   return check_launch("icap_layernorm_fwd");
 }
 
@@ -453,7 +462,8 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
                                   const void* dy, int64_t lddy, const void* dres, int64_t lddres,
                                   void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
                                   uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
-                                  void* workspace, const int32_t* dy_rowmap, void* stream) {
+                                  void* workspace, const int32_t* dy_rowmap, const int32_t* rows_dev,
+                                  void* stream) {
   ICAP_REQUIRE(x && gamma && mean && rstd && dy && dx, "icap_layernorm_bwd: null pointer");
   const bool wide8 = ln8_ok(dtype, D, x, ldx) && ln8_ok(dtype, D, dy, lddy) && ln8_ok(dtype, D, dx, lddx) &&
                      (dres == nullptr || ln8_ok(dtype, D, dres, lddres)) &&
@@ -479,7 +489,7 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
 #define ICAP_LN_BWD8N(T, P, NC)                                                                                 \
   hipLaunchKernelGGL((ln_bwd8_kernel<T, P, NC>), dim3(nb8), dim3(256), 0, s, rows, (int)D, (const T*)x, ldx, gamma, \
                      mean, rstd, (const T*)dy, lddy, (const T*)dres, lddres, (T*)dx, lddx, (T*)dx_drop, thr,     \
-                     inv_keep, seed, seed_ptr, offset, partial, dy_rowmap)
+                     inv_keep, seed, seed_ptr, offset, partial, dy_rowmap, rows_dev)
     if (dtype == ICAP_BF16) {
       if (want_params) ICAP_LN_BWD8(bf16_t, true); else ICAP_LN_BWD8(bf16_t, false);
     } else {
@@ -490,11 +500,11 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
   } else if (dtype == ICAP_BF16)
     hipLaunchKernelGGL(ln_bwd_kernel<bf16_t>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const bf16_t*)x, ldx,
                        gamma, mean, rstd, (const bf16_t*)dy, lddy, (const bf16_t*)dres, lddres, (bf16_t*)dx,
-                       lddx, (bf16_t*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial, dy_rowmap);
+                       lddx, (bf16_t*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial, dy_rowmap, rows_dev);
   else
     hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nb), dim3(256), 0, s, rows, (int)D, (const float*)x, ldx,
                        gamma, mean, rstd, (const float*)dy, lddy, (const float*)dres, lddres, (float*)dx,
-                       lddx, (float*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial, dy_rowmap);
+                       lddx, (float*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial, dy_rowmap, rows_dev);
   int rc = check_launch("icap_layernorm_bwd");
   if (rc != ICAP_OK || !want_params) return rc;
   hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 63) / 64), 2), dim3(1024), 0, s, nb, (int)D, partial,

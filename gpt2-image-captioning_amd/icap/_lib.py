@@ -46,6 +46,7 @@ class GemmArgs(C.Structure):
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
         ("path", i32),
         ("a_scale", vp), ("b_scale", vp),
+        ("m_hint", i64),
     ]
 
 
@@ -64,6 +65,7 @@ class AttnArgs(C.Structure):
         ("seed_ptr", vp),
         ("dout", vp), ("ld_dout", i64),
         ("dqkv", vp), ("ld_dqkv", i64),
+        ("seq_off", vp), ("seq_len", vp),
     ]
 
 
@@ -101,10 +103,10 @@ SIGNATURES = {
     "icap_gemm_kernel_name": (C.c_char_p, [C.POINTER(GemmArgs)]),
     "icap_mx_scale_bytes": (sz, [i64, i64]),
     "icap_quantize_mx": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, vp, vp, vp]),
-    "icap_layernorm_fwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, f32, vp, i64, vp, vp, vp, vp]),
+    "icap_layernorm_fwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, f32, vp, i64, vp, vp, vp, vp, vp]),
     "icap_layernorm_bwd_workspace_bytes": (sz, [i64, i64]),
     "icap_layernorm_bwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, vp,
-                                     f32, u64, u64, vp, vp, vp, vp, vp, vp]),
+                                     f32, u64, u64, vp, vp, vp, vp, vp, vp, vp]),
     "icap_attention_fwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_bwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_decode": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, i64, f32, vp]),
@@ -115,9 +117,11 @@ SIGNATURES = {
     "icap_beam_rowtop": (C.c_int, [i32, i64, i64, vp, i64, i32, vp, vp, vp, vp, vp]),
     "icap_beam_update": (C.c_int, [C.POINTER(BeamArgs), i32, i32, vp]),
     "icap_beam_finalize": (C.c_int, [C.POINTER(BeamArgs), vp, vp, vp]),
-    "icap_gpt2_embed": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, vp, f32, u64, u64, vp, vp]),
+    "icap_gpt2_embed": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, vp, f32, u64, u64, vp, vp, vp, vp]),
     "icap_embedding_scatter_add": (C.c_int, [i32, i32, i32, i32, i32, vp, vp, vp, vp]),
     "icap_caption_prep": (C.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "icap_caption_pack": (C.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "icap_rows_unpack": (C.c_int, [i32, i32, i32, i32, vp, vp, vp, vp, i64, vp]),
     "icap_cross_entropy_workspace_bytes": (sz, [i64]),
     "icap_cross_entropy": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, f32, vp, vp, vp]),
     "icap_adamw_workspace_bytes": (sz, [i64]),

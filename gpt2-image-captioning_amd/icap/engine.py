@@ -27,7 +27,8 @@ class CaptionTrainer:
     def __init__(self, model, batch_size: int, caption_len: int, *, lr: float = 1e-4, weight_decay: float = 0.01,
                  betas=(0.9, 0.999), eps: float = 1e-8, max_norm: float = 1.0, num_warmup_steps: int = 0,
                  num_training_steps: int = 1, dropout: bool = True, seed: int = 0, clip_model=None,
-                 grad_accum_steps: int = 1, process_group=None, compact_head: bool = True):
+                 grad_accum_steps: int = 1, process_group=None, compact_head: bool = True,
+                 pack_rows: Optional[bool] = None):
         self.model = model
         self.dtype = model.compute_dtype
         self.B, self.Lc = batch_size, caption_len
@@ -68,7 +69,12 @@ class CaptionTrainer:
         P = model.total_prefix_length
         self.P = P
         self.mws = self.mcore.alloc(B, train=True)
-        self.gws = self.gcore.alloc_train(B, P, Lc, keep_for_dw=self.gpt_trainable, compact_head=compact_head)
+        # packed token rows (GPT2Core.alloc_train): the blocks skip each caption's dead tail (positions after its
+        # last loss target, which the causal mask keeps out of every loss term); default on, ICAP_PACK=0 disables
+        if pack_rows is None:
+            pack_rows = os.environ.get("ICAP_PACK", "1") != "0"
+        self.gws = self.gcore.alloc_train(B, P, Lc, keep_for_dw=self.gpt_trainable, compact_head=compact_head,
+                                          pack=pack_rows)
         D = self.gcore.D
         M2 = self.mws.M
         E = self.mcore.E
@@ -142,6 +148,10 @@ class CaptionTrainer:
     # -- inputs -----------------------------------------------------------------------------------------------
     def load_batch(self, ids: Tensor, mask: Tensor, labels: Tensor, emb: Optional[Tensor] = None,
                    pixels: Optional[Tensor] = None) -> None:
+        if self.gws.pack and self.gws.live_rows_hint is None:
+            # the first batch's packed row count (one host read, before any capture): the GEMM kernel choice for the
+            # expected live rows (icap_gemm_args.m_hint); the device count of every batch is what bounds the work
+            self.gws.live_rows_hint = live_rows(labels, self.P)
         self.ids.copy_(ids, non_blocking=True)
         self.mask.copy_(mask, non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)
@@ -422,6 +432,15 @@ class CaptionTrainer:
 
 
 @torch.no_grad()
+def live_rows(labels: Tensor, P: int) -> int:
+    """Packed token rows of a batch (icap_caption_pack's m_live, computed on the host side of the copy):
+    sum over captions of max(P, P + last caption index with a target)."""
+    valid = (labels != -100).to(torch.int64)
+    pos = torch.arange(1, labels.shape[1] + 1, device=labels.device, dtype=torch.int64)
+    last = (valid * pos).max(dim=1).values  # last target index + 1, or 0
+    return int((P + (last - 1).clamp_min(0)).sum().item())
+
+
 def broadcast_replicas(modules, process_group=None) -> None:
     """Broadcast every parameter and buffer of `modules` from the group's rank 0, in place, then drop the compute
     copies derived from them (GPT-2 / mapper / image-tower cores, the mapper's bf16 flat copy) so they are rebuilt

@@ -320,11 +320,15 @@ class GPT2Core:
 
     # -- workspaces --------------------------------------------------------------------------------------
     def alloc_train(self, B: int, P: int, Lc: int, keep_for_dw: bool = False,
-                    compact_head: bool = False) -> SimpleNamespace:
+                    compact_head: bool = False, pack: bool = False) -> SimpleNamespace:
         """compact_head: the LM head and CE run on the rows whose shifted label is not -100 only (at most B*Lc;
         the count lives on the device). The loss ignores every other row (HF/loss/loss_utils.py:32-46,
         ignore_index=-100), so their logits feed nothing and their dlogits are exactly 0: loss and gradients are
-        those of the full-width head. Needs labels; not with a trainable (tied) wte."""
+        those of the full-width head. Needs labels; not with a trainable (tied) wte.
+        pack (with compact_head): the blocks run on packed token rows — each sequence's prefix and caption
+        positions up to its last loss target (icap_caption_pack), the rest of the [B, P + Lc] grid is dead under
+        the causal mask — so every block GEMM, LayerNorm and attention launch covers the live rows only (row
+        count on the device; launches sized for the padded grid, so one captured graph serves every batch)."""
         S = P + Lc
         M = B * S
         D, H, dt, dev = self.D, self.H, self.dtype, self.dev
@@ -334,6 +338,15 @@ class GPT2Core:
         ws.compact = bool(compact_head and Lc > 0 and not keep_for_dw)
         ws.Mh = B * Lc if ws.compact else M  # rows of the LM head / CE buffers
         ws.head_rows_hint = None  # host-known number of target rows (roofline bookkeeping only)
+        ws.pack = bool(pack and ws.compact)
+        ws.live_rows_hint = None  # host-known number of packed rows (roofline bookkeeping only)
+        ws.seqs = ws.m_live = None
+        if ws.pack:
+            ws.seq_off = e(B, dtype=torch.int32)
+            ws.seq_len = e(B, dtype=torch.int32)
+            ws.m_live = e(1, dtype=torch.int32)
+            ws.seqs = (ws.seq_off, ws.seq_len)
+            ws.d_emb = e(M, D)  # the prefix rows' gradient back in the padded [B, S, D] layout
         ws.x = [e(M, D) for _ in range(nl + 1)]
         ws.h1 = [e(M, D) for _ in range(nl)]
         ws.qkv = [e(M, 3 * D) for _ in range(nl)]
@@ -375,6 +388,16 @@ class GPT2Core:
             ws.qhf, ws.qdl = mx(Mh, D), mx(Mh, self.Vp)
         return ws
 
+    def _bmm(self, ws, A: Tensor, qA, W: Tensor, qW, out: Tensor, **kw) -> Tensor:
+        """A block GEMM over the token rows: with packed rows only rows < m_live are computed (m_dev)."""
+        if not ws.pack:
+            return self._mm(A, qA, W, qW, out, **kw)
+        if ws.live_rows_hint is not None:
+            if "alg_flops" not in kw:
+                kw["alg_flops"] = 2.0 * ws.live_rows_hint * W.shape[0] * A.shape[1]
+            kw["m_hint"] = ws.live_rows_hint  # kernel choice for the expected live rows
+        return self._mm(A, qA, W, qW, out, rows_dev=ws.m_live, m_dev=ws.m_live, **kw)
+
     def _mm(self, A: Tensor, qA, W: Tensor, qW, out: Tensor, rows_dev: Optional[Tensor] = None, **kw) -> Tensor:
         """out = epi(A . W^T): the bf16 / f32 GEMM, or (fp8_mx) quantise A into qA and run the MX product with
         the weight's MX copy qW (same epilogue arguments)."""
@@ -413,12 +436,17 @@ class GPT2Core:
         cp = ws.compact
         if cp and labels is None:
             raise L.IcapError("compact LM head needs labels")
-        ops.caption_prep(B, P, Lc, mask, labels, ws.key_mask, ws.labels_shift, ws.n_valid,
-                         ws.row_slot if cp else None, ws.labels_c if cp else None)
-        ops.gpt2_embed(prefix, prefix_bstride, self.wte, self.wpe, ids, ws.x[0], B=B, P=P, L_=Lc, D=D, drop=dr.embd)
+        if ws.pack:
+            ops.caption_pack(B, P, Lc, mask, labels, ws.seq_off, ws.seq_len, ws.m_live, ws.key_mask, ws.labels_shift,
+                             ws.n_valid, ws.row_slot, ws.labels_c)
+        else:
+            ops.caption_prep(B, P, Lc, mask, labels, ws.key_mask, ws.labels_shift, ws.n_valid,
+                             ws.row_slot if cp else None, ws.labels_c if cp else None)
+        ops.gpt2_embed(prefix, prefix_bstride, self.wte, self.wpe, ids, ws.x[0], B=B, P=P, L_=Lc, D=D, drop=dr.embd,
+                       seqs=ws.seqs)
         self._blocks_fwd(ws, dr, B, S, M, causal_mask=ws.key_mask if mask is not None else None)
         ops.layernorm_fwd(ws.x[-1], self.lnf_g, self.lnf_b, self.eps, ws.hf, ws.meanf, ws.rstdf,
-                          y_rowmap=ws.row_slot if cp else None)
+                          y_rowmap=ws.row_slot if cp else None, rows_dev=ws.m_live)
         rows = ws.head_rows_hint if (cp and ws.head_rows_hint is not None) else ws.Mh
         self._mm(ws.hf, ws.qhf, self.wte, getattr(self, "qwte", None), ws.logits, rows_dev=ws.n_valid if cp else None,
                  M=ws.Mh, m_dev=ws.n_valid if cp else None, alg_flops=2.0 * rows * self.V * self.D)
@@ -430,17 +458,21 @@ class GPT2Core:
     def _blocks_fwd(self, ws, dr, B, S, M, causal_mask):
         D, H, hd = self.D, self.H, self.hd
         scale = 1.0 / math.sqrt(hd)
+        rd = getattr(ws, "m_live", None)  # packed rows: device row count (None: every row)
+        seqs = getattr(ws, "seqs", None)
         for l, lw in enumerate(self.layers):
             x = ws.x[l]
             q = lw if self.fp8 else SimpleNamespace(qw_attn_t=None, qw_proj_t=None, qw_fc_t=None, qw_mp_t=None)
-            ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, ws.a1[l], ws.mean1[l], ws.rstd1[l])
-            self._mm(ws.a1[l], ws.qD, lw.w_attn_t, q.qw_attn_t, ws.qkv[l], bias=lw.b_attn)
+            ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, ws.a1[l], ws.mean1[l], ws.rstd1[l], rows_dev=rd)
+            self._bmm(ws, ws.a1[l], ws.qD, lw.w_attn_t, q.qw_attn_t, ws.qkv[l], bias=lw.b_attn)
             ops.attention_fwd(ws.qkv[l], ws.o[l], B=B, S=S, H=H, hd=hd, scale=scale, causal=True, key_mask=causal_mask,
-                              lse=ws.lse[l], drop=dr.attn(l))
-            self._mm(ws.o[l], ws.qD, lw.w_proj_t, q.qw_proj_t, ws.h1[l], bias=lw.b_proj, resid=x, drop=dr.ra(l))
-            ops.layernorm_fwd(ws.h1[l], lw.ln2_g, lw.ln2_b, self.eps, ws.a2[l], ws.mean2[l], ws.rstd2[l])
-            self._mm(ws.a2[l], ws.qD, lw.w_fc_t, q.qw_fc_t, ws.f[l], bias=lw.b_fc, act=L.ACT_GELU_NEW, aux=ws.z[l])
-            self._mm(ws.f[l], ws.q4D, lw.w_mp_t, q.qw_mp_t, ws.x[l + 1], bias=lw.b_mp, resid=ws.h1[l], drop=dr.rm(l))
+                              lse=ws.lse[l], drop=dr.attn(l), seqs=seqs)
+            self._bmm(ws, ws.o[l], ws.qD, lw.w_proj_t, q.qw_proj_t, ws.h1[l], bias=lw.b_proj, resid=x, drop=dr.ra(l))
+            ops.layernorm_fwd(ws.h1[l], lw.ln2_g, lw.ln2_b, self.eps, ws.a2[l], ws.mean2[l], ws.rstd2[l], rows_dev=rd)
+            self._bmm(ws, ws.a2[l], ws.qD, lw.w_fc_t, q.qw_fc_t, ws.f[l], bias=lw.b_fc, act=L.ACT_GELU_NEW,
+                      aux=ws.z[l])
+            self._bmm(ws, ws.f[l], ws.q4D, lw.w_mp_t, q.qw_mp_t, ws.x[l + 1], bias=lw.b_mp, resid=ws.h1[l],
+                      drop=dr.rm(l))
 
     # -- backward (dX through the frozen GPT-2; + dW when trainable) ---------------------------------------------
     def backward(self, ws, dr, causal_mask, dlogits: Tensor, grads=None, dw=None) -> Tensor:
@@ -463,10 +495,11 @@ class GPT2Core:
                  M=ws.Mh, m_dev=ws.n_valid if cp else None, alg_flops=2.0 * rows * D * self.V, split_k=split)
         if grads is not None:  # d(wte) from the tied LM head: dW[V,D] += dlogits^T . hf
             dw.dW(dlogits, ws.hf, grads.wte, M=M, N=self.V)
+        rd, seqs = ws.m_live, ws.seqs  # packed rows (None: every row)
         ops.layernorm_bwd(ws.x[-1], self.lnf_g, ws.meanf, ws.rstdf, ws.dhf, ws.dx, dx_drop=ws.dxd,
                           drop=dr.rm(nl - 1), dgamma=grads.lnf_g if grads else None,
                           dbeta=grads.lnf_b if grads else None, workspace=dw.ln_ws if dw else None,
-                          dy_rowmap=ws.row_slot if cp else None)
+                          dy_rowmap=ws.row_slot if cp else None, rows_dev=rd)
         dres, dnew = ws.dx, ws.dx2
         for l in reversed(range(nl)):
             lw = self.layers[l]
@@ -476,32 +509,36 @@ class GPT2Core:
                 dw.dW(dy, ws.f[l], g.w_mp, M=M, transpose_out=True)
                 dw.db(dy, g.b_mp, M=M)
             q = lw if self.fp8 else SimpleNamespace(qw_attn=None, qw_proj=None, qw_fc=None, qw_mp=None)
-            self._mm(dy, ws.qD, lw.w_mp, q.qw_mp, ws.dff, dact=L.ACT_GELU_NEW, dact_src=ws.z[l])
+            self._bmm(ws, dy, ws.qD, lw.w_mp, q.qw_mp, ws.dff, dact=L.ACT_GELU_NEW, dact_src=ws.z[l])
             if g is not None:
                 dw.dW(ws.dff, ws.a2[l], g.w_fc, M=M, transpose_out=True)
                 dw.db(ws.dff, g.b_fc, M=M)
-            self._mm(ws.dff, ws.q4D, lw.w_fc, q.qw_fc, ws.da)
+            self._bmm(ws, ws.dff, ws.q4D, lw.w_fc, q.qw_fc, ws.da)
             ops.layernorm_bwd(ws.h1[l], lw.ln2_g, ws.mean2[l], ws.rstd2[l], ws.da, dnew, dres=dres, dx_drop=ws.dxd,
                               drop=dr.ra(l), dgamma=g.ln2_g if g else None, dbeta=g.ln2_b if g else None,
-                              workspace=dw.ln_ws if dw else None)
+                              workspace=dw.ln_ws if dw else None, rows_dev=rd)
             dres, dnew = dnew, dres
             dy = ws.dxd if dr.ra(l).p > 0 else dres
             if g is not None:
                 dw.dW(dy, ws.o[l], g.w_proj, M=M, transpose_out=True)
                 dw.db(dy, g.b_proj, M=M)
-            self._mm(dy, ws.qD, lw.w_proj, q.qw_proj, ws.do)
+            self._bmm(ws, dy, ws.qD, lw.w_proj, q.qw_proj, ws.do)
             ops.attention_bwd(ws.qkv[l], ws.do, ws.lse[l], ws.dqkv, B=B, S=S, H=H, hd=hd, scale=scale, causal=True,
-                              key_mask=causal_mask, drop=dr.attn(l), out=ws.o[l])
+                              key_mask=causal_mask, drop=dr.attn(l), out=ws.o[l], seqs=seqs)
             if g is not None:
                 dw.dW(ws.dqkv, ws.a1[l], g.w_attn, M=M, transpose_out=True)
                 dw.db(ws.dqkv, g.b_attn, M=M)
-            self._mm(ws.dqkv, ws.q3D, lw.w_attn, q.qw_attn, ws.da)
+            self._bmm(ws, ws.dqkv, ws.q3D, lw.w_attn, q.qw_attn, ws.da)
             nxt = dr.rm(l - 1) if l > 0 else dr.embd
             ops.layernorm_bwd(ws.x[l], lw.ln1_g, ws.mean1[l], ws.rstd1[l], ws.da, dnew, dres=dres, dx_drop=ws.dxd,
                               drop=nxt, dgamma=g.ln1_g if g else None, dbeta=g.ln1_b if g else None,
-                              workspace=dw.ln_ws if dw else None)
+                              workspace=dw.ln_ws if dw else None, rows_dev=rd)
             dres, dnew = dnew, dres
-        return ws.dxd if dr.embd.p > 0 else dres
+        d_in = ws.dxd if dr.embd.p > 0 else dres
+        if ws.pack:  # the prefix rows' gradient, back in the padded layout the mapper backward reads
+            ops.rows_unpack(d_in, ws.seq_off, ws.seq_len, ws.d_emb, B=B, P=ws.P, D=D, dst_bstride=S * D)
+            return ws.d_emb
+        return d_in
 
     # -- inference ----------------------------------------------------------------------------------------------
     @torch.no_grad()

@@ -150,7 +150,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None,
          alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None,
          trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None,
-         tile_only: bool = False, g256: bool = False) -> Tensor:
+         tile_only: bool = False, g256: bool = False, m_hint: Optional[int] = None) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
     workspace: fp32 split-K scratch; by default one buffer per (device, stream), so GEMMs issued on different
     streams never share slabs (gemm_workspace). The split count depends on the shape alone, so the result is
@@ -159,7 +159,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     ln: (gamma, beta, eps) — A is LayerNorm-ed over its K columns inside the GEMM (M <= 128 launches).
     alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).
     split_k: 0 = automatic split-K for launches of <= 64 output tiles, 1 = never, > 1 = forced.
-    m_dev: device int32 row count <= M (rows past it are neither computed nor stored).
+    m_dev: device int32 row count <= M (rows past it are neither computed nor stored); m_hint: its expected value
+    (kernel choice only).
     tile_only: the 128-row tile kernels only; g256: the 256 x 256 kernel wherever eligible (A/B measurements,
     path-equality tests)."""
     mx = isinstance(A, MXTensor)
@@ -206,6 +207,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
         if workspace is None else workspace
     a.workspace, a.workspace_bytes, a.split_k = ws.data_ptr(), ws.numel() * 4, split_k
     a.m_dev = _p(m_dev)
+    a.m_hint = int(m_hint) if (m_hint is not None and m_dev is not None) else 0
     a.path = 1 if tile_only else (3 if g256 else 0)
     if ln is not None:
         a.ln_gamma, a.ln_beta, a.ln_eps = ln[0].data_ptr(), ln[1].data_ptr(), float(ln[2])
@@ -257,12 +259,14 @@ GEMM_TIMER = None  # set to an object with .launch(key, flops, fn) to time every
 
 
 def layernorm_fwd(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, y: Tensor, mean: Optional[Tensor],
-                  rstd: Optional[Tensor], rows: Optional[int] = None, y_rowmap: Optional[Tensor] = None) -> Tensor:
-    """y_rowmap: int32 [rows]; row r goes to y row y_rowmap[r] (skipped when < 0)."""
+                  rstd: Optional[Tensor], rows: Optional[int] = None, y_rowmap: Optional[Tensor] = None,
+                  rows_dev: Optional[Tensor] = None) -> Tensor:
+    """y_rowmap: int32 [rows]; row r goes to y row y_rowmap[r] (skipped when < 0).
+    rows_dev: device int32 row count <= rows (packed token rows): rows past it are untouched."""
     rows = _rows(x) if rows is None else rows
     D = gamma.shape[0]
     call("icap_layernorm_fwd", dtype_code(x.dtype), rows, D, x.data_ptr(), _ld(x), gamma.data_ptr(),
-         beta.data_ptr(), eps, y.data_ptr(), _ld(y), _p(mean), _p(rstd), _p(y_rowmap), _stream())
+         beta.data_ptr(), eps, y.data_ptr(), _ld(y), _p(mean), _p(rstd), _p(y_rowmap), _p(rows_dev), _stream())
     return y
 
 
@@ -274,20 +278,22 @@ def layernorm_bwd(x: Tensor, gamma: Tensor, mean: Tensor, rstd: Tensor, dy: Tens
                   dres: Optional[Tensor] = None, dx_drop: Optional[Tensor] = None, drop: Dropout = NO_DROP,
                   dgamma: Optional[Tensor] = None, dbeta: Optional[Tensor] = None,
                   workspace: Optional[Tensor] = None, rows: Optional[int] = None,
-                  dy_rowmap: Optional[Tensor] = None) -> Tensor:
-    """dy_rowmap: int32 [rows]; dy of row r is dy row dy_rowmap[r] (zero when < 0)."""
+                  dy_rowmap: Optional[Tensor] = None, rows_dev: Optional[Tensor] = None) -> Tensor:
+    """dy_rowmap: int32 [rows]; dy of row r is dy row dy_rowmap[r] (zero when < 0). rows_dev: as layernorm_fwd."""
     rows = _rows(x) if rows is None else rows
     D = gamma.shape[0]
     call("icap_layernorm_bwd", dtype_code(x.dtype), rows, D, x.data_ptr(), _ld(x), gamma.data_ptr(),
          mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), _ld(dy), _p(dres), _ld(dres) if dres is not None else 0,
          dx.data_ptr(), _ld(dx), _p(dx_drop), drop.p, drop.seed, drop.offset, drop.ptr, _p(dgamma), _p(dbeta),
-         _p(workspace), _p(dy_rowmap), _stream())
+         _p(workspace), _p(dy_rowmap), _p(rows_dev), _stream())
     return dx
 
 
 def _attn_args(qkv: Tensor, B: int, S: int, H: int, hd: int, rsb: int, rss: int, scale: float, causal: bool,
-               key_mask: Optional[Tensor], lse: Optional[Tensor], drop: Dropout) -> AttnArgs:
+               key_mask: Optional[Tensor], lse: Optional[Tensor], drop: Dropout, seqs=None) -> AttnArgs:
     a = AttnArgs()
+    if seqs is not None:  # packed sequences: (seq_off, seq_len) int32 [B] (icap_caption_pack)
+        a.seq_off, a.seq_len = seqs[0].data_ptr(), seqs[1].data_ptr()
     a.dtype = dtype_code(qkv.dtype)
     a.B, a.S, a.H, a.hd = B, S, H, hd
     a.row_stride_b, a.row_stride_s = rsb, rss
@@ -302,8 +308,9 @@ def _attn_args(qkv: Tensor, B: int, S: int, H: int, hd: int, rsb: int, rss: int,
 
 def attention_fwd(qkv: Tensor, out: Tensor, *, B: int, S: int, H: int, hd: int, scale: float,
                   causal: bool = False, key_mask: Optional[Tensor] = None, lse: Optional[Tensor] = None,
-                  drop: Dropout = NO_DROP, rsb: Optional[int] = None, rss: int = 1) -> Tensor:
-    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop)
+                  drop: Dropout = NO_DROP, rsb: Optional[int] = None, rss: int = 1, seqs=None) -> Tensor:
+    """seqs: (seq_off, seq_len) device int32 [B] — packed sequences (include/icap.h icap_attn_args)."""
+    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop, seqs)
     a.out, a.ld_out = out.data_ptr(), _ld(out)
     call("icap_attention_fwd", C.byref(a), _stream())
     return out
@@ -311,9 +318,9 @@ def attention_fwd(qkv: Tensor, out: Tensor, *, B: int, S: int, H: int, hd: int, 
 
 def attention_bwd(qkv: Tensor, dout: Tensor, lse: Tensor, dqkv: Tensor, *, B: int, S: int, H: int, hd: int,
                   scale: float, causal: bool = False, key_mask: Optional[Tensor] = None, drop: Dropout = NO_DROP,
-                  rsb: Optional[int] = None, rss: int = 1, out: Optional[Tensor] = None) -> Tensor:
-    """out: the forward's O (optional; enables the transpose-free bf16 MFMA backward)."""
-    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop)
+                  rsb: Optional[int] = None, rss: int = 1, out: Optional[Tensor] = None, seqs=None) -> Tensor:
+    """out: the forward's O (optional; enables the transpose-free bf16 MFMA backward). seqs: as attention_fwd."""
+    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop, seqs)
     if out is not None:
         a.out, a.ld_out = out.data_ptr(), _ld(out)
     a.dout, a.ld_dout = dout.data_ptr(), _ld(dout)
@@ -402,9 +409,11 @@ class BeamState:
 
 
 def gpt2_embed(prefix: Optional[Tensor], prefix_bstride: int, wte: Tensor, wpe: Tensor, ids: Optional[Tensor],
-               x: Tensor, *, B: int, P: int, L_: int, D: int, drop: Dropout = NO_DROP) -> Tensor:
+               x: Tensor, *, B: int, P: int, L_: int, D: int, drop: Dropout = NO_DROP, seqs=None) -> Tensor:
+    """seqs: (seq_off, seq_len) — write the live tokens of each sequence at its packed rows."""
+    so, sl = (seqs[0].data_ptr(), seqs[1].data_ptr()) if seqs is not None else (None, None)
     call("icap_gpt2_embed", dtype_code(x.dtype), B, P, L_, D, _p(prefix), prefix_bstride, wte.data_ptr(),
-         wpe.data_ptr(), _p(ids), x.data_ptr(), drop.p, drop.seed, drop.offset, drop.ptr, _stream())
+         wpe.data_ptr(), _p(ids), x.data_ptr(), drop.p, drop.seed, drop.offset, drop.ptr, so, sl, _stream())
     return x
 
 
@@ -417,6 +426,32 @@ def caption_prep(B: int, P: int, L_: int, mask: Optional[Tensor], labels: Option
             raise L.IcapError("caption_prep: mask/labels must be int64")
     call("icap_caption_prep", B, P, L_, _p(mask), _p(labels), _p(key_mask), _p(labels_shift), _p(n_valid),
          _p(row_slot), _p(labels_compact), _stream())
+
+
+def caption_pack(B: int, P: int, L_: int, mask: Optional[Tensor], labels: Tensor, seq_off: Tensor, seq_len: Tensor,
+                 m_live: Tensor, key_mask: Tensor, labels_shift: Tensor, n_valid: Optional[Tensor],
+                 row_slot: Optional[Tensor] = None, labels_compact: Optional[Tensor] = None) -> None:
+    """Packed token rows of a training batch (include/icap.h icap_caption_pack): each sequence keeps its prefix
+    and caption positions up to the last loss target; offsets, lengths and the live row count on the device."""
+    for t in (mask, labels):
+        if t is not None and t.dtype != torch.int64:
+            raise L.IcapError("caption_pack: mask/labels must be int64")
+    for t in (seq_off, seq_len, m_live, key_mask, labels_shift):
+        if t.dtype != torch.int32:
+            raise L.IcapError("caption_pack: outputs must be int32")
+    call("icap_caption_pack", B, P, L_, _p(mask), _p(labels), seq_off.data_ptr(), seq_len.data_ptr(),
+         m_live.data_ptr(), key_mask.data_ptr(), labels_shift.data_ptr(), _p(n_valid), _p(row_slot),
+         _p(labels_compact), _stream())
+
+
+def rows_unpack(src: Tensor, seq_off: Tensor, seq_len: Tensor, dst: Tensor, *, B: int, P: int, D: int,
+                dst_bstride: int) -> Tensor:
+    """dst[b, t] = src[seq_off[b] + t] for the P prefix rows of each packed sequence (zero when absent)."""
+    if src.dtype != dst.dtype:
+        raise L.IcapError("rows_unpack: src and dst must share a dtype")
+    call("icap_rows_unpack", dtype_code(src.dtype), B, P, D, src.data_ptr(), seq_off.data_ptr(), seq_len.data_ptr(),
+         dst.data_ptr(), dst_bstride, _stream())
+    return dst
 
 
 def cross_entropy_workspace(rows: int) -> int:

@@ -118,6 +118,9 @@ typedef struct {
   /* i.e. K/32 * ceil(R/64) * 64 bytes. The product is sum_k a[m,k] 2^(sa-127) b[n,k] 2^(sb-127) in fp32       */
   /* (v_mfma_scale_f32_16x16x128_f8f6f4), then the same epilogue as bf16 / f32 inputs.                       */
   const uint8_t* a_scale; const uint8_t* b_scale;
+  /* m_hint (with m_dev): the expected device row count, for the kernel choice only (0: M). Any count <= M is   */
+  /* computed correctly whatever the hint; a captured graph keeps the choice made at capture.                   */
+  int64_t m_hint;
 } icap_gemm_args;
 /* MX block quantisation (the A / B operands of an ICAP_FP8_MX GEMM): x [R, K] (f32 or bf16, row stride ldx) */
 /* -> q [R, K] OCP e4m3fn bytes (row stride ldq % 16 == 0) + the E8M0 scales in icap_gemm_args.a_scale      */
@@ -143,22 +146,26 @@ int icap_gemm(const icap_gemm_args* a, void* stream);
 /* ------------------------------------------------------------------------- */
 /* y_rowmap (optional int32 [rows]): row r is stored to y row y_rowmap[r], or  */
 /* not at all when it is < 0 (gathers the LM-head target rows).                */
+/* rows_dev (optional device int32, <= rows): only rows < *rows_dev are read and written (packed token rows, */
+/* icap_caption_pack); the launch stays sized for `rows`, so one captured graph serves every count.          */
 int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
                        const float* gamma, const float* beta, float eps, void* y, int64_t ldy,
-                       float* mean, float* rstd, const int32_t* y_rowmap, void* stream);
+                       float* mean, float* rstd, const int32_t* y_rowmap, const int32_t* rows_dev,
+                       void* stream);
 /* dx = LN'(x)^T dy [+ dres];  optional dx_drop = dx * dropmask(p,seed,offset)  */
 /* (the residual-dropout backward of the producing layer, fused);             */
 /* optional dgamma/dbeta (+= into fp32 [D]) via a caller workspace of          */
 /* icap_layernorm_bwd_workspace_bytes(rows, D) bytes.                           */
 /* dy_rowmap (optional int32 [rows]): dy of row r is dy row dy_rowmap[r], or 0 */
 /* when it is < 0 (scatters the LM-head target-row gradient back).             */
+/* rows_dev: as in icap_layernorm_fwd.                                         */
 size_t icap_layernorm_bwd_workspace_bytes(int64_t rows, int64_t D);
 int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const void* x, int64_t ldx,
                        const float* gamma, const float* mean, const float* rstd,
                        const void* dy, int64_t lddy, const void* dres, int64_t lddres,
                        void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
                        uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
-                       void* workspace, const int32_t* dy_rowmap, void* stream);
+                       void* workspace, const int32_t* dy_rowmap, const int32_t* rows_dev, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Multi-head softmax attention over a fused QKV activation.                  */
@@ -186,6 +193,11 @@ typedef struct {
   /* backward only */
   const void* dout; int64_t ld_dout;
   void* dqkv; int64_t ld_dqkv;
+  /* packed (unpadded) sequences, both or neither (icap_caption_pack): sequence b has seq_len[b] <= S tokens */
+  /* at rows seq_off[b] + s (row_stride_s must be 1; row_stride_b is unused); key_mask is then indexed by    */
+  /* that packed row. lse and the dropout index keep the padded [B, H, S(, S)] numbering, so a packed and a   */
+  /* padded call draw the same masks for the same (b, h, q, k).                                                */
+  const int32_t* seq_off; const int32_t* seq_len;
 } icap_attn_args;
 int icap_attention_fwd(const icap_attn_args* a, void* stream);
 int icap_attention_bwd(const icap_attn_args* a, void* stream);
@@ -212,10 +224,13 @@ int icap_attention_decode_anc(int32_t dtype, int32_t B, int32_t H, int32_t hd, i
 /*   labels_shift[b*S+t] = t+1<S ? (t+1<P ? -100 : labels[b,t+1-P]) : -100    */
 /*   (HF/loss/loss_utils.py:49-71 shift).  S = P + L. ids/mask/labels int64.   */
 /* ------------------------------------------------------------------------- */
+/* seq_off / seq_len (optional, both or neither; icap_caption_pack): packed rows — token (b,t) goes to row   */
+/* seq_off[b] + t and only t < seq_len[b] is written (the dropout index is that row's element index).        */
 int icap_gpt2_embed(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D,
                     const void* prefix, int64_t prefix_bstride, const void* wte,
                     const void* wpe, const int64_t* ids, void* x, float drop_p,
-                    uint64_t seed, uint64_t offset, const uint64_t* seed_ptr, void* stream);
+                    uint64_t seed, uint64_t offset, const uint64_t* seed_ptr,
+                    const int32_t* seq_off, const int32_t* seq_len, void* stream);
 /* backward of the caption-token gather when GPT-2 is trained (freeze_gpt_weights=False): */
 /* dwte[ids[b,t]] += dx[b*(P+L) + P + t]  (fp32 atomics)                                    */
 int icap_embedding_scatter_add(int32_t dtype, int32_t B, int32_t P, int32_t L, int32_t D,
@@ -228,6 +243,24 @@ int icap_embedding_scatter_add(int32_t dtype, int32_t B, int32_t P, int32_t L, i
 int icap_caption_prep(int32_t B, int32_t P, int32_t L, const int64_t* mask,
                       const int64_t* labels, int32_t* key_mask, int32_t* labels_shift,
                       int32_t* n_valid, int32_t* row_slot, int32_t* labels_compact, void* stream);
+/* Packed (unpadded) token rows for the training step. A position t of caption b feeds the loss only if its  */
+/* shifted label is not -100 (loss_utils.py:32-46) or if a later such position attends to it; attention is   */
+/* causal (modeling_gpt2.py causal mask), so every position after the last target-feeding one is dead: its   */
+/* hidden states reach no loss term and no gradient (padding keys are masked out, labels -100). Only the     */
+/* live prefix of each sequence is kept:                                                                     */
+/*   seq_len[b] = max(P, 1 + last t with labels_shift[b,t] != -100), seq_off = exclusive scan, m_live = sum;  */
+/*   key_mask / labels_shift / row_slot (+ labels_compact, n_valid: as icap_caption_prep) in packed rows;     */
+/*   rows in [m_live, B*(P+L)) get key_mask 0, labels_shift -100, row_slot -1.                               */
+/* The compacted target rows come out in the same order as icap_caption_prep's, so the LM head / CE see the  */
+/* same rows; loss and gradients equal the padded computation's (within the GEMM summation order).          */
+int icap_caption_pack(int32_t B, int32_t P, int32_t L, const int64_t* mask, const int64_t* labels,
+                      int32_t* seq_off, int32_t* seq_len, int32_t* m_live, int32_t* key_mask,
+                      int32_t* labels_shift, int32_t* n_valid, int32_t* row_slot, int32_t* labels_compact,
+                      void* stream);
+/* dst[b*dst_bstride + t*D + d] = t < seq_len[b] ? src[(seq_off[b] + t)*D + d] : 0, for t < P (the prefix     */
+/* rows' gradient of a packed step back to the [B, P, D] layout the mapper backward reads). D % 4 == 0.     */
+int icap_rows_unpack(int32_t dtype, int32_t B, int32_t P, int32_t D, const void* src, const int32_t* seq_off,
+                     const int32_t* seq_len, void* dst, int64_t dst_bstride, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Causal-LM cross entropy fused with its backward (HF/loss/loss_utils.py     */

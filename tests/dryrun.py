@@ -50,6 +50,9 @@ def accesses(name, args):
         es = ES[t.dtype]
         D = t.H * t.hd
         maxrow = (t.B - 1) * t.row_stride_b + (t.S - 1) * t.row_stride_s
+        if t.seq_off:  # packed sequences: rows seq_off[b] + s < B*S (the offsets live on the device)
+            maxrow = t.B * t.S - 1
+            out += [("seq_off", t.seq_off, t.B * 4), ("seq_len", t.seq_len, t.B * 4)]
         out += [("qkv", t.qkv, (maxrow * t.ld_qkv + 3 * D) * es), ("lse", t.lse, t.B * t.H * t.S * 4),
                 ("key_mask", t.key_mask, t.B * t.S * 4), ("seed_ptr", t.seed_ptr, 8)]
         if name == "icap_attention_fwd":
@@ -64,37 +67,48 @@ def accesses(name, args):
                 ("v", t.exp_avg_sq, n * 4), ("bf16_out", t.bf16_out, n * 2), ("state", t.state, 64),
                 ("ws", a[1], ops.adamw_workspace(n))]
     elif name == "icap_layernorm_fwd":
-        dt, rows, D, x, ldx, gm, bt, _, y, ldy, mean, rstd, ymap, _s = a
+        dt, rows, D, x, ldx, gm, bt, _, y, ldy, mean, rstd, ymap, rdev, _s = a
         es = ES[dt]
         # with a row map the stored rows are the compacted slots (< n_valid <= B*L, set on the device by
         # icap_caption_prep): only the first row is checkable here
         yrows = 1 if ymap else rows
         out += [("x", x, _rows(rows, ldx, D, es)), ("gamma", gm, D * 4), ("beta", bt, D * 4),
                 ("y", y, _rows(yrows, ldy, D, es)), ("mean", mean, rows * 4), ("rstd", rstd, rows * 4),
-                ("y_rowmap", ymap, rows * 4)]
+                ("y_rowmap", ymap, rows * 4), ("rows_dev", rdev, 4)]
     elif name == "icap_layernorm_bwd":
         (dt, rows, D, x, ldx, gm, mean, rstd, dy, lddy, dres, lddres, dx, lddx, dxd, _p, _sd, _o, sp, dg, db, ws,
-         dymap, _s) = a
+         dymap, rdev, _s) = a
         es = ES[dt]
         dyrows = 1 if dymap else rows  # row map: compacted slots (see layernorm_fwd)
         out += [("x", x, _rows(rows, ldx, D, es)), ("gamma", gm, D * 4), ("mean", mean, rows * 4),
                 ("rstd", rstd, rows * 4), ("dy", dy, _rows(dyrows, lddy, D, es)),
                 ("dres", dres, _rows(rows, lddres, D, es)), ("dx", dx, _rows(rows, lddx, D, es)),
                 ("dx_drop", dxd, _rows(rows, lddx, D, es)), ("seed_ptr", sp, 8), ("dgamma", dg, D * 4),
-                ("dbeta", db, D * 4), ("dy_rowmap", dymap, rows * 4)]
+                ("dbeta", db, D * 4), ("dy_rowmap", dymap, rows * 4), ("rows_dev", rdev, 4)]
         if dg or db:
             out.append(("ws", ws, ops.layernorm_bwd_workspace(rows, D)))
     elif name == "icap_gpt2_embed":
-        dt, B, P, L, D, pre, pbs, wte, wpe, ids, x, _p, _sd, _o, sp, _s = a
+        dt, B, P, L, D, pre, pbs, wte, wpe, ids, x, _p, _sd, _o, sp, so, sl, _s = a
         es = ES[dt]
         out += [("prefix", pre, ((B - 1) * pbs + P * D) * es if P else 0), ("wte", wte, D * es),
                 ("wpe", wpe, (P + L) * D * es), ("ids", ids, B * L * 8), ("x", x, B * (P + L) * D * es),
-                ("seed_ptr", sp, 8)]
+                ("seed_ptr", sp, 8), ("seq_off", so, B * 4), ("seq_len", sl, B * 4)]
     elif name == "icap_caption_prep":
         B, P, L, mask, labels, km, ls, nv, slot, labc, _s = a
         out += [("mask", mask, B * L * 8), ("labels", labels, B * L * 8), ("key_mask", km, B * (P + L) * 4),
                 ("labels_shift", ls, B * (P + L) * 4), ("n_valid", nv, 4), ("row_slot", slot, B * (P + L) * 4),
                 ("labels_compact", labc, B * L * 4)]
+    elif name == "icap_caption_pack":
+        B, P, L, mask, labels, so, sl, ml, km, ls, nv, slot, labc, _s = a
+        n = B * (P + L)
+        out += [("mask", mask, B * L * 8), ("labels", labels, B * L * 8), ("seq_off", so, B * 4),
+                ("seq_len", sl, B * 4), ("m_live", ml, 4), ("key_mask", km, n * 4), ("labels_shift", ls, n * 4),
+                ("n_valid", nv, 4), ("row_slot", slot, n * 4), ("labels_compact", labc, B * L * 4)]
+    elif name == "icap_rows_unpack":
+        dt, B, P, D, src, so, sl, dst, dbs, _s = a
+        # src rows seq_off[b] + t < seq_off[b] + seq_len[b] <= the packed row count (checked: first row)
+        out += [("src", src, D * ES[dt]), ("seq_off", so, B * 4), ("seq_len", sl, B * 4),
+                ("dst", dst, ((B - 1) * dbs + P * D) * ES[dt])]
     elif name == "icap_cross_entropy":
         dt, rows, V, lg, ld, lab, nv, loss, dl, _g, ws, rdev, _s = a
         es = ES[dt]
