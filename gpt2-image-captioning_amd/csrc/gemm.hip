@@ -371,10 +371,88 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     }
   }
 
+  // ---- split-K combine inside the launch (p.tickets): the splits of a tile take a ticket when their K range is
+  // done; every split but the last publishes its fp32 accumulators (write-through sc1 stores, in register order: lane
+  // l of wave w stores acc[i][j] at ((w TM TN + i TN + j) 64 + l) 16 bytes of its slot) and counts itself done; the
+  // last arriver waits for that count, adds the partials in split order (its own from registers: a fixed order,
+  // so the sum is deterministic), resets the tile's two counters for the next launch, and runs the whole epilogue.
+  // Nobody waits on a block that has not taken its ticket, so there is no residency assumption
+  // (cdna_hip_programming.md §5 "In-launch split-K reduction", §6 Guideline 16 R1 with sc1 loads).
+  const bool fused = splits > 1 && p.tickets != nullptr;
+  if (fused) {
+    typedef uint32_t u32x4f_t __attribute__((ext_vector_type(4)));
+    int* sflag = reinterpret_cast<int*>(smem);
+    __syncthreads();  // every wave is done with the stage buffers (NST 1 reads them up to its last MFMA)
+    int32_t* cnt = p.tickets + 2 * (int64_t)tile;
+    if (tid == 0) sflag[0] = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int order = sflag[0];
+    constexpr uint32_t PB = (uint32_t)NW * TM * TN * 64 * 16;  // bytes of one split's partial tile
+    char* pbase = reinterpret_cast<char*>(p.workspace) + (int64_t)tile * splits * PB;
+    const uint32_t lofs = (uint32_t)((wave * TM * TN * 64 + lane) * 16);
+    if (order < splits - 1) {
+      const __amdgpu_buffer_rsrc_t rs = make_rsrc(pbase + (int64_t)split * PB, PB);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4f_t, acc[i][j]), rs,
+                                                 lofs + (uint32_t)((i * TN + j) * 1024), 0, 16 /* sc1 */);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload has left
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {
+      while (__hip_atomic_load(cnt + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < splits - 1)
+        __builtin_amdgcn_s_sleep(2);
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // every payload load below is sc1 (no stale L1 copy)
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(pbase, (uint64_t)PB * splits);
+    // the other splits' partials, GI accumulator rows at a time (all loads of a group in flight together; one row
+    // at 3-4 blocks per CU, whose register budget is 170 / 128)
+    constexpr int GI = MINB >= 3 ? 1 : 2;
+#pragma unroll
+    for (int i0 = 0; i0 < TM; i0 += GI) {
+      f32x4_t v[3][GI][TN];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        if (q < splits - 1) {
+          const int sq = q < split ? q : q + 1;  // the q-th other split, in split order
+#pragma unroll
+          for (int ii = 0; ii < GI; ++ii)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              v[q][ii][j] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                  rs, (uint32_t)sq * PB + lofs + (uint32_t)(((i0 + ii) * TN + j) * 1024), 0, 16 /* sc1 */));
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < GI; ++ii)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const f32x4_t own = acc[i0 + ii][j];
+          f32x4_t t = split == 0 ? own : v[0][ii][j];
+#pragma unroll
+          for (int pos = 1; pos < 4; ++pos) {
+            if (pos < splits) {
+              const f32x4_t x = pos < split ? v[pos][ii][j] : (pos == split ? own : v[pos - 1][ii][j]);
+              t += x;
+            }
+          }
+          acc[i0 + ii][j] = t;
+        }
+    }
+  }
+  const bool whole = splits == 1 || fused;  // this block applies the full epilogue
+
   uint64_t seed = 0;
-  if (splits == 1 && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
-  // split-K partial slab of this split: raw fp32 [M, N] (N % 4 == 0 is guaranteed by the host)
-  float* slab = splits > 1 ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
+  if (whole && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
+  // split-K partial slab of this split (separate reduce pass): raw fp32 [M, N] (N % 4 == 0 is guaranteed by the host)
+  float* slab = !whole ? reinterpret_cast<float*>(p.workspace) + (int64_t)split * M * N : nullptr;
 
   // ---- LDS-staged epilogue: each wave re-reads its accumulators EW = 8 consecutive columns per lane, so every
   // global access of the epilogue is 16 bytes (bf16) — the store tail is issue-bound (cdna_hip_programming.md T21)
@@ -389,7 +467,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   float biasw[EW];
 #pragma unroll
   for (int e = 0; e < EW; ++e) biasw[e] = 0.f;
-  if (splits == 1 && p.bias && p.dact == ICAP_ACT_NONE) {
+  if (whole && p.bias && p.dact == ICAP_ACT_NONE) {
 #pragma unroll
     for (int e = 0; e < EW; ++e) biasw[e] = (col + e < N) ? p.bias[col + e] : 0.f;
   }
@@ -421,7 +499,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     __builtin_amdgcn_sched_barrier(0);  // keep the loads here: hipcc would sink each to its use
   };
   if constexpr (std::is_same<TC, bf16_t>::value) {
-    if (splits == 1) {
+    if (whole) {
       if (ACT && p.dact != ICAP_ACT_NONE) {
         esrc = reinterpret_cast<const bf16_t*>(p.dact_src);
         eld = p.ld_dact;
@@ -475,7 +553,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       __syncthreads();
       static_for<0, EPR / RPI>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        store_row(h, t, fullw ? &pre[(h % HPG) * (EPR / RPI) + t] : nullptr);
+        store_row(h, t, (want_pre && fullw) ? &pre[(h % HPG) * (EPR / RPI) + t] : nullptr);
       });
       __syncthreads();
     });
@@ -902,6 +980,7 @@ struct GemmPlan {
   int sku = 3;           // skinny: k-steps in flight per wave
   int variant = 0;       // tile kernel (see ICAP_GEMM_LAUNCH)
   int splits = 1, nk_split = 0, tiles_n = 0;
+  bool fused = false;    // split-K combined inside the launch (tickets), no reduce pass
   bool act = true;       // tile kernels: the instantiation with the activation epilogue compiled in
   dim3 grid, block;
   uint32_t thr = 0;
@@ -983,12 +1062,31 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
     return ICAP_OK;
   }
   // split-K over K stages for launches that cannot fill the chip (decode-time M = batch, small projections):
-  // fp32 partial slabs in the caller's workspace + one deterministic reduce/epilogue pass.
+  // fp32 partial slabs in the caller's workspace + one deterministic reduce/epilogue pass — or, with tickets, the
+  // in-launch combine (long K over fewer tiles than CUs: the packed step's N = 768 products, the mapper's M = 3200
+  // products and weight gradients): S = 2 * CUs / tiles rounded, 2..4, so the tile x split blocks fill the chip
+  // about twice, and no slab round trip or extra launch.
   const int64_t bke = 128 / es;
   const int64_t nk = (p.K + bke - 1) / bke;
   const int64_t slab = p.M * p.N * (int64_t)sizeof(float);
+  const int64_t cus = device_cus();
+  // with a device row count the kernel choice follows the expected count (m_hint)
+  const int64_t m_plan = (p.m_dev && p.m_hint > 0 && p.m_hint < p.M) ? p.m_hint : p.M;
+  const int64_t tiles_plan = ((m_plan + GBM - 1) / GBM) * tiles_n;
   int64_t splits = 1;
-  if (p.split_k > 1) {
+  pl.fused = false;
+  if (p.split_k == 0 && p.tickets && p.workspace && (p.N & 3) == 0 && nk >= 24 && tiles_plan < cus) {
+    int64_t sf = (2 * cus + tiles_plan / 2) / tiles_plan;
+    if (sf > 4) sf = 4;
+    while (sf > 2 && nk / sf < 8) --sf;
+    const int64_t pbytes = (int64_t)GBM * GBN * (int64_t)sizeof(float);
+    if (sf >= 2 && p.tickets_len >= 2 * tiles && p.workspace_bytes >= tiles * sf * pbytes) {
+      splits = sf;
+      pl.fused = true;
+    }
+  }
+  if (pl.fused) {
+  } else if (p.split_k > 1) {
     splits = p.split_k;
   } else if (p.split_k == 0 && p.workspace && (p.N & 3) == 0 && nk >= 2 && (tiles <= 64 || (tiles < 256 && nk >= 16))) {
     // the count depends on the shape alone — never on the workspace a caller passes — so a product computed on
@@ -1002,12 +1100,15 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   if (splits < 1) splits = 1;
   const int64_t nk_split = nk > 0 ? (nk + splits - 1) / splits : 0;
   if (nk_split > 0) splits = (nk + nk_split - 1) / nk_split;  // every split gets >= 1 stage
-  if (splits > 1) {
+  if (splits > 1 && !pl.fused) {
     ICAP_REQUIRE((p.N & 3) == 0, "icap_gemm: split-K requires N % 4 == 0");
     ICAP_REQUIRE(p.workspace && (reinterpret_cast<uintptr_t>(p.workspace) & 15) == 0 &&
                      p.workspace_bytes >= splits * slab,
                  "icap_gemm: split-K workspace missing, misaligned or too small");
   }
+  if (pl.fused)
+    ICAP_REQUIRE((reinterpret_cast<uintptr_t>(p.workspace) & 15) == 0 && (reinterpret_cast<uintptr_t>(p.tickets) & 7) == 0,
+                 "icap_gemm: split-K workspace / tickets misaligned");
   // Short-K launches (<= 16 stages) of fewer than 4 tiles of 128 x 128 per CU (the N = 768 products, the mapper's
   // M = 3200 and CLIP's M = 6400 ones) run faster on 128 x 64 tiles: twice the blocks, so a CU holds more of them
   // to hide each one's prologue / epilogue; longer K keeps 128 x 128 (profiles/r01_gemm_narrow.txt).
@@ -1015,12 +1116,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   pl.splits = (int)splits;
   pl.nk_split = (int)nk_split;
   pl.variant = gemm_variant(p, nk_split);
-  // Long K over about one 128 x 128 tile per CU (the packed step's N = 768 products: M_live ~ 3600 -> 168 tiles):
-  // the 4-stage ring at one block per CU (the double-buffered loop at 2 blocks per CU only pays when a CU holds two
-  // tiles). With a device row count the choice follows the expected count (m_hint).
-  const int64_t m_plan = (p.m_dev && p.m_hint > 0 && p.m_hint < p.M) ? p.m_hint : p.M;
-  const int64_t tiles_plan = ((m_plan + GBM - 1) / GBM) * tiles_n;
-  if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 && nk_split > 16 && tiles_plan * 4 <= (int64_t)device_cus() * 5)
+  // Long K over at most one 128 x 128 tile per CU and no split (no tickets given): the 4-stage ring at one block per
+  // CU (the double-buffered loop at 2 blocks per CU only pays when a CU holds two tiles).
+  if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 && nk_split > 16 && tiles_plan <= cus)
     pl.variant = 16;
   if (mx && pl.variant == 5) pl.variant = 4;  // MX at 4 blocks / CU (128 VGPRs) spills: 3 blocks / CU
   if (narrow) {
@@ -1030,7 +1128,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   }
   if (p.trans_ab) pl.variant = nk_split > 16 ? 14 : 15;  // K-outer forms of variants 0 / 4
   pl.tiles_n = (int)tiles_n;
-  pl.act = splits == 1 && (p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE);
+  pl.act = (splits == 1 || pl.fused) && (p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE);
   pl.block = dim3(GNT);
   pl.grid = dim3((unsigned)(tiles * splits));
   return ICAP_OK;
@@ -1070,13 +1168,27 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
   return buf;
 }
 
+extern "C" int icap_gemm_plan_info(const icap_gemm_args* a, int32_t* splits, int32_t* fused) {
+  ICAP_REQUIRE(a != nullptr && splits != nullptr && fused != nullptr, "icap_gemm_plan_info: null pointer");
+  GemmPlan pl;
+  const int rc = gemm_plan(*a, pl);
+  if (rc != ICAP_OK) return rc;
+  *splits = pl.skinny || pl.g256 ? 1 : pl.splits;
+  *fused = pl.fused ? 1 : 0;
+  return ICAP_OK;
+}
+
 extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   ICAP_REQUIRE(a != nullptr, "icap_gemm: null args");
-  const icap_gemm_args& p = *a;
-  if (p.M == 0 || p.N == 0) return ICAP_OK;
+  if (a->M == 0 || a->N == 0) return ICAP_OK;
   GemmPlan pl;
-  const int prc = gemm_plan(p, pl);
+  const int prc = gemm_plan(*a, pl);
   if (prc != ICAP_OK) return prc;
+  // the kernels take the in-launch combine exactly when tickets reach them: only for the plan that chose it (a
+  // reduce-pass split must write its slabs, whatever the caller passed)
+  icap_gemm_args pk = *a;
+  if (!pl.fused) pk.tickets = nullptr;
+  const icap_gemm_args& p = pk;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const uint32_t thr = pl.thr;
   const float inv_keep = pl.inv_keep;
@@ -1165,7 +1277,7 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   }
 #undef ICAP_GEMM_LAUNCH
 #undef ICAP_GK
-  if (sp > 1) {
+  if (sp > 1 && !pl.fused) {
     if (p.c_dtype == ICAP_BF16)
       hipLaunchKernelGGL((gemm_splitk_reduce<bf16_t>), rgrid, dim3(256), 0, s, p, sp, thr, inv_keep);
     else

@@ -47,6 +47,7 @@ class GemmArgs(C.Structure):
         ("path", i32),
         ("a_scale", vp), ("b_scale", vp),
         ("m_hint", i64),
+        ("tickets", vp), ("tickets_len", i64),
     ]
 
 
@@ -101,6 +102,7 @@ SIGNATURES = {
     "icap_device_arch_ok": (C.c_int, []),
     "icap_gemm": (C.c_int, [C.POINTER(GemmArgs), vp]),
     "icap_gemm_kernel_name": (C.c_char_p, [C.POINTER(GemmArgs)]),
+    "icap_gemm_plan_info": (C.c_int, [C.POINTER(GemmArgs), vp, vp]),
     "icap_mx_scale_bytes": (sz, [i64, i64]),
     "icap_quantize_mx": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, vp, vp, vp]),
     "icap_layernorm_fwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, f32, vp, i64, vp, vp, vp, vp, vp]),

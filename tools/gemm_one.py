@@ -22,12 +22,13 @@ def main():
     A = (torch.rand((M, K), generator=g) * 2 - 1).to(dev, torch.bfloat16)
     B = (torch.rand((N, K), generator=g) * 2 - 1).to(dev, torch.bfloat16)
     C = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-    ops.gemm(A, B, C)
+    kw = dict(g256=True, split_k=1) if os.environ.get("GEMM_G256") == "1" else {}
+    ops.gemm(A, B, C, **kw)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        ops.gemm(A, B, C)
+        ops.gemm(A, B, C, **kw)
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / reps * 1e3
