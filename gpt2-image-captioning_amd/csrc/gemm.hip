@@ -1075,7 +1075,10 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   const int64_t tiles_plan = ((m_plan + GBM - 1) / GBM) * tiles_n;
   int64_t splits = 1;
   pl.fused = false;
-  if (p.split_k == 0 && p.tickets && p.workspace && (p.N & 3) == 0 && nk >= 24 && tiles_plan < cus) {
+  // (not for the K-outer weight-gradient products: measured, their in-launch combine ran 6-7 µs slower than the
+  // slab + reduce pass — 768x3072x3200 53 vs 47 µs, profiles/r03_gemm_detail_fused.txt — since the last arriver of
+  // a 3-block-per-CU tile reads its partials one accumulator row at a time)
+  if (p.split_k == 0 && p.tickets && p.workspace && !p.trans_ab && (p.N & 3) == 0 && nk >= 24 && tiles_plan < cus) {
     int64_t sf = (2 * cus + tiles_plan / 2) / tiles_plan;
     if (sf > 4) sf = 4;
     while (sf > 2 && nk / sf < 8) --sf;
