@@ -971,6 +971,17 @@ static bool g256_pick(const icap_gemm_args& p) {
 
 static bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
+// A/B switches for the in-launch split-K (read once): ICAP_FUSED_S = forced split count, ICAP_FUSED_NST = 1 gives
+// its K ranges the variant rule (default: the double-buffered kernel)
+static int fused_s_override() {
+  static const int v = [] { const char* e = getenv("ICAP_FUSED_S"); return e ? atoi(e) : 0; }();
+  return v;
+}
+static int fused_nst_override() {
+  static const int v = [] { const char* e = getenv("ICAP_FUSED_NST"); return e ? atoi(e) : 0; }();
+  return v;
+}
+
 namespace {
 // What icap_gemm launches for one call (shared by the launcher and icap_gemm_kernel_name).
 struct GemmPlan {
@@ -1082,6 +1093,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
     int64_t sf = (2 * cus + tiles_plan / 2) / tiles_plan;
     if (sf > 4) sf = 4;
     while (sf > 2 && nk / sf < 8) --sf;
+    if (fused_s_override() > 1) sf = fused_s_override();  // A/B measurements only (ICAP_FUSED_S)
     const int64_t pbytes = (int64_t)GBM * GBN * (int64_t)sizeof(float);
     if (sf >= 2 && p.tickets_len >= 2 * tiles && p.workspace_bytes >= tiles * sf * pbytes) {
       splits = sf;
@@ -1119,6 +1131,10 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   pl.splits = (int)splits;
   pl.nk_split = (int)nk_split;
   pl.variant = gemm_variant(p, nk_split);
+  // in-launch split-K: the double-buffered main loop at 2 blocks per CU for every split's K range (measured on the
+  // packed 3584 x 768 x 3072 / x 2304 products: 36.6 / 30.4 vs 40.1 / 32.4 µs with the single-stage form the
+  // per-split K of 16 stages would pick; profiles/r03_fused_ab.txt); ICAP_FUSED_NST=1 restores the variant rule
+  if (pl.fused && fused_nst_override() != 1) pl.variant = 0;
   // Long K over at most one 128 x 128 tile per CU and no split (no tickets given): the 4-stage ring at one block per
   // CU (the double-buffered loop at 2 blocks per CU only pays when a CU holds two tiles).
   if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 && nk_split > 16 && tiles_plan <= cus)
