@@ -226,6 +226,7 @@ class ClipCore:
         ws.qkv = e(M, 3 * D)
         ws.f = e(M, c.intermediate_size)
         ws.pooled = e(B, D)
+        ws.xc = e(B, D)  # the last layer's CLS rows (see run)
         ws.feat = e(B, c.projection_dim)
         ws.emb = e(B, c.projection_dim, dtype=torch.float32)
         ws.feat32 = e(B, c.projection_dim, dtype=torch.float32)
@@ -241,15 +242,27 @@ class ClipCore:
         ops.vit_embed(ws.pe, self.cls, self.pos, ws.h1, B, self.G * self.G, D)
         ops.layernorm_fwd(ws.h1, self.pre[0], self.pre[1], eps, ws.x, None, None)
         scale = self.hd ** -0.5
-        for w in self.layers:
+        nl = len(self.layers)
+        for i, w in enumerate(self.layers):
             ops.layernorm_fwd(ws.x, w.ln1[0], w.ln1[1], eps, ws.a, None, None)
             ops.gemm(ws.a, w.qkv_w, ws.qkv, bias=w.qkv_b)
             ops.attention_fwd(ws.qkv, ws.o, B=B, S=self.S, H=self.H, hd=self.hd, scale=scale, causal=False)
+            if i == nl - 1:
+                # last layer: only the CLS rows reach the output (pooler_output = post_layernorm(last_hidden[:, 0]),
+                # modeling_clip.py:741-752), so the rows past attention — out_proj, LayerNorm 2, the MLP — run on the
+                # B CLS rows alone (strided views: row b at b*S*D); every other token's keys / values were used above
+                o_c, x_c = ws.o.view(B, self.S * D)[:, :D], ws.x.view(B, self.S * D)[:, :D]
+                h1, a, f = ws.h1[:B], ws.a[:B], ws.f[:B]
+                ops.gemm(o_c, w.out_w, h1, bias=w.out_b, resid=x_c)
+                ops.layernorm_fwd(h1, w.ln2[0], w.ln2[1], eps, a, None, None)
+                ops.gemm(a, w.fc1_w, f, bias=w.fc1_b, act=L.ACT_QUICK_GELU)
+                ops.gemm(f, w.fc2_w, ws.xc, bias=w.fc2_b, resid=h1)
+                break
             ops.gemm(ws.o, w.out_w, ws.h1, bias=w.out_b, resid=ws.x)
             ops.layernorm_fwd(ws.h1, w.ln2[0], w.ln2[1], eps, ws.a, None, None)
             ops.gemm(ws.a, w.fc1_w, ws.f, bias=w.fc1_b, act=L.ACT_QUICK_GELU)
             ops.gemm(ws.f, w.fc2_w, ws.x, bias=w.fc2_b, resid=ws.h1)
-        cls_rows = ws.x.view(B, self.S * D)[:, :D]  # CLS token of every image
+        cls_rows = ws.xc  # CLS token of every image after the last layer
         ops.layernorm_fwd(cls_rows, self.post[0], self.post[1], eps, ws.pooled, None, None, rows=B)
         ops.gemm(ws.pooled, self.w_proj, ws.feat32)
         ops.l2norm_rows(ws.feat32, ws.emb)
