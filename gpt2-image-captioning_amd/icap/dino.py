@@ -336,6 +336,7 @@ class DinoCore:
         ws.qkv = e(M, 3 * D)
         ws.f = e(M, c.intermediate_size)
         ws.cls = e(B, D)
+        ws.xc = e(B, D)  # the last layer's CLS rows (see run)
         ws.pool = e(B, D, dtype=torch.float32)
         ws.emb = e(B, D, dtype=torch.float32)
         self._ws = {B: ws}  # keep only the latest batch size
@@ -349,16 +350,28 @@ class DinoCore:
         ops.gemm(ws.patches, self.w_patch, ws.pe, bias=self.b_patch)  # Conv2d(stride=patch, bias) as a GEMM
         ops.prefix_embed(ws.pe, self.prefix, ws.x, B, self.G * self.G, D)  # [CLS || registers || patches]
         scale = self.hd ** -0.5
-        for w in self.layers:
+        nl = len(self.layers)
+        for i, w in enumerate(self.layers):
             ops.layernorm_fwd(ws.x, w.ln1[0], w.ln1[1], eps, ws.a, None, None)
             ops.gemm(ws.a, w.qkv_w, ws.qkv, bias=w.qkv_b)
             ops.rope_patches(ws.qkv, self.cos, self.sin, B=B, S=S, NP=self.NP, H=self.H, hd=self.hd)
             ops.attention_fwd(ws.qkv, ws.o, B=B, S=S, H=self.H, hd=self.hd, scale=scale, causal=False)
+            if i == nl - 1:
+                # last layer: pooler_output is the normed CLS row (modeling_dinov3_vit.py:540-541), so past attention
+                # the layer runs on the B CLS rows (strided views, row b at b*S*D); the registers' and patches' keys /
+                # values were used above
+                o_c, x_c = ws.o.view(B, S * D)[:, :D], ws.x.view(B, S * D)[:, :D]
+                h1, a, f = ws.h1[:B], ws.a[:B], ws.f[:B]
+                ops.gemm(o_c, w.o_w, h1, bias=w.o_b, resid=x_c)
+                ops.layernorm_fwd(h1, w.ln2[0], w.ln2[1], eps, a, None, None)
+                ops.gemm(a, w.up_w, f, bias=w.up_b, act=L.ACT_GELU_ERF)
+                ops.gemm(f, w.down_w, ws.xc, bias=w.down_b, resid=h1)
+                break
             ops.gemm(ws.o, w.o_w, ws.h1, bias=w.o_b, resid=ws.x)
             ops.layernorm_fwd(ws.h1, w.ln2[0], w.ln2[1], eps, ws.a, None, None)
             ops.gemm(ws.a, w.up_w, ws.f, bias=w.up_b, act=L.ACT_GELU_ERF)
             ops.gemm(ws.f, w.down_w, ws.x, bias=w.down_b, resid=ws.h1)
-        cls_rows = ws.x.view(B, S * D)[:, :D]  # pooler_output = the normed CLS row (modeling_dinov3_vit.py:540-541)
+        cls_rows = ws.xc  # CLS token of every image after the last layer
         ops.layernorm_fwd(cls_rows, self.lnf[0], self.lnf[1], eps, ws.cls, None, None, rows=B)
         if ws.cls.dtype == torch.float32:
             ws.pool.copy_(ws.cls)

@@ -255,6 +255,7 @@ class ViTCore:
         ws.qkv = e(M, 3 * D)
         ws.f = e(M, c.intermediate_size)
         ws.cls = e(B, D)
+        ws.xc = e(B, D)  # the last layer's CLS rows (see run)
         ws.pool = e(B, D, dtype=torch.float32)
         ws.emb = e(B, D, dtype=torch.float32)
         self._ws = {B: ws}  # keep only the latest batch size
@@ -268,15 +269,26 @@ class ViTCore:
         ops.gemm(ws.patches, self.w_patch, ws.pe, bias=self.b_patch)  # Conv2d(stride=patch, bias) as a GEMM
         ops.vit_embed(ws.pe, self.cls, self.pos, ws.x, B, self.G * self.G, D)  # [CLS || patches] + positions
         scale = self.hd ** -0.5
-        for w in self.layers:
+        nl = len(self.layers)
+        for i, w in enumerate(self.layers):
             ops.layernorm_fwd(ws.x, w.ln1[0], w.ln1[1], eps, ws.a, None, None)
             ops.gemm(ws.a, w.qkv_w, ws.qkv, bias=w.qkv_b)
             ops.attention_fwd(ws.qkv, ws.o, B=B, S=self.S, H=self.H, hd=self.hd, scale=scale, causal=False)
+            if i == nl - 1:
+                # last layer: the pooler reads token 0 only (modeling_vit.py:289-301), so past attention the layer
+                # runs on the B CLS rows (strided views, row b at b*S*D); the other tokens' keys / values were used
+                o_c, x_c = ws.o.view(B, self.S * D)[:, :D], ws.x.view(B, self.S * D)[:, :D]
+                h1, a, f = ws.h1[:B], ws.a[:B], ws.f[:B]
+                ops.gemm(o_c, w.out_w, h1, bias=w.out_b, resid=x_c)
+                ops.layernorm_fwd(h1, w.ln2[0], w.ln2[1], eps, a, None, None)
+                ops.gemm(a, w.fc1_w, f, bias=w.fc1_b, act=L.ACT_GELU_ERF)
+                ops.gemm(f, w.fc2_w, ws.xc, bias=w.fc2_b, resid=h1)
+                break
             ops.gemm(ws.o, w.out_w, ws.h1, bias=w.out_b, resid=ws.x)
             ops.layernorm_fwd(ws.h1, w.ln2[0], w.ln2[1], eps, ws.a, None, None)
             ops.gemm(ws.a, w.fc1_w, ws.f, bias=w.fc1_b, act=L.ACT_GELU_ERF)
             ops.gemm(ws.f, w.fc2_w, ws.x, bias=w.fc2_b, resid=ws.h1)
-        cls_rows = ws.x.view(B, self.S * D)[:, :D]  # the pooler reads token 0 only (modeling_vit.py:289-301)
+        cls_rows = ws.xc  # CLS token of every image after the last layer
         ops.layernorm_fwd(cls_rows, self.lnf[0], self.lnf[1], eps, ws.cls, None, None, rows=B)
         ops.gemm(ws.cls, self.w_pool, ws.pool, bias=self.b_pool, act=L.ACT_TANH)
         ops.l2norm_rows(ws.pool, ws.emb)
