@@ -1103,6 +1103,12 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   if (pl.fused) {
   } else if (p.split_k > 1) {
     splits = p.split_k;
+  } else if (p.split_k == 0 && p.workspace && p.trans_ab && (p.N & 3) == 0 && nk >= 16 && tiles < 320) {
+    // K-outer weight gradients over the token rows (the mapper's 3200-row products): about 320 blocks, at most 6
+    // splits — measured 31.8 / 23.3 / 35.4 / 35.8 us for 2304x768 / 768x768 / 3072x768 / 768x3072 over 3200 rows
+    // against 33.9 / 24.7 / 40.3 / 40.2 with the 512-block rule below (profiles/r03_dw_bench.txt)
+    splits = (320 + tiles - 1) / tiles;
+    if (splits > 6) splits = 6;
   } else if (p.split_k == 0 && p.workspace && (p.N & 3) == 0 && nk >= 2 && (tiles <= 64 || (tiles < 256 && nk >= 16))) {
     // the count depends on the shape alone — never on the workspace a caller passes — so a product computed on
     // another stream with its own scratch sums its K ranges in the same order and rounds identically (a
