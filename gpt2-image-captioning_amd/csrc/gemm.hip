@@ -720,7 +720,11 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   __shared__ float lnp2[SK_WAVES][BM];
   // (instantiations with few fragment registers only: the others would spill; LN-fused launches have K = D)
   constexpr bool LN_FRAG = ES == 2 && SKU * (MT + NT) <= 24;
-  const bool ln_frag = LN_FRAG && fuse_ln && nks <= (int64_t)SK_WAVES * SKU;
+  // folded LayerNorm (icap_gemm_args.ln_wsum): the same row statistics, but only the epilogue needs them
+  // (C = rstd (A.B^T - mean wsum) + bias), so the MFMAs run on the raw fragments without waiting for them: the
+  // wave partials go to LDS here and are summed by the epilogue threads after the partial-tile reduction barrier
+  const bool fold = p.ln_wsum != nullptr;
+  const bool ln_frag = LN_FRAG && (fuse_ln || fold) && nks <= (int64_t)SK_WAVES * SKU;
   float ln_mean[MT], ln_rs[MT];
   if (LN_FRAG && ln_frag) {
     // one pass over the fragments: per-row sums of (x - x0) and (x - x0)^2 with x0 the row's first element (the
@@ -756,23 +760,26 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
       if (fg == 0) {
         lnp[wave][i * 16 + fr] = part[i];
         lnp2[wave][i * 16 + fr] = part2[i];
+        if (fold && wave == 0) ln_mr[i * 16 + fr][0] = x0[i];
       }
     }
-    __syncthreads();
+    if (fuse_ln) {  // (fold: the partials are published by the reduction barrier below)
+      __syncthreads();
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      float t = 0.f, t2 = 0.f;
+      for (int i = 0; i < MT; ++i) {
+        float t = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < SK_WAVES; ++w) {
-        t += lnp[w][i * 16 + fr];
-        t2 += lnp2[w][i * 16 + fr];
+        for (int w = 0; w < SK_WAVES; ++w) {
+          t += lnp[w][i * 16 + fr];
+          t2 += lnp2[w][i * 16 + fr];
+        }
+        const float dm = t / (float)K;
+        ln_mean[i] = x0[i] + dm;
+        const float var = t2 / (float)K - dm * dm;
+        ln_rs[i] = 1.f / sqrtf((var > 0.f ? var : 0.f) + p.ln_eps);
       }
-      const float dm = t / (float)K;
-      ln_mean[i] = x0[i] + dm;
-      const float var = t2 / (float)K - dm * dm;
-      ln_rs[i] = 1.f / sqrtf((var > 0.f ? var : 0.f) + p.ln_eps);
     }
-  } else if (fuse_ln) {
+  } else if (fuse_ln || fold) {
     const int t = threadIdx.x & 15;
     for (int rr = threadIdx.x >> 4; rr < BM; rr += 64 * SK_WAVES / 16) {
       const int64_t row = m0 + rr < M ? m0 + rr : M - 1;
@@ -876,6 +883,26 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   for (int w = 1; w < HALF; ++w) {
     const float4 v = *reinterpret_cast<const float4*>(&red[w][er * RLD + ec]);
     x[0] += v.x; x[1] += v.y; x[2] += v.z; x[3] += v.w;
+  }
+  if (fold) {  // rstd (acc - mean wsum); the host passed bias = b + W . beta
+    float mean, rs;
+    if (ln_frag) {  // the wave partials in wave order (the order of the LN-fused form above)
+      float t = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < SK_WAVES; ++w) {
+        t += lnp[w][er];
+        t2 += lnp2[w][er];
+      }
+      const float dm = t / (float)K;
+      mean = ln_mr[er][0] + dm;
+      const float var = t2 / (float)K - dm * dm;
+      rs = 1.f / sqrtf((var > 0.f ? var : 0.f) + p.ln_eps);
+    } else {
+      mean = ln_mr[er][0];
+      rs = ln_mr[er][1];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = ecol + e < N ? rs * (x[e] - mean * p.ln_wsum[ecol + e]) : x[e];
   }
   // two call sites rather than a selected pointer (a pointer select on a local puts it in scratch)
   if (use_pre) epiw<TC, 4>(p, erow, ecol, x, bias4, ecol + 4 <= N, seed, drop_thresh, inv_keep, &pre);
@@ -1047,7 +1074,10 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   const bool fuse_ln = p.ln_gamma != nullptr;
   ICAP_REQUIRE(!fuse_ln || (p.ln_beta && p.M <= 128 && p.split_k == 0 && !p.trans_ab && p.K <= 4096),
                "icap_gemm: ln_gamma needs ln_beta, M <= 128, K <= 4096, no split_k / trans_ab");
-  if (p.M <= 128 && p.split_k == 0 && (tiles <= 128 || fuse_ln) && !p.trans_ab && !mx) {
+  const bool fold_ln = p.ln_wsum != nullptr;
+  ICAP_REQUIRE(!fold_ln || (!fuse_ln && p.M <= 128 && p.split_k == 0 && !p.trans_ab && !mx && p.K <= 4096),
+               "icap_gemm: ln_wsum needs M <= 128, no ln_gamma / split_k / trans_ab / FP8_MX, K <= 4096");
+  if (p.M <= 128 && p.split_k == 0 && (tiles <= 128 || fuse_ln || fold_ln) && !p.trans_ab && !mx) {
     pl.skinny = true;
     // the fewest 16-column slabs per block that keep the grid within one pass over the CUs (every CU streams one
     // block's A rows + W slab; a second block on a CU doubles its bytes), then enough k-steps in flight per wave

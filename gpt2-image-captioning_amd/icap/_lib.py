@@ -48,6 +48,7 @@ class GemmArgs(C.Structure):
         ("a_scale", vp), ("b_scale", vp),
         ("m_hint", i64),
         ("tickets", vp), ("tickets_len", i64),
+        ("ln_wsum", vp),
     ]
 
 

@@ -12,6 +12,7 @@ explicit kernel schedules (no autograd, no torch compute).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from types import SimpleNamespace
 from typing import List, Optional
@@ -23,6 +24,10 @@ from . import _lib as L
 from . import ops
 from .ops import Dropout
 from .weights import det_tensor
+
+# decode steps (M <= 128) of a frozen GPT-2: ln_1 / ln_2 folded into the QKV / c_fc weights (GPT2Core._fold_ln);
+# ICAP_LN_FOLD=0 keeps the LayerNorm-fused GEMMs (A/B measurements)
+LN_FOLD = os.environ.get("ICAP_LN_FOLD", "1") != "0"
 
 Tensor = torch.Tensor
 
@@ -277,6 +282,12 @@ class GPT2Core:
             self.wpe = torch.empty_like(t.wpe.weight.data, dtype=self.dtype)
             ops.convert(t.wpe.weight.data, self.wpe)
         self.eps = self.cfg.layer_norm_epsilon
+        if LN_FOLD:  # decode: ln_1 / ln_2 folded into the QKV / c_fc weights (frozen weights: once)
+            for blk, lw in zip(t.h, self.layers):
+                lw.wf_attn_t, lw.ws_attn, lw.bf_attn = self._fold_ln(blk.attn.c_attn.weight.data, lw.ln1_g,
+                                                                     lw.ln1_b, lw.b_attn)
+                lw.wf_fc_t, lw.ws_fc, lw.bf_fc = self._fold_ln(blk.mlp.c_fc.weight.data, lw.ln2_g, lw.ln2_b,
+                                                               lw.b_fc)
         if self.fp8:  # MX e4m3 copies of every frozen product's weight operand, both orientations
             for lw in self.layers:
                 for nm in ("w_attn", "w_proj", "w_fc", "w_mp"):
@@ -284,6 +295,30 @@ class GPT2Core:
                     setattr(lw, "q" + nm, ops.quantize_mx(getattr(lw, nm)))
             self.qwte = ops.quantize_mx(self.wte)
             self.qwte_t = ops.quantize_mx(self.wte_t)
+
+    def _fold_ln(self, w: Tensor, gamma: Tensor, beta: Tensor, bias: Tensor):
+        """LayerNorm(x) . W + b = rstd (x . (W*gamma) - mean * wsum) + (b + beta . W) for a Conv1D master w [in,out]
+        (fp32): returns (W*gamma as [out,in] in the compute dtype, wsum [out] = row sums of those stored values,
+        b + beta . W [out]), all fp32 arithmetic on the MFMA GEMM (W*gamma = W^T . diag(gamma): one nonzero
+        product per output, exact before the rounding to the compute dtype)."""
+        nin, nout = w.shape
+        wt = torch.empty((nout, nin), dtype=torch.float32, device=self.dev)
+        ops.transpose(w, wt)
+        dg = torch.zeros((nin, nin), dtype=torch.float32, device=self.dev)
+        dg.view(-1)[:: nin + 1].copy_(gamma)
+        wg = torch.empty((nout, nin), dtype=torch.float32, device=self.dev)
+        ops.gemm(wt, dg, wg, split_k=1)
+        if self.dtype == torch.float32:
+            wf = wg
+        else:
+            wf = torch.empty((nout, nin), dtype=self.dtype, device=self.dev)
+            ops.convert(wg, wf)
+        ones = torch.ones((1, nin), dtype=self.dtype, device=self.dev)
+        wsum = torch.empty((1, nout), dtype=torch.float32, device=self.dev)
+        ops.gemm(ones, wf, wsum, split_k=1)
+        bf = torch.empty((1, nout), dtype=torch.float32, device=self.dev)
+        ops.gemm(beta.reshape(1, nin).contiguous(), wt, bf, bias=bias, split_k=1)
+        return wf, wsum.view(nout), bf.view(nout)
 
     @torch.no_grad()
     def bind_flat(self, flat) -> None:
@@ -296,6 +331,7 @@ class GPT2Core:
             raise L.IcapError("fp8_mx is the frozen-GPT-2 path (weights quantised once); train GPT-2 in bf16")
         t = self.model.transformer
         for blk, lw in zip(t.h, self.layers):
+            lw.wf_attn_t = lw.wf_fc_t = None  # trained weights: decode keeps ln_1 / ln_2 in the GEMMs (no fold)
             lw.w_attn, lw.w_proj = flat.view_c(blk.attn.c_attn.weight), flat.view_c(blk.attn.c_proj.weight)
             lw.w_fc, lw.w_mp = flat.view_c(blk.mlp.c_fc.weight), flat.view_c(blk.mlp.c_proj.weight)
             lw.b_attn, lw.b_proj = blk.attn.c_attn.bias.data, blk.attn.c_proj.bias.data
@@ -602,7 +638,10 @@ class GPT2Core:
         for l, lw in enumerate(self.layers):
             q = lw if mx else nq
             qkv = ds.cache[l][pos0 * B: (pos0 + npos) * B]
-            if fuse_ln:
+            fold = fuse_ln and getattr(lw, "wf_attn_t", None) is not None
+            if fold:
+                ops.gemm(x, lw.wf_attn_t, qkv, bias=lw.bf_attn, M=rows, ln_fold=(lw.ws_attn, self.eps))
+            elif fuse_ln:
                 ops.gemm(x, lw.w_attn_t, qkv, bias=lw.b_attn, M=rows, ln=(lw.ln1_g, lw.ln1_b, self.eps))
             else:
                 ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, a, None, None, rows=rows)
@@ -613,7 +652,9 @@ class GPT2Core:
                 ops.attention_decode(ds.cache[l], o, B=B, H=H, hd=hd, pos=pos0, scale=scale,
                                      anc=getattr(ds, "anc", None))
             self._mm(o, qD, lw.w_proj_t, q.qw_proj_t, h1, bias=lw.b_proj, resid=x, M=rows)
-            if fuse_ln:
+            if fold:
+                ops.gemm(h1, lw.wf_fc_t, f, bias=lw.bf_fc, act=L.ACT_GELU_NEW, M=rows, ln_fold=(lw.ws_fc, self.eps))
+            elif fuse_ln:
                 ops.gemm(h1, lw.w_fc_t, f, bias=lw.b_fc, act=L.ACT_GELU_NEW, M=rows, ln=(lw.ln2_g, lw.ln2_b, self.eps))
             else:
                 ops.layernorm_fwd(h1, lw.ln2_g, lw.ln2_b, self.eps, a, None, None, rows=rows)

@@ -151,13 +151,16 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          M: Optional[int] = None, N: Optional[int] = None, K: Optional[int] = None,
          alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None,
          trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None,
-         tile_only: bool = False, g256: bool = False, m_hint: Optional[int] = None) -> Tensor:
+         tile_only: bool = False, g256: bool = False, m_hint: Optional[int] = None,
+         ln_fold: Optional[tuple] = None) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
     workspace: fp32 split-K scratch; by default one buffer per (device, stream), so GEMMs issued on different
     streams never share slabs (gemm_workspace). The split count depends on the shape alone, so the result is
     bitwise the same with any workspace; one too small for the shape's split raises.
     trans_ab: A and B are K-outer ([K, M] / [K, N] row-major: out = epi(alpha * A^T @ B)), bf16 only.
     ln: (gamma, beta, eps) — A is LayerNorm-ed over its K columns inside the GEMM (M <= 128 launches).
+    ln_fold: (wsum, eps) — LayerNorm folded into the weights (fold_layernorm): B = W*gamma, bias = b + W.beta,
+    out = rstd * (A.B^T - mean * wsum) + bias with A's row statistics taken in the launch (M <= 128 launches).
     alg_flops: algorithmic FLOPs when M/N/K include padding (vocab 50257->50304, dW rows -> multiple of 64).
     split_k: 0 = automatic split-K for launches of <= 64 output tiles, 1 = never, > 1 = forced.
     m_dev: device int32 row count <= M (rows past it are neither computed nor stored); m_hint: its expected value
@@ -215,6 +218,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     a.path = 1 if tile_only else (3 if g256 else 0)
     if ln is not None:
         a.ln_gamma, a.ln_beta, a.ln_eps = ln[0].data_ptr(), ln[1].data_ptr(), float(ln[2])
+    if ln_fold is not None:
+        a.ln_wsum, a.ln_eps = ln_fold[0].data_ptr(), float(ln_fold[1])
     if GEMM_TIMER is None:
         call("icap_gemm", C.byref(a), _stream())
     else:  # per-launch HIP-event timing (bench.py kernel roofline pass; never inside a captured graph)
@@ -222,7 +227,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
         key = (name.decode() if name else "?",
                f"{M}x{N}x{K} act{act} dact{dact} drop{int(drop.p > 0)} res{int(resid is not None)} "
                f"aux{int(aux is not None)} beta{beta:g}{' m_dev' if m_dev is not None else ''}"
-               f"{' kout' if trans_ab else ''}{' ln' if ln is not None else ''}")
+               f"{' kout' if trans_ab else ''}{' ln' if ln is not None else ''}{' lnfold' if ln_fold is not None else ''}")
         GEMM_TIMER.launch(key, 2.0 * M * N * K if alg_flops is None else alg_flops,
                           lambda: call("icap_gemm", C.byref(a), _stream()))
     return out

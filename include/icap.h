@@ -127,6 +127,12 @@ typedef struct {
   /* others' partials in split order and applies the epilogue — instead of a separate reduce pass over fp32 slabs. */
   /* Needs 2 entries per 128 x 128 output tile. One buffer per stream (like workspace); deterministic.            */
   int32_t* tickets; int64_t tickets_len;
+  /* ln_wsum != NULL (M <= 128, no ln_gamma): LayerNorm folded into the weights — B holds W[n,k] * gamma[k],  */
+  /* ln_wsum[n] = sum_k B[n,k] (fp32, over the stored B values) and bias = b + W . beta, so                    */
+  /* C = rstd_m * (A . B^T - mean_m * ln_wsum) + bias equals LN(A) . W^T + b with the row mean / rstd of A  */
+  /* (eps = ln_eps) taken inside the launch from the A fragments it already reads; the product runs on raw A  */
+  /* (the decode step's ln_1 / ln_2, frozen GPT-2: HF/models/gpt2/modeling_gpt2.py:281,301).                 */
+  const float* ln_wsum;
 } icap_gemm_args;
 /* MX block quantisation (the A / B operands of an ICAP_FP8_MX GEMM): x [R, K] (f32 or bf16, row stride ldx) */
 /* -> q [R, K] OCP e4m3fn bytes (row stride ldq % 16 == 0) + the E8M0 scales in icap_gemm_args.a_scale      */
