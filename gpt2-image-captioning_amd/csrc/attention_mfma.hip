@@ -33,6 +33,7 @@ struct Geo {
   int64_t rsb, rss;
   int Sst;
   int64_t base, kmb;
+  int slo, shi;  // length class of the launch: blocks whose sequence has slo < S <= shi (packed short / long pass)
 };
 
 __device__ __forceinline__ int64_t trow(const Geo& g, int b, int s) { return g.base + (int64_t)s * g.rss; }
@@ -50,7 +51,7 @@ __device__ __forceinline__ bool localize(Geo& g, const icap_attn_args& p, int b)
     g.base = (int64_t)b * g.rsb;
     g.kmb = (int64_t)b * g.Sst;
   }
-  return g.S > 0;
+  return g.S > g.slo && g.S <= g.shi;  // (slo >= 0: empty sequences do nothing)
 }
 
 __device__ __forceinline__ f32x4_t mfma(const uint4& a, const uint4& b, f32x4_t c) {
@@ -810,6 +811,19 @@ amfma::Geo mfma_geo(const icap_attn_args* a) {
   g.Sp16 = rup(a->S, 16); g.Sp32 = rup(a->S, 32); g.ldT = g.Sp32 + 8;
   g.rsb = a->row_stride_b; g.rss = a->row_stride_s;
   g.Sst = a->S; g.base = 0; g.kmb = 0;
+  g.slo = 0; g.shi = 1 << 30;
+  return g;
+}
+
+// Packed sequences (seq_len) in a launch of S > SHORT_S tokens: the v2 kernels run as two passes, the sequences of
+// at most SHORT_S tokens with LDS and waves sized for SHORT_S (many blocks per CU: one round over the grid), then the
+// longer ones with the launch's sizing (the short ones exit at once). The caption batches of the train step are all
+// short (prefix + caption up to its last target); the split only changes which blocks run, never the arithmetic.
+constexpr int SHORT_S = 32;
+static bool packed_split(const icap_attn_args* a) { return a->seq_len != nullptr && a->S > SHORT_S; }
+static amfma::Geo short_geo(amfma::Geo g) {
+  g.slo = 0; g.shi = SHORT_S;
+  g.Sp16 = SHORT_S; g.Sp32 = SHORT_S; g.ldT = g.Sp32 + 8;
   return g;
 }
 
@@ -889,17 +903,23 @@ int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float
     return check_launch("icap_attention_fwd(mfma v3)");
   }
   if (!bwd && mfma_fwd2_ok(a)) {
-    const size_t lds2 = mfma_fwd2_lds(g);
-    const dim3 block2((unsigned)(64 * (g.Sp16 / 16)));
-    if (a->hd == 64) {
-      static bool once = (lds_limit(amfma::fwd2_kernel<64>), true); (void)once;
-      hipLaunchKernelGGL(amfma::fwd2_kernel<64>, grid, block2, lds2, s, *a, g, thr, inv_keep);
-    } else if (a->hd == 128) {
-      static bool once = (lds_limit(amfma::fwd2_kernel<128>), true); (void)once;
-      hipLaunchKernelGGL(amfma::fwd2_kernel<128>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+    static bool once = (lds_limit(amfma::fwd2_kernel<64>), lds_limit(amfma::fwd2_kernel<128>),
+                        lds_limit(amfma::fwd2_kernel<96>), true);
+    (void)once;
+    auto go = [&](const amfma::Geo& gg) {
+      const size_t lds2 = mfma_fwd2_lds(gg);
+      const dim3 block2((unsigned)(64 * (gg.Sp16 / 16)));
+      if (a->hd == 64) hipLaunchKernelGGL(amfma::fwd2_kernel<64>, grid, block2, lds2, s, *a, gg, thr, inv_keep);
+      else if (a->hd == 128) hipLaunchKernelGGL(amfma::fwd2_kernel<128>, grid, block2, lds2, s, *a, gg, thr, inv_keep);
+      else hipLaunchKernelGGL(amfma::fwd2_kernel<96>, grid, block2, lds2, s, *a, gg, thr, inv_keep);
+    };
+    if (packed_split(a)) {
+      go(short_geo(g));
+      amfma::Geo gl = g;
+      gl.slo = SHORT_S;
+      go(gl);
     } else {
-      static bool once = (lds_limit(amfma::fwd2_kernel<96>), true); (void)once;
-      hipLaunchKernelGGL(amfma::fwd2_kernel<96>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+      go(g);
     }
     return check_launch("icap_attention_fwd(mfma v2)");
   }
@@ -914,17 +934,23 @@ int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float
     }
   } else {
     if (mfma_bwd2_ok(a)) {
-      const size_t lds2 = mfma_bwd2_lds(g);
-      const dim3 block2((unsigned)(64 * (g.Sp16 / 16)));
-      if (a->hd == 64) {
-        static bool once = (lds_limit(amfma::bwd2_kernel<64>), true); (void)once;
-        hipLaunchKernelGGL(amfma::bwd2_kernel<64>, grid, block2, lds2, s, *a, g, thr, inv_keep);
-      } else if (a->hd == 128) {
-        static bool once = (lds_limit(amfma::bwd2_kernel<128>), true); (void)once;
-        hipLaunchKernelGGL(amfma::bwd2_kernel<128>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+      static bool once = (lds_limit(amfma::bwd2_kernel<64>), lds_limit(amfma::bwd2_kernel<128>),
+                          lds_limit(amfma::bwd2_kernel<96>), true);
+      (void)once;
+      auto go = [&](const amfma::Geo& gg) {
+        const size_t lds2 = mfma_bwd2_lds(gg);
+        const dim3 block2((unsigned)(64 * (gg.Sp16 / 16)));
+        if (a->hd == 64) hipLaunchKernelGGL(amfma::bwd2_kernel<64>, grid, block2, lds2, s, *a, gg, thr, inv_keep);
+        else if (a->hd == 128) hipLaunchKernelGGL(amfma::bwd2_kernel<128>, grid, block2, lds2, s, *a, gg, thr, inv_keep);
+        else hipLaunchKernelGGL(amfma::bwd2_kernel<96>, grid, block2, lds2, s, *a, gg, thr, inv_keep);
+      };
+      if (packed_split(a)) {
+        go(short_geo(g));
+        amfma::Geo gl = g;
+        gl.slo = SHORT_S;
+        go(gl);
       } else {
-        static bool once = (lds_limit(amfma::bwd2_kernel<96>), true); (void)once;
-        hipLaunchKernelGGL(amfma::bwd2_kernel<96>, grid, block2, lds2, s, *a, g, thr, inv_keep);
+        go(g);
       }
       return check_launch("icap_attention_bwd(mfma v2)");
     }

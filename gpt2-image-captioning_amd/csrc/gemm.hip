@@ -186,11 +186,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  // K-skew (host: kskew_for): bits 20+ of nk_split rotate this tile's k-step order within its K range
+  const int kskew = nk_split >> 20;
+  nk_split &= 0xFFFFF;
   const int nk_all = (int)((K + BKE - 1) / BKE);
   const int kt0 = split * nk_split;
   const int nk = (nk_all - kt0 < nk_split ? nk_all - kt0 : nk_split);  // >= 1 by the host's choice of splits
   const int64_t kbase = (int64_t)kt0 * BKE;
   const int fr = lane & 15, fg = lane >> 4;
+  const int koff = kskew ? (int)(((int64_t)(tm * 7 + tn) * kskew) % nk) : 0;
+  auto kstep = [&](int kt) -> int64_t { const int j = kt + koff; return (int64_t)(j >= nk ? j - nk : j) * BKE; };
 
   // MX scales (mx_scale_off layout): this lane's 16 bytes per stage = the scales of rows i*16 + fr (i = 0..3) of the
   // wave's 64-row group, blocks 0..3; the lane's own block is fg (byte 8 fg of each word after the shift below)
@@ -289,7 +294,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     }
 #pragma unroll
     for (int s = 0; s < 3; ++s)
-      if (s < nk) load_stage(kbase + (int64_t)s * BKE, s);
+      if (s < nk) load_stage(kbase + kstep(s), s);
 #define ICAP_RING_RD(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
     for (int kt = 0; kt < nk; ++kt) {
       __builtin_amdgcn_sched_barrier(0);
@@ -298,7 +303,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if (kt + 3 < nk) load_stage(kbase + (int64_t)(kt + 3) * BKE, (kt + 3) & 3);
+      if (kt + 3 < nk) load_stage(kbase + kstep(kt + 3), (kt + 3) & 3);
       __builtin_amdgcn_sched_barrier(0);
       const uint32_t sb = sbase + (uint32_t)((kt & 3) * STB);
       u32x4_t fa0[4], fb0[4], fa1[4], fb1[4];
@@ -332,7 +337,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();  // (no DMA outstanding) every wave is done reading the ring before the epilogue reuses it
   } else if (NST == 2) {
-    load_stage(kbase, 0);
+    load_stage(kbase + kstep(0), 0);
     load_scales(kt0, sca_cur, scb_cur);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -344,7 +349,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       read_frags(smem + cur * STB, af, bfr);
       // the other buffer was last read in iteration kt-1, which every wave finished before the barrier below
       if (kt + 1 < nk) {
-        load_stage(kbase + (int64_t)(kt + 1) * BKE, cur ^ 1);
+        load_stage(kbase + kstep(kt + 1), cur ^ 1);
         load_scales(kt0 + kt + 1, sca_nxt, scb_nxt);
       }
       mfmas(af, bfr);
@@ -361,7 +366,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   } else {
     for (int kt = 0; kt < nk; ++kt) {
       if (kt > 0) __syncthreads();  // every wave has finished reading the previous stage
-      load_stage(kbase + (int64_t)kt * BKE, 0);
+      load_stage(kbase + kstep(kt), 0);
       load_scales(kt0 + kt, sca_cur, scb_cur);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -1004,6 +1009,18 @@ static int fused_s_override() {
   static const int v = [] { const char* e = getenv("ICAP_FUSED_S"); return e ? atoi(e) : 0; }();
   return v;
 }
+// K-skew: tile (tm, tn) walks its K range starting at step ((7 tm + tn) * skew) mod nk and wraps, so the tiles of
+// one XCD that share an A row panel (consecutive tn) or a B panel do not request the same lines in lockstep (a
+// line they all miss on is fetched once and waited for by every one of them). Measured over the packed train step
+// (eager per-shape table, profiles/r03_kskew_ab.txt): skew 1 took the N = 768 products 5-15 % shorter and the step
+// 11.3 -> 10.9 ms; skew 2-4 less; launches over more than 64 k-steps per split (the LM-head dX, K = 50304) ran
+// longer, so they keep the natural order. ICAP_KSKEW overrides the skew (0 = off; A/B only); path 1 (tile_only)
+// keeps the natural order (the path-equality tests compare it bitwise with the 256 x 256 kernel).
+static int kskew_for(const icap_gemm_args& p, int64_t nk_split) {
+  static const int v = [] { const char* e = getenv("ICAP_KSKEW"); return e ? atoi(e) : 1; }();
+  if (p.path == 1 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
+  return v > 0 && v < 2048 ? v : 0;
+}
 static int fused_nst_override() {
   static const int v = [] { const char* e = getenv("ICAP_FUSED_NST"); return e ? atoi(e) : 0; }();
   return v;
@@ -1285,7 +1302,8 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   }
   if (pl.g256) return gemm256_launch(p, thr, inv_keep, s);
   const dim3 grid = pl.grid, block = pl.block;
-  const int sp = pl.splits, nks = pl.nk_split, tn = pl.tiles_n;
+  const int sp = pl.splits, tn = pl.tiles_n;
+  const int nks = pl.nk_split | (kskew_for(p, pl.nk_split) << 20);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
 #define ICAP_GK(TI, TC, NST, MINB, TM_, TN_, KOUT)                                                              \
   do {                                                                                                       \
