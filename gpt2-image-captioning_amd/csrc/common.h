@@ -137,7 +137,7 @@ __device__ __forceinline__ float act_fwd(int act, float x) {
       return x * __builtin_amdgcn_rcpf(1.f + __expf(-c2 * (x + 0.044715f * x * x * x)));
     }
     case ICAP_ACT_RELU: return x > 0.f ? x : 0.f;
-    case ICAP_ACT_QUICK_GELU: return x / (1.f + __expf(-1.702f * x));
+    case ICAP_ACT_QUICK_GELU: return x * __builtin_amdgcn_rcpf(1.f + __expf(-1.702f * x));  // (v_rcp, not a full division)
     case ICAP_ACT_TANH: return tanhf(x);
     case ICAP_ACT_GELU_ERF: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));  // HF ACT2FN["gelu"]
     default: return x;

@@ -73,7 +73,7 @@ __device__ __forceinline__ uint4 kout_frag(const char* img, int r0, int c0, int 
 // activation code is then not compiled into the kernel at all. Measured (profiles/r03_k768_counters.txt): with it
 // present, the plain 8320 x 2304 x 768 product ran 53.7 vs 45.0 us — the same memory instructions, +7 % VALU and
 // +22 % SQ_WAIT_ANY (the larger function scheduled its main loop worse), SQ_WAIT_INST_ANY +1 % (not instruction fetch).
-template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, bool ACT = true>
+template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, int ACT = ACT_ANY>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
                                                                   int nk_split, uint32_t drop_thresh, float inv_keep) {
   static_assert(!KOUT || (sizeof(TI) == 2 && 16 * WM * TM == 128 && 16 * WN * TN == 128),
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   };
   if constexpr (std::is_same<TC, bf16_t>::value) {
     if (whole) {
-      if (ACT && p.dact != ICAP_ACT_NONE) {
+      if (ACT >= ACT_BWD || (ACT == ACT_ANY && p.dact != ICAP_ACT_NONE)) {
         esrc = reinterpret_cast<const bf16_t*>(p.dact_src);
         eld = p.ld_dact;
       } else if (p.resid) {
@@ -951,10 +951,18 @@ using namespace icap;
 // bound by the per-block prologue/epilogue, which co-resident blocks hide -> single LDS buffer, 3-4 blocks/CU (4
 // when the epilogue moves a second M x N tensor: dact_src read / aux store); long K favours the double-buffered
 // main loop at 2 blocks/CU.
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
 static int gemm_variant(const icap_gemm_args& p, int64_t nk_per_block) {
   if (nk_per_block > 16) return 0;
   const bool heavy = p.dact != ICAP_ACT_NONE || p.aux;
-  return heavy ? 5 : 4;
+  const bool act = p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE;
+  // (A/B) ICAP_VAR_HEAVY / ICAP_VAR_ACT / ICAP_VAR_LIGHT: variant for short-K launches with dact / aux, with an
+  // activation only, and with neither
+  static const int vh = env_int("ICAP_VAR_HEAVY", 5), va = env_int("ICAP_VAR_ACT", 4), vl = env_int("ICAP_VAR_LIGHT", 4);
+  return heavy ? vh : act ? va : vl;
 }
 
 // compute units of the current device (the skinny-GEMM grid rule, the 256 x 256 kernel's pick)
@@ -1021,6 +1029,10 @@ static int kskew_for(const icap_gemm_args& p, int64_t nk_split) {
   if (p.path == 1 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
   return v > 0 && v < 2048 ? v : 0;
 }
+static bool spec_act_on() {  // ICAP_SPEC_ACT=0: the runtime-dispatch epilogue everywhere (A/B only)
+  static const bool v = [] { const char* e = getenv("ICAP_SPEC_ACT"); return !(e && e[0] == '0'); }();
+  return v;
+}
 static int fused_nst_override() {
   static const int v = [] { const char* e = getenv("ICAP_FUSED_NST"); return e ? atoi(e) : 0; }();
   return v;
@@ -1036,7 +1048,7 @@ struct GemmPlan {
   int variant = 0;       // tile kernel (see ICAP_GEMM_LAUNCH)
   int splits = 1, nk_split = 0, tiles_n = 0;
   bool fused = false;    // split-K combined inside the launch (tickets), no reduce pass
-  bool act = true;       // tile kernels: the instantiation with the activation epilogue compiled in
+  int actk = ACT_ANY;    // tile kernels: the epilogue's activation instantiation (ACT_OFF / ACT_ANY / a specialised one)
   dim3 grid, block;
   uint32_t thr = 0;
   float inv_keep = 1.f;
@@ -1200,23 +1212,39 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   }
   if (p.trans_ab) pl.variant = nk_split > 16 ? 14 : 15;  // K-outer forms of variants 0 / 4
   pl.tiles_n = (int)tiles_n;
-  pl.act = (splits == 1 || pl.fused) && (p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE);
+  const bool any_act = (splits == 1 || pl.fused) && (p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE);
+  pl.actk = any_act ? ACT_ANY : ACT_OFF;
+  // the step's activated products get an epilogue compiled for their one activation (gemm_common.h ACT_FWD /
+  // ACT_BWD): GPT-2 c_fc gelu_new (+ aux) and its dgelu, CLIP c_fc quick_gelu, ViT / DINOv3 c_fc erf gelu, the
+  // mapper's relu / drelu (128 x 64 tiles). Measured over the packed step (tools/specact_ab.sh, profiles/
+  // r03_specact_ab.txt): 10.98 -> 10.61 ms; the mapper's 3200x3072x768 relu 36.4 -> 29.1 µs, CLIP's quick_gelu
+  // 68.6 -> 64.0, gelu + aux 64.5 -> 57.6 — the runtime dispatch over five activations (libm erff / tanhf / expf
+  // inlined per case) cost registers and scratch in the epilogue of every activated launch.
+  if (any_act && p.in_dtype == ICAP_BF16 && p.c_dtype == ICAP_BF16 && !p.trans_ab && spec_act_on()) {
+    const int fa = p.dact == ICAP_ACT_NONE ? p.act : -1, ba = p.act == ICAP_ACT_NONE ? p.dact : -1;
+    if ((pl.variant == 5 || pl.variant == 0) && fa == ICAP_ACT_GELU_NEW) pl.actk = ACT_FWD + ICAP_ACT_GELU_NEW;
+    else if ((pl.variant == 5 || pl.variant == 0) && ba == ICAP_ACT_GELU_NEW) pl.actk = ACT_BWD + ICAP_ACT_GELU_NEW;
+    else if (pl.variant == 4 && fa == ICAP_ACT_QUICK_GELU) pl.actk = ACT_FWD + ICAP_ACT_QUICK_GELU;
+    else if (pl.variant == 4 && fa == ICAP_ACT_GELU_ERF) pl.actk = ACT_FWD + ICAP_ACT_GELU_ERF;
+    else if (pl.variant == 13 && fa == ICAP_ACT_RELU) pl.actk = ACT_FWD + ICAP_ACT_RELU;
+    else if (pl.variant == 13 && ba == ICAP_ACT_RELU) pl.actk = ACT_BWD + ICAP_ACT_RELU;
+  }
   pl.block = dim3(GNT);
   pl.grid = dim3((unsigned)(tiles * splits));
   return ICAP_OK;
 }
 
-// "TI, TC, template ints" of each tile variant (keep in sync with the launch switch below); %%s = ACT
+// "TI, TC, template ints" of each tile variant (keep in sync with the launch switch below); %%d = ACT kind
 static const char* variant_kernel(int v) {
   switch (v) {
-    case 0: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, false, %s>";
-    case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, false, %s>";
-    case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4, false, %s>";
-    case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2, false, %s>";
-    case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2, false, %s>";
-    case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true, %s>";
-    case 16: return "gemm_kernel<%s, %s, 4, 1, 2, 2, 4, 4, false, %s>";
-    default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %s>";
+    case 0: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, false, %d>";
+    case 4: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, false, %d>";
+    case 5: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 4, false, %d>";
+    case 12: return "gemm_kernel<%s, %s, 2, 3, 2, 2, 4, 2, false, %d>";
+    case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2, false, %d>";
+    case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true, %d>";
+    case 16: return "gemm_kernel<%s, %s, 4, 1, 2, 2, 4, 4, false, %d>";
+    default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %d>";
   }
 }
 
@@ -1232,10 +1260,13 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
     snprintf(buf, sizeof buf, "icap::gemm256_kernel<%s>", tc);
     return buf;
   }
-  if (pl.skinny) snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2, %d>", pl.nt, pl.sku);
-  else snprintf(fmt, sizeof fmt, "%s", variant_kernel(pl.variant));
   char inner[128];
-  snprintf(inner, sizeof inner, fmt, ti, tc, pl.act ? "true" : "false");
+  if (pl.skinny) {
+    snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2, %d>", pl.nt, pl.sku);
+    snprintf(inner, sizeof inner, fmt, ti, tc);
+  } else {
+    snprintf(inner, sizeof inner, variant_kernel(pl.variant), ti, tc, pl.actk);
+  }
   snprintf(buf, sizeof buf, "icap::%s", inner);
   return buf;
 }
@@ -1307,8 +1338,8 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
 #define ICAP_GK(TI, TC, NST, MINB, TM_, TN_, KOUT)                                                              \
   do {                                                                                                       \
-    if (pl.act) hipLaunchKernelGGL((gemm_kernel<TI, TC, NST, MINB, 2, 2, TM_, TN_, KOUT, true>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
-    else hipLaunchKernelGGL((gemm_kernel<TI, TC, NST, MINB, 2, 2, TM_, TN_, KOUT, false>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
+    if (pl.actk == ACT_ANY) hipLaunchKernelGGL((gemm_kernel<TI, TC, NST, MINB, 2, 2, TM_, TN_, KOUT, ACT_ANY>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
+    else hipLaunchKernelGGL((gemm_kernel<TI, TC, NST, MINB, 2, 2, TM_, TN_, KOUT, ACT_OFF>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
   } while (0)
 #define ICAP_GEMM_LAUNCH(TI, TC)                                    \
   switch (pl.variant) {                                             \
@@ -1316,7 +1347,26 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     case 4: ICAP_GK(TI, TC, 1, 3, 4, 4, false); break;              \
     default: ICAP_GK(TI, TC, 1, 4, 4, 4, false); break;             \
   }
-  if (pl.variant == 14 || pl.variant == 15) {  // K-outer operands (bf16 inputs only)
+#define ICAP_GKS(NST, MINB, TM_, TN_, KIND) \
+  hipLaunchKernelGGL((gemm_kernel<bf16_t, bf16_t, NST, MINB, 2, 2, TM_, TN_, false, KIND>), grid, block, 0, s, p, tn, sp, \
+                     nks, thr, inv_keep)
+  if (pl.actk >= ACT_FWD) {  // specialised activation epilogues (gemm_plan: bf16 in / out, variants 0, 4, 5, 13)
+    switch (pl.actk) {
+      case ACT_FWD + ICAP_ACT_GELU_NEW:  // (variant 0: GPT-2 large / medium c_fc, K = 1280 / 1024 > 16 stages)
+        if (pl.variant == 0) ICAP_GKS(2, 2, 4, 4, ACT_FWD + ICAP_ACT_GELU_NEW);
+        else ICAP_GKS(1, 4, 4, 4, ACT_FWD + ICAP_ACT_GELU_NEW);
+        break;
+      case ACT_BWD + ICAP_ACT_GELU_NEW:
+        if (pl.variant == 0) ICAP_GKS(2, 2, 4, 4, ACT_BWD + ICAP_ACT_GELU_NEW);
+        else ICAP_GKS(1, 4, 4, 4, ACT_BWD + ICAP_ACT_GELU_NEW);
+        break;
+      case ACT_FWD + ICAP_ACT_QUICK_GELU: ICAP_GKS(1, 3, 4, 4, ACT_FWD + ICAP_ACT_QUICK_GELU); break;
+      case ACT_FWD + ICAP_ACT_GELU_ERF: ICAP_GKS(1, 3, 4, 4, ACT_FWD + ICAP_ACT_GELU_ERF); break;
+      case ACT_FWD + ICAP_ACT_RELU: ICAP_GKS(1, 4, 4, 2, ACT_FWD + ICAP_ACT_RELU); break;
+      default: ICAP_GKS(1, 4, 4, 2, ACT_BWD + ICAP_ACT_RELU); break;
+    }
+#undef ICAP_GKS
+  } else if (pl.variant == 14 || pl.variant == 15) {  // K-outer operands (bf16 inputs only)
     if (p.c_dtype == ICAP_BF16) {
       if (pl.variant == 14) ICAP_GK(bf16_t, bf16_t, 2, 2, 4, 4, true);
       else ICAP_GK(bf16_t, bf16_t, 1, 3, 4, 4, true);

@@ -166,7 +166,12 @@ __device__ __forceinline__ void unpack_bf16(const uint4 w, float v[8]) {
 // instruction fetch: 8320 x 3072 x 768 with relu 97 us vs 61 plain, tools/act_epilogue_probe.py.) The arithmetic
 // per element is unchanged (act_fwd / act_bwd), so outputs are bitwise the same.
 // backward form: x = alpha * acc * dropmask * act'(a)
-template <int W>
+// Activation kinds of an epilogue instantiation (template int ACT): ACT_OFF none (the host guarantees act == dact ==
+// NONE), ACT_ANY the runtime dispatch below, ACT_FWD + a forward activation a only, ACT_BWD + a backward dact a only:
+// the specialised forms compile a single straight run (no dispatch, none of the other activations' code, fewer live
+// registers in the epilogue); the arithmetic per element is act_fwd / act_bwd in every form (bitwise the same).
+constexpr int ACT_OFF = 0, ACT_ANY = 1, ACT_FWD = 16, ACT_BWD = 32;
+template <int W, int ACT = ACT_ANY>
 __device__ __forceinline__ void epi_bwd_math(const icap_gemm_args& p, float x[W], const float a[W], uint64_t seed,
                                              uint64_t didx, uint32_t drop_thresh, float inv_keep) {
 #pragma clang fp contract(off)
@@ -175,6 +180,11 @@ __device__ __forceinline__ void epi_bwd_math(const icap_gemm_args& p, float x[W]
   for (int e = 0; e < W; ++e) {
     y[e] = p.alpha * x[e];
     if (drop_thresh != 0u) y[e] = y[e] * drop_scale(seed, didx + e, drop_thresh, inv_keep);
+  }
+  if constexpr (ACT >= ACT_BWD) {
+#pragma unroll
+    for (int e = 0; e < W; ++e) x[e] = y[e] * act_bwd(ACT - ACT_BWD, a[e]);
+    return;
   }
   switch (p.dact) {
 #define ICAP_DACT_CASE(A)                                              \
@@ -195,12 +205,22 @@ __device__ __forceinline__ void epi_bwd_math(const icap_gemm_args& p, float x[W]
 // forward form, first half: x = act(alpha * acc + bias); a = the aux value (pre-activation, or tanh output).
 // ACT = false: an instantiation for launches without an activation (the host guarantees act == dact == NONE), so
 // none of the activation code is compiled into that kernel (see gemm_kernel's ACT parameter).
-template <int W, bool ACT = true>
+template <int W, int ACT = ACT_ANY>
 __device__ __forceinline__ void epi_fwd_act(const icap_gemm_args& p, float x[W], const float biasw[W], float a[W]) {
 #pragma clang fp contract(off)
 #pragma unroll
   for (int e = 0; e < W; ++e) x[e] = __builtin_fmaf(p.alpha, x[e], biasw[e]);
-  if (!ACT || __builtin_expect(p.act == ICAP_ACT_NONE, 1)) {  // no activation: keep this path short and first
+  if constexpr (ACT >= ACT_FWD && ACT < ACT_BWD) {
+    constexpr int A = ACT - ACT_FWD;
+#pragma unroll
+    for (int e = 0; e < W; ++e) {
+      const float y = act_fwd(A, x[e]);
+      a[e] = (A == ICAP_ACT_TANH) ? y : x[e];
+      x[e] = y;
+    }
+    return;
+  }
+  if (ACT == ACT_OFF || ACT >= ACT_BWD || __builtin_expect(p.act == ICAP_ACT_NONE, 1)) {  // no activation: short, first
     if (p.aux) {
 #pragma unroll
       for (int e = 0; e < W; ++e) a[e] = x[e];
@@ -246,7 +266,7 @@ __device__ __forceinline__ void epi_fwd_tail(float x[W], const float r[W], bool 
 // W-wide vector access is used per operand where its leading dimension and base pointer are W-aligned.
 // pre: optional prefetched raw bf16 vector of the epilogue's input operand at (row, col..) — dact_src in the
 // backward form, resid in the forward form — loaded by the caller ahead of the LDS staging (fullw rows only).
-template <typename TC, int W, bool ACT = true>
+template <typename TC, int W, int ACT = ACT_ANY>
 __device__ __forceinline__ void epiw(const icap_gemm_args& p, int64_t row, int64_t col, float x[W],
                                      const float biasw[W], bool fullw, uint64_t seed, uint32_t drop_thresh,
                                      float inv_keep, const typename rawbf<W>::T* pre = nullptr) {
@@ -262,11 +282,11 @@ __device__ __forceinline__ void epiw(const icap_gemm_args& p, int64_t row, int64
   constexpr uintptr_t VA = (W * sizeof(TC) > 16 ? 16 : W * sizeof(TC)) - 1;
   auto vok = [&](int64_t ld, const void* ptr) { return (ld % W) == 0 && (reinterpret_cast<uintptr_t>(ptr) & VA) == 0; };
   fullw = fullw && vok(p.ldc, C);
-  if (ACT && p.dact != ICAP_ACT_NONE) {
+  if (ACT >= ACT_BWD || (ACT == ACT_ANY && p.dact != ICAP_ACT_NONE)) {
     if (pre) unpack_bf16(*pre, a);
     else if (fullw && vok(p.ld_dact, dsrc)) vecio<TC, W>::ld(dsrc + row * p.ld_dact + col, a);
     else for (int e = 0; e < W; ++e) a[e] = (col + e < N) ? io<TC>::ld(dsrc + row * p.ld_dact + col + e) : 0.f;
-    epi_bwd_math<W>(p, x, a, seed, didx, drop_thresh, inv_keep);
+    epi_bwd_math<W, ACT>(p, x, a, seed, didx, drop_thresh, inv_keep);
   } else {
     epi_fwd_act<W, ACT>(p, x, biasw, a);
     if (aux) {
