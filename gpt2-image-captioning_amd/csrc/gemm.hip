@@ -1222,8 +1222,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // inlined per case) cost registers and scratch in the epilogue of every activated launch.
   if (any_act && p.in_dtype == ICAP_BF16 && p.c_dtype == ICAP_BF16 && !p.trans_ab && spec_act_on()) {
     const int fa = p.dact == ICAP_ACT_NONE ? p.act : -1, ba = p.act == ICAP_ACT_NONE ? p.dact : -1;
-    if ((pl.variant == 5 || pl.variant == 0) && fa == ICAP_ACT_GELU_NEW) pl.actk = ACT_FWD + ICAP_ACT_GELU_NEW;
-    else if ((pl.variant == 5 || pl.variant == 0) && ba == ICAP_ACT_GELU_NEW) pl.actk = ACT_BWD + ICAP_ACT_GELU_NEW;
+    const bool v045 = pl.variant == 0 || pl.variant == 4 || pl.variant == 5;
+    if (v045 && fa == ICAP_ACT_GELU_NEW) pl.actk = ACT_FWD + ICAP_ACT_GELU_NEW;
+    else if (v045 && ba == ICAP_ACT_GELU_NEW) pl.actk = ACT_BWD + ICAP_ACT_GELU_NEW;
     else if (pl.variant == 4 && fa == ICAP_ACT_QUICK_GELU) pl.actk = ACT_FWD + ICAP_ACT_QUICK_GELU;
     else if (pl.variant == 4 && fa == ICAP_ACT_GELU_ERF) pl.actk = ACT_FWD + ICAP_ACT_GELU_ERF;
     else if (pl.variant == 13 && fa == ICAP_ACT_RELU) pl.actk = ACT_FWD + ICAP_ACT_RELU;
@@ -1354,10 +1355,12 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     switch (pl.actk) {
       case ACT_FWD + ICAP_ACT_GELU_NEW:  // (variant 0: GPT-2 large / medium c_fc, K = 1280 / 1024 > 16 stages)
         if (pl.variant == 0) ICAP_GKS(2, 2, 4, 4, ACT_FWD + ICAP_ACT_GELU_NEW);
+        else if (pl.variant == 4) ICAP_GKS(1, 3, 4, 4, ACT_FWD + ICAP_ACT_GELU_NEW);
         else ICAP_GKS(1, 4, 4, 4, ACT_FWD + ICAP_ACT_GELU_NEW);
         break;
       case ACT_BWD + ICAP_ACT_GELU_NEW:
         if (pl.variant == 0) ICAP_GKS(2, 2, 4, 4, ACT_BWD + ICAP_ACT_GELU_NEW);
+        else if (pl.variant == 4) ICAP_GKS(1, 3, 4, 4, ACT_BWD + ICAP_ACT_GELU_NEW);
         else ICAP_GKS(1, 4, 4, 4, ACT_BWD + ICAP_ACT_GELU_NEW);
         break;
       case ACT_FWD + ICAP_ACT_QUICK_GELU: ICAP_GKS(1, 3, 4, 4, ACT_FWD + ICAP_ACT_QUICK_GELU); break;
