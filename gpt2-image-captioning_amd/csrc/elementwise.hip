@@ -576,11 +576,11 @@ __global__ __launch_bounds__(256) void colsum_kernel(int64_t M, int64_t N, const
 // 16-bit transpose with 16-byte accesses on both sides: 64x64 tile through LDS (row stride 68 halves, so the
 // column gathers of the write phase are at most 2-way bank conflicted). Needs cols % 8 == 0, lds/ldd % 8 == 0,
 // 16-byte aligned src/dst and rows_pad % 64 == 0 (checked by the host).
-__global__ __launch_bounds__(256) void transpose16_vec_kernel(int64_t rows, int64_t cols, const uint16_t* __restrict__ src,
-                                                              int64_t lds, uint16_t* __restrict__ dst, int64_t ldd) {
-  constexpr int TLD = 68;
-  __shared__ __attribute__((aligned(16))) uint16_t tile[64 * TLD];
-  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+constexpr int T16_TLD = 68;
+__device__ __forceinline__ void transpose16_tile(int64_t rows, int64_t cols, const uint16_t* __restrict__ src,
+                                                 int64_t lds, uint16_t* __restrict__ dst, int64_t ldd, int64_t r0,
+                                                 int64_t c0, uint16_t* tile) {
+  constexpr int TLD = T16_TLD;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int idx = threadIdx.x + 256 * h;
@@ -603,6 +603,33 @@ __global__ __launch_bounds__(256) void transpose16_vec_kernel(int64_t rows, int6
       w[e] = (uint32_t)tile[(8 * rq + 2 * e) * TLD + c] | ((uint32_t)tile[(8 * rq + 2 * e + 1) * TLD + c] << 16);
     *reinterpret_cast<uint4*>(dst + (c0 + c) * ldd + r0 + 8 * rq) = make_uint4(w[0], w[1], w[2], w[3]);
   }
+}
+
+__global__ __launch_bounds__(256) void transpose16_vec_kernel(int64_t rows, int64_t cols, const uint16_t* __restrict__ src,
+                                                              int64_t lds, uint16_t* __restrict__ dst, int64_t ldd) {
+  __shared__ __attribute__((aligned(16))) uint16_t tile[64 * T16_TLD];
+  transpose16_tile(rows, cols, src, lds, dst, ldd, (int64_t)blockIdx.y * 64, (int64_t)blockIdx.x * 64, tile);
+}
+
+// Several bf16 transposes in one launch (the trained mapper's transposed weight copies after every optimizer step:
+// 32 launches of 3-25 µs before): block b works on tile b - off[i] of the item i whose tile range holds b.
+constexpr int T16_BATCH = 32;
+struct Transpose16Batch {
+  int n;
+  int64_t off[T16_BATCH + 1];
+  const uint16_t* src[T16_BATCH];
+  uint16_t* dst[T16_BATCH];
+  int64_t rows[T16_BATCH], cols[T16_BATCH], lds[T16_BATCH], ldd[T16_BATCH];
+};
+__global__ __launch_bounds__(256) void transpose16_batch_kernel(Transpose16Batch b) {
+  __shared__ __attribute__((aligned(16))) uint16_t tile[64 * T16_TLD];
+  const int64_t bid = blockIdx.x;
+  int i = 0;
+  while (i + 1 < b.n && bid >= b.off[i + 1]) ++i;  // block-uniform
+  const int64_t t = bid - b.off[i];
+  const int64_t tx = (b.cols[i] + 63) / 64;
+  const int64_t ty = t / tx;
+  transpose16_tile(b.rows[i], b.cols[i], b.src[i], b.lds[i], b.dst[i], b.ldd[i], ty * 64, (t - ty * tx) * 64, tile);
 }
 
 // column sums, 4 columns per lane (16-byte / 8-byte row segments), 4 waves over the rows of a chunk
@@ -1261,6 +1288,40 @@ extern "C" int icap_transpose(int32_t dtype, int64_t rows, int64_t cols, const v
     hipLaunchKernelGGL(transpose_kernel<uint32_t>, grid, dim3(256), 0, S_(stream), rows, cols, (const uint32_t*)src,
                        lds, (uint32_t*)dst, ldd, rows_pad);
   return check_launch("icap_transpose");
+}
+
+extern "C" int icap_transpose_batch(int32_t n, const icap_transpose_item* items, void* stream) {
+  ICAP_REQUIRE(n >= 0 && (n == 0 || items), "icap_transpose_batch: bad args");
+  for (int32_t i0 = 0; i0 < n; i0 += T16_BATCH) {
+    const int m = n - i0 < T16_BATCH ? n - i0 : T16_BATCH;
+    Transpose16Batch b;
+    b.n = 0;
+    b.off[0] = 0;
+    for (int j = 0; j < m; ++j) {
+      const icap_transpose_item& it = items[i0 + j];
+      ICAP_REQUIRE(it.src && it.dst && it.rows >= 0 && it.cols >= 0, "icap_transpose_batch: bad item");
+      if (it.rows == 0 || it.cols == 0) continue;
+      const bool vec = it.cols % 8 == 0 && it.lds % 8 == 0 && it.ldd % 8 == 0 && it.rows % 64 == 0 &&
+                       it.lds >= it.cols && it.ldd >= it.rows && (reinterpret_cast<uintptr_t>(it.src) & 15) == 0 &&
+                       (reinterpret_cast<uintptr_t>(it.dst) & 15) == 0;
+      if (!vec) {  // (the batched form is the 16-byte tile path only)
+        const int rc = icap_transpose(ICAP_BF16, it.rows, it.cols, it.src, it.lds, it.dst, it.ldd, it.rows, stream);
+        if (rc) return rc;
+        continue;
+      }
+      const int k = b.n++;
+      b.src[k] = static_cast<const uint16_t*>(it.src);
+      b.dst[k] = static_cast<uint16_t*>(it.dst);
+      b.rows[k] = it.rows; b.cols[k] = it.cols; b.lds[k] = it.lds; b.ldd[k] = it.ldd;
+      b.off[k + 1] = b.off[k] + ((it.cols + 63) / 64) * (it.rows / 64);
+    }
+    if (b.n == 0) continue;
+    ICAP_REQUIRE(b.off[b.n] < (1ll << 31), "icap_transpose_batch: too many tiles");
+    hipLaunchKernelGGL(transpose16_batch_kernel, dim3((unsigned)b.off[b.n]), dim3(256), 0, S_(stream), b);
+    const int rc = check_launch("icap_transpose_batch");
+    if (rc) return rc;
+  }
+  return ICAP_OK;
 }
 
 static int64_t colsum_chunks(int64_t M) {

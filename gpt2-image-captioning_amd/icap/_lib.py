@@ -52,6 +52,10 @@ class GemmArgs(C.Structure):
     ]
 
 
+class TransposeItem(C.Structure):
+    _fields_ = [("src", vp), ("lds", i64), ("dst", vp), ("ldd", i64), ("rows", i64), ("cols", i64)]
+
+
 class AttnArgs(C.Structure):
     _fields_ = [
         ("dtype", i32),
@@ -131,6 +135,7 @@ SIGNATURES = {
     "icap_adamw_step": (C.c_int, [C.POINTER(AdamWArgs), vp, vp]),
     "icap_sqnorm": (C.c_int, [i64, vp, vp, vp, vp]),
     "icap_transpose": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, i64, vp]),
+    "icap_transpose_batch": (C.c_int, [i32, vp, vp]),
     "icap_colsum_workspace_bytes": (sz, [i64, i64]),
     "icap_colsum": (C.c_int, [i32, i64, i64, vp, i64, vp, i32, vp, vp]),
     "icap_dropout_apply": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, f32, u64, u64, vp, vp]),

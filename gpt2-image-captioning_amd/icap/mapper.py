@@ -274,11 +274,13 @@ class TransformerMapperCore:
         return max(self.Hl * self.D, 4 * self.D, self.E)
 
     def refresh_transposes(self) -> None:
-        for w in self.layers:
-            ops.transpose(w.in_w, w.in_wt)
-            ops.transpose(w.out_w, w.out_wt)
-            ops.transpose(w.l1_w, w.l1_wt)
-            ops.transpose(w.l2_w, w.l2_wt)
+        pairs = [(a, b) for w in self.layers
+                 for a, b in ((w.in_w, w.in_wt), (w.out_w, w.out_wt), (w.l1_w, w.l1_wt), (w.l2_w, w.l2_wt))]
+        if pairs and pairs[0][0].dtype == torch.bfloat16:
+            ops.transpose_batch(pairs)  # one launch for every layer's copies (was 4 per layer)
+        else:
+            for a, b in pairs:
+                ops.transpose(a, b)
 
     def grads(self, flat) -> SimpleNamespace:
         m = self.m

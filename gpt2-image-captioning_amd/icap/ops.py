@@ -521,6 +521,21 @@ def transpose(src: Tensor, dst: Tensor, rows_pad: Optional[int] = None, rows: Op
     return dst
 
 
+def transpose_batch(pairs) -> None:
+    """dst = src^T for every (src, dst) of bf16 matrices in one launch (icap_transpose_batch; items it cannot tile
+    fall back to icap_transpose inside the library)."""
+    pairs = list(pairs)
+    if not pairs:
+        return
+    items = (L.TransposeItem * len(pairs))()
+    for it, (src, dst) in zip(items, pairs):
+        if src.dtype != torch.bfloat16 or dst.dtype != torch.bfloat16:
+            raise L.IcapError("transpose_batch: bf16 matrices only")
+        it.src, it.lds, it.dst, it.ldd = src.data_ptr(), _ld(src), dst.data_ptr(), _ld(dst)
+        it.rows, it.cols = src.shape[0], src.shape[1]
+    call("icap_transpose_batch", len(pairs), C.cast(items, C.c_void_p), _stream())
+
+
 def colsum_workspace(M: int, N: int) -> int:
     return int(L.load().icap_colsum_workspace_bytes(M, N))
 

@@ -324,6 +324,13 @@ int icap_sqnorm(int64_t n, const float* x, float* out, void* workspace, void* st
 /* dst[c*ldd + r] = src[r*lds + c] for r<rows, c<cols; zero for rows<=r<rows_pad */
 int icap_transpose(int32_t dtype, int64_t rows, int64_t cols, const void* src, int64_t lds,
                    void* dst, int64_t ldd, int64_t rows_pad, void* stream);
+/* Several bf16 transposes in one launch: dst[c*ldd + r] = src[r*lds + c] per item (r < rows, c < cols). Items   */
+/* with rows % 64, cols % 8, lds % 8, ldd % 8 == 0 and 16-byte aligned pointers share one launch (up to 32 per     */
+/* launch); others fall back to icap_transpose. (The trained mapper's transposed weight copies after each step.)   */
+typedef struct {
+  const void* src; int64_t lds; void* dst; int64_t ldd; int64_t rows; int64_t cols;
+} icap_transpose_item;
+int icap_transpose_batch(int32_t n, const icap_transpose_item* items, void* stream);
 /* out[n] (+)= sum_m src[m*ld + n]  (bias grads, prefix_const grad); fp32 out */
 size_t icap_colsum_workspace_bytes(int64_t M, int64_t N);
 int icap_colsum(int32_t dtype, int64_t M, int64_t N, const void* src, int64_t ld, float* out,

@@ -120,6 +120,12 @@ def accesses(name, args):
         dt, rows, cols, src, lds, dst, ldd, rp, _s = a
         es = ES[dt]
         out += [("src", src, _rows(rows, lds, cols, es)), ("dst", dst, _rows(cols, ldd, rp, es))]
+    elif name == "icap_transpose_batch":
+        n, ptr, _s = a
+        from icap import _lib as _L
+        addr = ptr.value if hasattr(ptr, "value") else ptr
+        for it in (_L.TransposeItem * n).from_address(addr):
+            out += [("src", it.src, _rows(it.rows, it.lds, it.cols, 2)), ("dst", it.dst, _rows(it.cols, it.ldd, it.rows, 2))]
     elif name == "icap_colsum":
         dt, M, N, src, ld, o, _acc, ws, _s = a
         out += [("src", src, _rows(M, ld, N, ES[dt])), ("out", o, N * 4), ("ws", ws, ops.colsum_workspace(M, N))]

@@ -558,3 +558,15 @@ def test_cross_entropy_rows_dev(dev):
     assert abs(loss.item() - ref.item()) < 1e-5 * max(1, abs(ref.item()))
     assert rel_err(dl[:nr, :V], gx) < 1e-4
     assert torch.all(dl[nr:] == 5.0)
+
+
+def test_transpose_batch_equals_single(dev):
+    """icap_transpose_batch (one launch over the mapper's transposed weight copies) == per-matrix transposes,
+    including an item the tile path cannot take (rows % 64 != 0: falls back inside the library)"""
+    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072), (130, 96)] * 7  # 35 items: two launches
+    srcs = [rnd(sh, dev, torch.bfloat16, seed=70 + i) for i, sh in enumerate(shapes)]
+    outs = [torch.full((sh[1], sh[0]), 5.0, device=dev, dtype=torch.bfloat16) for sh in shapes]
+    ops.transpose_batch(zip(srcs, outs))
+    torch.cuda.synchronize()
+    for s_, o in zip(srcs, outs):
+        assert torch.equal(o, s_.t())
