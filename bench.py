@@ -41,18 +41,31 @@ class GemmTimer:
         self.rec = []
 
     def launch(self, key, flops, fn):
+        from icap import ops
+
         s = torch.cuda.current_stream()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
         fn()
         e1.record(s)
-        self.rec.append((key, flops, e0, e1))
+        self.rec.append((key, flops, e0, e1, ops.TIMER_TAG))
+
+    def tagged(self, tag):
+        """(launches, algorithmic FLOPs, ms) of the launches recorded under ops.timer_tag(tag) (GEMMs + attention)."""
+        torch.cuda.synchronize()
+        n, fl, ms = 0, 0.0, 0.0
+        for _, f, e0, e1, t in self.rec:
+            if t == tag:
+                n, fl, ms = n + 1, fl + f, ms + e0.elapsed_time(e1)
+        return n, fl, ms
 
     def summary(self, detail_path=None):
         """Aggregate per kernel instantiation (what rocprof reports per kernel name); optional per-shape dump."""
         torch.cuda.synchronize()
         agg, shapes = {}, {}
-        for (kind, desc), fl, e0, e1 in self.rec:
+        for (kind, desc), fl, e0, e1, tag in self.rec:
+            if kind.startswith("attn"):  # attention launches: only in the tagged (GPT-2 block) aggregate
+                continue
             ms = e0.elapsed_time(e1)
             for d, k in ((agg, kind), (shapes, (kind, desc))):
                 a = d.setdefault(k, [0, 0.0, 0.0])
@@ -60,6 +73,12 @@ class GemmTimer:
                 a[1] += fl
                 a[2] += ms
         if detail_path:
+            for (kind, desc), fl, e0, e1, tag in self.rec:
+                if kind.startswith("attn"):
+                    a = shapes.setdefault((kind, desc), [0, 0.0, 0.0])
+                    a[0] += 1
+                    a[1] += fl
+                    a[2] += e0.elapsed_time(e1)
             with open(detail_path, "w") as f:
                 for (kind, desc), (n, fl, ms) in sorted(shapes.items(), key=lambda kv: -kv[1][2]):
                     f.write(f"{kind:10s} {desc:60s} n={n:3d} total_ms={ms:8.3f} avg_us={ms / n * 1e3:9.1f} "
@@ -67,12 +86,12 @@ class GemmTimer:
         return agg
 
 
-def live_rows(labels, P):
+def live_rows(labels, P, squares=False):
     """Host copy of the packed token-row count icap_caption_pack computes on the device (roofline pricing and the
-    GEMM kernel choice): per caption max(P, P + last caption index with a target)."""
+    GEMM kernel choice): per caption max(P, P + last caption index with a target); squares: sum of their squares."""
     from icap.engine import live_rows as lr
 
-    return lr(labels, P)
+    return lr(labels, P, squares=squares)
 
 
 def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16, fp8=False, pack=None):
@@ -420,7 +439,8 @@ def kernel_peak(name: str) -> float:
 
 def train_rate(trainer, B, steps, warmup, use_graph, world, dev):
     """images/s over `steps` graph-replayed steps after `warmup` (barrier + synchronize on both sides, max over
-    ranks), and the GEMM roofline of one eager step (HIP events around every GEMM launch)."""
+    ranks), the per-step median (HIP events between the steps on the launch stream), and the GEMM roofline of one
+    eager step (HIP events around every GEMM / GPT-2-block attention launch)."""
     from icap import ops
 
     dist = world > 1
@@ -430,15 +450,25 @@ def train_rate(trainer, B, steps, warmup, use_graph, world, dev):
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(steps):
+    evs[0].record()
+    for i in range(steps):
         trainer.micro_step(use_graph=use_graph)
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
+    median_ms = per_step[len(per_step) // 2] if steps % 2 else 0.5 * (per_step[steps // 2 - 1] + per_step[steps // 2])
+    rank_ms = [el / steps * 1e3]
     if dist:
+        mine = torch.tensor([el / steps * 1e3], device=dev, dtype=torch.float64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(allr, mine)
+        rank_ms = [float(x.item()) for x in allr]
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
@@ -456,10 +486,15 @@ def train_rate(trainer, B, steps, warmup, use_graph, world, dev):
     dom = max(agg, key=lambda k: agg[k][2])
     n_l, fl, ms = agg[dom]
     achieved = fl / (ms * 1e-3) / 1e12
+    bn, bfl, bms = timer.tagged("gpt2_block")
     return {"el": el, "loss": loss, "images_per_s": world * B * steps / el, "ms_per_step": el / steps * 1e3,
+            "median_ms": median_ms, "rank_ms": rank_ms,
             "dom": dom, "n_l": n_l, "fl": fl, "ms": ms, "achieved": achieved,
             "frac": achieved / kernel_peak(dom), "gemm_ms": sum(v[2] for v in agg.values()),
-            "all_fl": sum(v[1] for v in agg.values()), "eager_ms": eager_ms}
+            "all_fl": sum(v[1] for v in agg.values()), "eager_ms": eager_ms,
+            "block": {"launches": bn, "alg_tflop": round(bfl / 1e12, 4), "ms": round(bms, 3),
+                      "achieved": round(bfl / (bms * 1e-3) / 1e12, 1) if bms else None,
+                      "frac": round(bfl / (bms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, 4) if bms else None}}
 
 
 def padded_rate(config, B, dev, world, fp8=False, steps=10):
@@ -480,23 +515,57 @@ def padded_rate(config, B, dev, world, fp8=False, steps=10):
 
 def batch_sweep(config, batches, dev, world, fp8=False):
     """SURVEY.md §8(d) perf batch sweep: the same train step at other per-GPU batches (weak-scaling B is a free
-    choice; the reference's is config.yml:32 = 128): images/s and the dominant GEMM's roofline fraction."""
+    choice; the reference's is config.yml:32 = 128; BASELINE.md §4 also names 8 and 32): images/s and the dominant
+    GEMM's roofline fraction."""
     out = []
     for Bs in batches:
         model, tower, tr = build(Bs, dev, config=config, fp8=fp8)
         ids, mask, labels, px = synthetic_batch(Bs, 11, dev)
         tr.load_batch(ids, mask, labels, pixels=px)
         tr.gws.head_rows_hint = int((labels != -100).sum().item())
-        tr.gws.live_rows_hint = live_rows(labels, tr.P)
-        r = train_rate(tr, Bs, 5, 2, True, world, dev)
+        r = train_rate(tr, Bs, 10 if Bs <= 32 else 5, 2, True, world, dev)
         out.append({"batch_per_gpu": Bs, "images_per_s": round(r["images_per_s"], 1),
-                    "ms_per_step": round(r["ms_per_step"], 3), "dominant_kernel": r["dom"],
-                    "dominant_frac": round(r["frac"], 4), "dominant_tflops": round(r["achieved"], 1),
-                    "all_gemm_ms_per_step": round(r["gemm_ms"], 3)})
+                    "ms_per_step": round(r["ms_per_step"], 3), "ms_per_step_median": round(r["median_ms"], 3),
+                    "dominant_kernel": r["dom"], "dominant_frac": round(r["frac"], 4),
+                    "dominant_tflops": round(r["achieved"], 1), "all_gemm_ms_per_step": round(r["gemm_ms"], 3),
+                    "gpt2_block_frac": r["block"]["frac"]})
         del model, tower, tr
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
     return out
+
+
+def unfrozen_rate(B, dev, world, steps=10):
+    """freeze_gpt_weights=False (src/models.py:216-217, config.yml:21-22): the same step with every GPT-2 tensor
+    trained (dW products, LN / bias / tied-wte / wpe grads, AdamW over 185 M params, refreshed forward copies),
+    graph-replayed: images/s beside the CPU baseline's train_b8_unfrozen row."""
+    from types import SimpleNamespace
+
+    from icap import CaptionTrainer, GPT2LMHeadModel, ImageCaptioningModel, TransformerMappingNetwork
+    from icap.clip import CLIPVisionTower
+
+    gpt = GPT2LMHeadModel.random_init(seed=0)
+    mapper = TransformerMappingNetwork.random_init(seed=0)
+    model = ImageCaptioningModel(mapper, tokenizer=SimpleNamespace(eos_token_id=50256), gpt=gpt,
+                                 freeze_gpt_weights=False, compute_dtype=torch.bfloat16).to(dev)
+    tower = CLIPVisionTower.random_init(None, seed=0).to(dev)
+    tr = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10 ** 6, clip_model=tower, dropout=True,
+                        seed=1234)
+    ids, mask, labels, px = synthetic_batch(B, 1, dev)
+    tr.load_batch(ids, mask, labels, pixels=px)
+    r = train_rate(tr, B, steps, 3, True, world, dev)
+    res = {"images_per_s": round(r["images_per_s"], 1), "ms_per_step": round(r["ms_per_step"], 3),
+           "ms_per_step_median": round(r["median_ms"], 3), "batch_per_gpu": B,
+           "trained_params": int(tr.flat.n), "final_loss": round(r["loss"], 4),
+           "dominant_kernel": r["dom"], "dominant_frac": round(r["frac"], 4),
+           "all_gemm_ms_per_step": round(r["gemm_ms"], 3),
+           "workload": "as the headline (CLIP-B/32 fwd on pixels, dropout 0.1) with GPT-2 small trained: + every "
+                       "block's dW, LN / bias grads, tied-wte and wpe grads, AdamW over all of them; padded token "
+                       "rows and the full LM head (the tied wte gradient reads every row)"}
+    del model, tower, tr
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
 
 EDIM = {"small": 512, "medium": 768, "large": 1024}  # image-embedding width per config (CLIP-B/32, CLIP-L/14, DINOv3-L)
@@ -519,7 +588,8 @@ def main():
     ap.add_argument("--fp8", action="store_true",
                     help="configs[4]'s fp8 path: GPT-2's frozen products as MX block-scaled e4m3 GEMMs")
     ap.add_argument("--sweep", default=None,
-                    help="comma-separated extra per-GPU batches for the batch sweep (default: 256,512 for small)")
+                    help="comma-separated extra per-GPU batches for the batch sweep (default: 8,32,256,512 for small)")
+    ap.add_argument("--no-unfrozen", action="store_true", help="skip the freeze_gpt_weights=False line")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -550,6 +620,7 @@ def main():
     packed = bool(trainer.gws.pack)
     token_rows = live_rows(labels, trainer.P) if packed else B * trainer.gws.S
     trainer.gws.live_rows_hint = token_rows if packed else None
+    trainer.gws.seq_sq_hint = live_rows(labels, trainer.P, squares=True) if packed else None
     use_graph = not args.no_graph
     # timed region + the kernel roofline pass (every GEMM launch of one eager step, timed with HIP events)
     r = train_rate(trainer, B, args.steps, args.warmup, use_graph, world, dev)
@@ -576,18 +647,32 @@ def main():
     extract = extraction_child() if (not args.no_decode and args.config == "small" and rank == 0) else None
     parity = parity_mode_rate(B, dev) if (not args.no_decode and args.config == "small" and world == 1) else None
     sweep_b = [int(x) for x in args.sweep.split(",") if x] if args.sweep is not None else \
-        ([256, 512] if args.config == "small" and not args.no_decode and world == 1 else [])
+        ([8, 32, 256, 512] if args.config == "small" and not args.no_decode and world == 1 else [])
     want_padded = packed and not args.no_decode and world == 1
-    if sweep_b or want_padded:
+    want_unfrozen = args.config == "small" and not args.no_decode and not args.no_unfrozen and world == 1
+    # data-parallel bookkeeping (self-check of an N > 1 line: what torch.distributed saw and what went over RCCL)
+    dp = None
+    if dist:
+        flat_n = int(trainer.flat.n)
+        bpe = 2 if trainer.dp_bf16 else 4
+        dp = {"world_size_seen": torch.distributed.get_world_size(), "backend": torch.distributed.get_backend(),
+              "rank_ms_per_step": [round(x, 3) for x in r["rank_ms"]],
+              "allreduce_bytes_per_step": flat_n * bpe, "allreduce_dtype": "bf16" if trainer.dp_bf16 else "fp32",
+              "buckets": len(trainer._ranges_mapper) + 1 if trainer.dp_overlap else 1,
+              "overlapped": bool(trainer.dp_overlap)}
+    if sweep_b or want_padded or want_unfrozen:
         del model, tower, trainer
         torch.cuda.empty_cache()
     padded = padded_rate(args.config, B, dev, world, args.fp8) if want_padded else None
+    unfrozen = unfrozen_rate(B, dev, world) if want_unfrozen else None
     sweep = batch_sweep(args.config, sweep_b, dev, world, args.fp8) if sweep_b else None
 
     if rank == 0:
         res = {
             "metric": METRIC, "value": round(imgs_per_s, 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "ms_per_step_median": round(r["median_ms"], 3),
+            "padded_images_per_s": padded["images_per_s"] if padded else None,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp8 (MX e4m3, GPT-2 products) + bf16" if args.fp8 else "bf16",
             "data": "synthetic (seeded COCO-shaped captions: 13 tokens + EOS, padded to 50; randn 224x224 pixels); "
@@ -623,6 +708,8 @@ def main():
             "clip_preprocess": prep,
             "clip_extraction": extract,
             "fp32_parity_mode": parity,
+            "train_unfrozen": unfrozen,
+            "data_parallel": dp,
             "batch_sweep": sweep,
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1),
                          "peak": kernel_peak(dom), "unit": "TFLOP/s", "frac": round(achieved / kernel_peak(dom), 4),
@@ -632,6 +719,10 @@ def main():
                          "alg_gflop_per_launch": round(fl / n_l / 1e9, 3),
                          "all_gemm_ms_per_step": round(gemm_ms, 3), "all_gemm_tflop_per_step": round(all_fl / 1e12, 4),
                          "eager_step_ms": round(eager_ms, 3),
+                         "gpt2_block": dict(r["block"], peak=BF16_PEAK_TFLOPS, unit="TFLOP/s",
+                                            what="the 12 GPT-2 blocks' GEMMs (fwd + dX) and attention (fwd + bwd) of "
+                                                 "one eager step: summed algorithmic FLOPs (live rows) / summed "
+                                                 "HIP-event time"),
                          "timing": "HIP events around every GEMM launch of one eager step on its launch stream "
                                    "(the timed region replays a HIP graph, which cannot host per-kernel events)"},
         }

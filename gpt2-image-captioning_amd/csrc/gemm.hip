@@ -129,10 +129,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   const int64_t nrows = N - n0 < BN ? N - n0 : BN;
   // (K-outer: the last row's range ends on a whole 16-byte chunk — the hardware zeroes a dword that crosses
   // num_records — which lda % 8 == 0, lda >= M keeps inside the allocation)
-  const __amdgpu_buffer_rsrc_t ra_rsrc =
-      make_rsrc(Ab, (uint64_t)(KOUT ? (K - 1) * p.lda + ((mrows + 7) & ~7ll) : (mrows - 1) * p.lda + K) * ES);
-  const __amdgpu_buffer_rsrc_t rb_rsrc =
-      make_rsrc(Bb, (uint64_t)(KOUT ? (K - 1) * p.ldb + ((nrows + 7) & ~7ll) : (nrows - 1) * p.ldb + K) * ES);
+  // timing diagnostic only (ICAP_GEMM_DIAG, never set in a real run): bits 28-29 of nk_split give the A / B
+  // descriptor zero records, so the range check drops that operand's staging loads (cdna_hip_programming.md §7:
+  // pricing one buffer's traffic) while the instruction stream, waits and barriers stay
+  const int diag = (nk_split >> 28) & 3;
+  const __amdgpu_buffer_rsrc_t ra_rsrc = make_rsrc(
+      Ab, (diag & 1) ? 0 : (uint64_t)(KOUT ? (K - 1) * p.lda + ((mrows + 7) & ~7ll) : (mrows - 1) * p.lda + K) * ES);
+  const __amdgpu_buffer_rsrc_t rb_rsrc = make_rsrc(
+      Bb, (diag & 2) ? 0 : (uint64_t)(KOUT ? (K - 1) * p.ldb + ((nrows + 7) & ~7ll) : (nrows - 1) * p.ldb + K) * ES);
   // LDS-DMA staging (buffer_load_dwordx4 ... lds): one wave-instruction writes 1 KiB = 8 LDS rows of
   // 128 B linearly (lane l -> row l>>3, physical chunk l&7). The XOR swizzle therefore goes on the SOURCE:
   // physical chunk pc of row r holds logical K-chunk pc ^ (r & 7) (cdna_hip_programming.md §5.4 rule 21).
@@ -186,8 +190,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  // K-skew (host: kskew_for): bits 20+ of nk_split rotate this tile's k-step order within its K range
-  const int kskew = nk_split >> 20;
+  // K-skew (host: kskew_for): bits 20-27 of nk_split rotate this tile's k-step order within its K range
+  const int kskew = (nk_split >> 20) & 0xFF;
   nk_split &= 0xFFFFF;
   const int nk_all = (int)((K + BKE - 1) / BKE);
   const int kt0 = split * nk_split;
@@ -415,7 +419,17 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       __hip_atomic_store(cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // every payload load below is sc1 (no stale L1 copy)
+    // Visibility without an agent-scope acquire (MI355X_MICROARCH.md "Valid forms", sc1 hand-off): every payload
+    // byte was stored sc1 (write-through, dropped from the producer XCD's L2) and drained (vmcnt(0)) by every storing
+    // wave before that block's barrier and its relaxed agent-scope add; every load below is an sc1 buffer load to
+    // registers (L1 bypassed), issued after the relaxed poll matched (lane 0) and the barrier above (other waves).
+    // A stale copy could only sit in THIS XCD's L2 if something on it had read the slot during this launch before
+    // the poll matched: nothing does (a slot is read only by its tile's last arriver, after the poll), and the
+    // dispatch of a launch invalidates the L2's copies from earlier launches. The alternative, an agent acquire
+    // fence (buffer_inv sc1 + vmcnt(0)), costs the last arriver ~1.7 us (x2 at 2 blocks / CU) on a ~36 us launch;
+    // a release add costs every publishing split a buffer_wbl2. tests/test_fused_splitk_gpu.py checks every output
+    // word (eager, graph, concurrent streams). If a launch faults, the tickets may be left non-zero: the HIP context
+    // is unusable after a device fault anyway; a new process (or re-zeroed tickets) starts clean.
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(pbase, (uint64_t)PB * splits);
     // the other splits' partials, GI accumulator rows at a time (all loads of a group in flight together; one row
     // at 3-4 blocks per CU, whose register budget is 170 / 128)
@@ -1027,7 +1041,13 @@ static int fused_s_override() {
 static int kskew_for(const icap_gemm_args& p, int64_t nk_split) {
   static const int v = [] { const char* e = getenv("ICAP_KSKEW"); return e ? atoi(e) : 1; }();
   if (p.path == 1 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
-  return v > 0 && v < 2048 ? v : 0;
+  return v > 0 && v < 256 ? v : 0;
+}
+// ICAP_GEMM_DIAG = 1 / 2 / 3: drop the A / B / both operands' staging loads of the tile kernels (zero-record
+// descriptors) — a timing diagnostic for what the operand traffic costs; the outputs are wrong. Never in a real run.
+static int gemm_diag() {  // (read per launch: an A/B driver toggles it in one process)
+  const char* e = getenv("ICAP_GEMM_DIAG");
+  return e ? (atoi(e) & 3) : 0;
 }
 static bool spec_act_on() {  // ICAP_SPEC_ACT=0: the runtime-dispatch epilogue everywhere (A/B only)
   static const bool v = [] { const char* e = getenv("ICAP_SPEC_ACT"); return !(e && e[0] == '0'); }();
@@ -1143,23 +1163,36 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // with a device row count the kernel choice follows the expected count (m_hint)
   const int64_t m_plan = (p.m_dev && p.m_hint > 0 && p.m_hint < p.M) ? p.m_hint : p.M;
   const int64_t tiles_plan = ((m_plan + GBM - 1) / GBM) * tiles_n;
+  // The split count is a function of the shape (M, N, K, dtype, trans_ab; with a device row count, the caller's
+  // expected count m_hint) alone — never of the workspace size or of whether tickets are attached — so the partial
+  // sums are always added in the same order. Tickets only choose HOW the splits combine (inside the launch or in a
+  // reduce pass over slabs); both add the partials in split order starting from split 0 and apply the same epilogue
+  // formula, so the two mechanisms store bitwise-identical outputs (tests/test_fused_splitk_gpu.py). A NULL workspace
+  // turns the automatic split off (documented: include/icap.h); a given one too small for the shape's split is an error.
   int64_t splits = 1;
   pl.fused = false;
+  bool fusable = false;  // the long-K / few-tiles rule below (the splits may combine inside the launch)
   // (not for the K-outer weight-gradient products: measured, their in-launch combine ran 6-7 µs slower than the
   // slab + reduce pass — 768x3072x3200 53 vs 47 µs, profiles/r03_gemm_detail_fused.txt — since the last arriver of
   // a 3-block-per-CU tile reads its partials one accumulator row at a time)
-  if (p.split_k == 0 && p.tickets && p.workspace && !p.trans_ab && (p.N & 3) == 0 && nk >= 24 && tiles_plan < cus) {
+  if (p.split_k == 0 && p.workspace && !p.trans_ab && (p.N & 3) == 0 && nk >= 24 && tiles_plan < cus) {
     int64_t sf = (2 * cus + tiles_plan / 2) / tiles_plan;
     if (sf > 4) sf = 4;
     while (sf > 2 && nk / sf < 8) --sf;
-    if (fused_s_override() > 1) sf = fused_s_override();  // A/B measurements only (ICAP_FUSED_S)
-    const int64_t pbytes = (int64_t)GBM * GBN * (int64_t)sizeof(float);
-    if (sf >= 2 && p.tickets_len >= 2 * tiles && p.workspace_bytes >= tiles * sf * pbytes) {
+    // A/B measurements only (ICAP_FUSED_S): the in-launch combine reads at most 3 other partials (4 splits)
+    if (fused_s_override() > 1) sf = fused_s_override() < 4 ? fused_s_override() : 4;
+    if (sf >= 2) {
       splits = sf;
-      pl.fused = true;
+      fusable = true;
     }
   }
-  if (pl.fused) {
+  if (fusable) {
+    const int64_t pbytes = (int64_t)GBM * GBN * (int64_t)sizeof(float);
+    const int64_t sfin = splits;
+    const int64_t nks_ = (nk + sfin - 1) / sfin;
+    const int64_t sreal = (nk + nks_ - 1) / nks_;  // the split count after every split got >= 1 stage (below)
+    // with a device row count the grid still covers every row tile of M, so tickets / partials for all of them
+    pl.fused = p.tickets && p.tickets_len >= 2 * tiles && p.workspace_bytes >= tiles * sreal * pbytes;
   } else if (p.split_k > 1) {
     splits = p.split_k;
   } else if (p.split_k == 0 && p.workspace && p.trans_ab && (p.N & 3) == 0 && nk >= 16 && tiles < 320) {
@@ -1335,7 +1368,7 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   if (pl.g256) return gemm256_launch(p, thr, inv_keep, s);
   const dim3 grid = pl.grid, block = pl.block;
   const int sp = pl.splits, tn = pl.tiles_n;
-  const int nks = pl.nk_split | (kskew_for(p, pl.nk_split) << 20);
+  const int nks = pl.nk_split | (kskew_for(p, pl.nk_split) << 20) | (gemm_diag() << 28);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
 #define ICAP_GK(TI, TC, NST, MINB, TM_, TN_, KOUT)                                                              \
   do {                                                                                                       \

@@ -152,6 +152,7 @@ class CaptionTrainer:
             # the first batch's packed row count (one host read, before any capture): the GEMM kernel choice for the
             # expected live rows (icap_gemm_args.m_hint); the device count of every batch is what bounds the work
             self.gws.live_rows_hint = live_rows(labels, self.P)
+            self.gws.seq_sq_hint = live_rows(labels, self.P, squares=True)
         self.ids.copy_(ids, non_blocking=True)
         self.mask.copy_(mask, non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)
@@ -432,13 +433,15 @@ class CaptionTrainer:
 
 
 @torch.no_grad()
-def live_rows(labels: Tensor, P: int) -> int:
+def live_rows(labels: Tensor, P: int, squares: bool = False) -> int:
     """Packed token rows of a batch (icap_caption_pack's m_live, computed on the host side of the copy):
-    sum over captions of max(P, P + last caption index with a target)."""
+    sum over captions of max(P, P + last caption index with a target); squares: the sum of their squares (the
+    attention launches' work)."""
     valid = (labels != -100).to(torch.int64)
     pos = torch.arange(1, labels.shape[1] + 1, device=labels.device, dtype=torch.int64)
     last = (valid * pos).max(dim=1).values  # last target index + 1, or 0
-    return int((P + (last - 1).clamp_min(0)).sum().item())
+    lens = P + (last - 1).clamp_min(0)
+    return int((lens * lens if squares else lens).sum().item())
 
 
 def broadcast_replicas(modules, process_group=None) -> None:

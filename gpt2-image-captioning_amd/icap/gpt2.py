@@ -376,6 +376,7 @@ class GPT2Core:
         ws.head_rows_hint = None  # host-known number of target rows (roofline bookkeeping only)
         ws.pack = bool(pack and ws.compact)
         ws.live_rows_hint = None  # host-known number of packed rows (roofline bookkeeping only)
+        ws.seq_sq_hint = None  # host-known sum of squared packed sequence lengths (attention FLOPs, bookkeeping only)
         ws.seqs = ws.m_live = None
         if ws.pack:
             ws.seq_off = e(B, dtype=torch.int32)
@@ -491,18 +492,34 @@ class GPT2Core:
             ops.cross_entropy(ws.logits, self.V, ws.labels_c if cp else ws.labels_shift, ws.n_valid, ws.loss, dl,
                               ws.ce_ws, grad_scale, rows=ws.Mh, rows_dev=ws.n_valid if cp else None)
 
+    def _attn_flops(self, ws, B, S, bwd: bool = False) -> Optional[float]:
+        """Algorithmic FLOPs of one attention launch (bench timing only): QK^T and PV over each sequence's live
+        tokens, dense S x S as the reference's SDPA computes them (4 S^2 hd per head forward; the backward's five
+        products 10 S^2 hd); None when no host-side count of the packed lengths is known."""
+        sq = getattr(ws, "seq_sq_hint", None)
+        if sq is None:
+            sq = None if getattr(ws, "pack", False) else B * S * S
+        if sq is None:
+            return None
+        return (10.0 if bwd else 4.0) * sq * self.hd * self.H
+
     def _blocks_fwd(self, ws, dr, B, S, M, causal_mask):
+        with ops.timer_tag("gpt2_block"):
+            self._blocks_fwd_(ws, dr, B, S, M, causal_mask)
+
+    def _blocks_fwd_(self, ws, dr, B, S, M, causal_mask):
         D, H, hd = self.D, self.H, self.hd
         scale = 1.0 / math.sqrt(hd)
         rd = getattr(ws, "m_live", None)  # packed rows: device row count (None: every row)
         seqs = getattr(ws, "seqs", None)
+        afl = self._attn_flops(ws, B, S)
         for l, lw in enumerate(self.layers):
             x = ws.x[l]
             q = lw if self.fp8 else SimpleNamespace(qw_attn_t=None, qw_proj_t=None, qw_fc_t=None, qw_mp_t=None)
             ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, ws.a1[l], ws.mean1[l], ws.rstd1[l], rows_dev=rd)
             self._bmm(ws, ws.a1[l], ws.qD, lw.w_attn_t, q.qw_attn_t, ws.qkv[l], bias=lw.b_attn)
             ops.attention_fwd(ws.qkv[l], ws.o[l], B=B, S=S, H=H, hd=hd, scale=scale, causal=True, key_mask=causal_mask,
-                              lse=ws.lse[l], drop=dr.attn(l), seqs=seqs)
+                              lse=ws.lse[l], drop=dr.attn(l), seqs=seqs, alg_flops=afl)
             self._bmm(ws, ws.o[l], ws.qD, lw.w_proj_t, q.qw_proj_t, ws.h1[l], bias=lw.b_proj, resid=x, drop=dr.ra(l))
             ops.layernorm_fwd(ws.h1[l], lw.ln2_g, lw.ln2_b, self.eps, ws.a2[l], ws.mean2[l], ws.rstd2[l], rows_dev=rd)
             self._bmm(ws, ws.a2[l], ws.qD, lw.w_fc_t, q.qw_fc_t, ws.f[l], bias=lw.b_fc, act=L.ACT_GELU_NEW,
@@ -537,6 +554,9 @@ class GPT2Core:
                           dbeta=grads.lnf_b if grads else None, workspace=dw.ln_ws if dw else None,
                           dy_rowmap=ws.row_slot if cp else None, rows_dev=rd)
         dres, dnew = ws.dx, ws.dx2
+        afl = self._attn_flops(ws, B, S, bwd=True)
+        tag = ops.timer_tag("gpt2_block")
+        tag.__enter__()
         for l in reversed(range(nl)):
             lw = self.layers[l]
             g = grads.layers[l] if grads is not None else None
@@ -560,7 +580,7 @@ class GPT2Core:
                 dw.db(dy, g.b_proj, M=M)
             self._bmm(ws, dy, ws.qD, lw.w_proj, q.qw_proj, ws.do)
             ops.attention_bwd(ws.qkv[l], ws.do, ws.lse[l], ws.dqkv, B=B, S=S, H=H, hd=hd, scale=scale, causal=True,
-                              key_mask=causal_mask, drop=dr.attn(l), out=ws.o[l], seqs=seqs)
+                              key_mask=causal_mask, drop=dr.attn(l), out=ws.o[l], seqs=seqs, alg_flops=afl)
             if g is not None:
                 dw.dW(ws.dqkv, ws.a1[l], g.w_attn, M=M, transpose_out=True)
                 dw.db(ws.dqkv, g.b_attn, M=M)
@@ -570,6 +590,7 @@ class GPT2Core:
                               drop=nxt, dgamma=g.ln1_g if g else None, dbeta=g.ln1_b if g else None,
                               workspace=dw.ln_ws if dw else None, rows_dev=rd)
             dres, dnew = dnew, dres
+        tag.__exit__(None, None, None)
         d_in = ws.dxd if dr.embd.p > 0 else dres
         if ws.pack:  # the prefix rows' gradient, back in the padded layout the mapper backward reads
             ops.rows_unpack(d_in, ws.seq_off, ws.seq_len, ws.d_emb, B=B, P=ws.P, D=D, dst_bstride=S * D)

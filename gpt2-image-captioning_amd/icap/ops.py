@@ -273,7 +273,27 @@ def gemm_workspace(device, stream=None) -> Tensor:
     return ws
 
 
-GEMM_TIMER = None  # set to an object with .launch(key, flops, fn) to time every GEMM launch
+GEMM_TIMER = None  # set to an object with .launch(key, flops, fn) to time every GEMM (and attention) launch
+TIMER_TAG = None  # label the timer records of the launches issued inside timer_tag(...) (bench roofline groups)
+
+
+@contextlib.contextmanager
+def timer_tag(tag: str):
+    """Label every launch GEMM_TIMER records in this block (e.g. "gpt2_block": bench.py's GPT-2-block roofline)."""
+    global TIMER_TAG
+    old, TIMER_TAG = TIMER_TAG, tag
+    try:
+        yield
+    finally:
+        TIMER_TAG = old
+
+
+def _timed(kind: str, desc: str, flops: Optional[float], fn) -> None:
+    """Run fn (one C-ABI launch); under GEMM_TIMER with HIP events around it (never inside a captured graph)."""
+    if GEMM_TIMER is None or flops is None:
+        fn()
+    else:
+        GEMM_TIMER.launch((kind, desc), flops, fn)
 
 
 def layernorm_fwd(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, y: Tensor, mean: Optional[Tensor],
@@ -326,24 +346,29 @@ def _attn_args(qkv: Tensor, B: int, S: int, H: int, hd: int, rsb: int, rss: int,
 
 def attention_fwd(qkv: Tensor, out: Tensor, *, B: int, S: int, H: int, hd: int, scale: float,
                   causal: bool = False, key_mask: Optional[Tensor] = None, lse: Optional[Tensor] = None,
-                  drop: Dropout = NO_DROP, rsb: Optional[int] = None, rss: int = 1, seqs=None) -> Tensor:
-    """seqs: (seq_off, seq_len) device int32 [B] — packed sequences (include/icap.h icap_attn_args)."""
+                  drop: Dropout = NO_DROP, rsb: Optional[int] = None, rss: int = 1, seqs=None,
+                  alg_flops: Optional[float] = None) -> Tensor:
+    """seqs: (seq_off, seq_len) device int32 [B] — packed sequences (include/icap.h icap_attn_args).
+    alg_flops: algorithmic FLOPs of the launch (bench timing only; None: not timed)."""
     a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop, seqs)
     a.out, a.ld_out = out.data_ptr(), _ld(out)
-    call("icap_attention_fwd", C.byref(a), _stream())
+    _timed("attn_fwd", f"B{B} S{S} H{H} hd{hd}{' packed' if seqs is not None else ''}", alg_flops,
+           lambda: call("icap_attention_fwd", C.byref(a), _stream()))
     return out
 
 
 def attention_bwd(qkv: Tensor, dout: Tensor, lse: Tensor, dqkv: Tensor, *, B: int, S: int, H: int, hd: int,
                   scale: float, causal: bool = False, key_mask: Optional[Tensor] = None, drop: Dropout = NO_DROP,
-                  rsb: Optional[int] = None, rss: int = 1, out: Optional[Tensor] = None, seqs=None) -> Tensor:
+                  rsb: Optional[int] = None, rss: int = 1, out: Optional[Tensor] = None, seqs=None,
+                  alg_flops: Optional[float] = None) -> Tensor:
     """out: the forward's O (optional; enables the transpose-free bf16 MFMA backward). seqs: as attention_fwd."""
     a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop, seqs)
     if out is not None:
         a.out, a.ld_out = out.data_ptr(), _ld(out)
     a.dout, a.ld_dout = dout.data_ptr(), _ld(dout)
     a.dqkv, a.ld_dqkv = dqkv.data_ptr(), _ld(dqkv)
-    call("icap_attention_bwd", C.byref(a), _stream())
+    _timed("attn_bwd", f"B{B} S{S} H{H} hd{hd}{' packed' if seqs is not None else ''}", alg_flops,
+           lambda: call("icap_attention_bwd", C.byref(a), _stream()))
     return dqkv
 
 

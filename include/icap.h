@@ -88,11 +88,12 @@ typedef struct {
   float drop_p; uint64_t seed; uint64_t offset;
   const uint64_t* seed_ptr;               /* optional device seed counter */
   /* split-K: fp32 scratch of >= splits*M*N*4 bytes (16-byte aligned) or NULL.   */
-  /* split_k: 0 = automatic (only launches of <= 64 output tiles, N % 4 == 0,   */
+  /* split_k: 0 = automatic (launches that cannot fill the chip, N % 4 == 0,    */
   /* and only when the workspace is given), 1 = never, > 1 = forced.            */
   /* The partial sums are reduced in a fixed order (deterministic). The split   */
-  /* count is a function of (M, N, K, dtype) only: a workspace smaller than     */
-  /* that split needs is ICAP_ERR_ARG, never a different summation order.       */
+  /* count is a function of (M, N, K, dtype, trans_ab, m_hint) only — never of  */
+  /* the workspace size or of the tickets: a workspace smaller than that split  */
+  /* needs is ICAP_ERR_ARG, never a different summation order.                  */
   void* workspace; int64_t workspace_bytes; int32_t split_k;
   /* optional device-side row count (int32, <= M): only rows < *m_dev are     */
   /* computed and stored; the launch geometry stays sized for M, so a graph   */
@@ -125,7 +126,9 @@ typedef struct {
   /* launch leaves them zero. With it (and the workspace), automatic split-K over few output tiles (long K, fewer  */
   /* tiles than CUs) combines the partial tiles inside the launch — the last split of a tile to finish adds the    */
   /* others' partials in split order and applies the epilogue — instead of a separate reduce pass over fp32 slabs. */
-  /* Needs 2 entries per 128 x 128 output tile. One buffer per stream (like workspace); deterministic.            */
+  /* Needs 2 entries per 128 x 128 output tile. One buffer per stream (like workspace); deterministic. The tickets */
+  /* choose only the mechanism: without them (or too few) the same split runs through the reduce pass, and both   */
+  /* store bitwise-identical outputs. After a device fault the tickets may be left non-zero (zero them again).    */
   int32_t* tickets; int64_t tickets_len;
   /* ln_wsum != NULL (M <= 128, no ln_gamma): LayerNorm folded into the weights — B holds W[n,k] * gamma[k],  */
   /* ln_wsum[n] = sum_k B[n,k] (fp32, over the stored B values) and bias = b + W . beta, so                    */

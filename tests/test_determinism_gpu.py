@@ -40,13 +40,6 @@ def _same(a, b):
     return bool(((a == b) | (a.isnan() & b.isnan())).all())
 
 
-def _same(a, b):
-    """Equal values with NaN == NaN: the compact LM head leaves the logits rows past the device's target count
-    unwritten, so they hold whatever an earlier allocation left there (NaN patterns included, which torch.equal
-    never calls equal)."""
-    return bool(((a == b) | (a.isnan() & b.isnan())).all())
-
-
 def _noise(dev, n):
     s = torch.cuda.Stream(dev)
     a = torch.randn((4096, 4096), device=dev).to(torch.bfloat16)

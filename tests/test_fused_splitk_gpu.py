@@ -76,26 +76,48 @@ def test_fused_split_k(dev, M, live, N, K, epi, kout):
     if live is not None:
         kw.update(m_dev=torch.tensor([live], dtype=torch.int32, device=dev), m_hint=live)
     rows = live or M
-    outs = []
-    names = []
-    for split in (0, 0, 1):  # fused (twice: determinism), then unsplit
+    outs, auxs, names = [], [], []
+    # fused (twice: determinism); the same split through a caller-supplied workspace (no tickets: slab + reduce
+    # pass, same split count by the shape rule); unsplit
+    ws_own = torch.empty(4 * M * N, dtype=torch.float32, device=dev)
+    for split, ws in ((0, None), (0, None), (0, ws_own), (1, None)):
         C = C0.clone()
-        names.append(_kernel_names(lambda: ops.gemm(A, B, C, split_k=split, **kw)))
+        if "aux" in kw:
+            kw["aux"] = torch.zeros((M, N), device=dev, dtype=cdt)
+        names.append(_kernel_names(lambda: ops.gemm(A, B, C, split_k=split, workspace=ws, **kw)))
         outs.append(C)
+        auxs.append(kw.get("aux"))
     torch.cuda.synchronize()
     assert len(names[0]) == 1 and names[0][0][1] >= 2 and names[0][0][2] == 1, names[0]  # combined in the launch
-    assert names[2][0][1] == 1, names[2]
+    assert names[2][0][1] == names[0][0][1] and names[2][0][2] == 0, names[2]  # same split, reduce pass
+    assert names[3][0][1] == 1, names[3]
     assert torch.equal(outs[0], outs[1])
-    a, b = outs[0][:rows].float(), outs[2][:rows].float()
-    if "aux" in kw:
-        assert torch.equal(kw["aux"], kw["aux"])  # (written by the fused launch: compared through C below)
-    if cdt == torch.bfloat16:
-        assert float((a - b).abs().max() / b.abs().max()) < 1.6e-2
-        assert float(((a - b).abs() > 1e-2 * b.abs().max()).float().mean()) < 1e-3
-    else:
-        assert float((a - b).abs().max() / b.abs().max()) < 1e-5
+    # the split count is a function of the shape alone: the slab mechanism sums in the same order (bitwise equal)
+    assert torch.equal(outs[0], outs[2])
+    a, b = outs[0][:rows].float(), outs[3][:rows].float()
+
+    def close(a, b):
+        if cdt == torch.bfloat16:
+            assert float((a - b).abs().max() / b.abs().max()) < 1.6e-2
+            assert float(((a - b).abs() > 1e-2 * b.abs().max()).float().mean()) < 1e-3
+        else:
+            assert float((a - b).abs().max() / b.abs().max()) < 1e-5
+
+    close(a, b)
+    if "aux" in kw:  # the pre-activation the fused launch stored, against the unsplit launch's
+        assert torch.equal(auxs[0], auxs[2])
+        close(auxs[0][:rows].float(), auxs[3][:rows].float())
     if live is not None:
         assert torch.equal(outs[0][live:], C0[live:])
     ws = ops.gemm_workspace(dev, torch.cuda.current_stream(dev))
     tk = ops._gemm_tickets[ws.data_ptr()]
     assert int(torch.count_nonzero(tk)) == 0  # left zero for the next launch
+
+
+def test_workspace_too_small_raises(dev):
+    """A caller workspace smaller than the shape's split needs is an error, never a different split."""
+    A = torch.randn((3200, 3072), device=dev).to(torch.bfloat16)
+    B = torch.randn((768, 3072), device=dev).to(torch.bfloat16)
+    C = torch.empty((3200, 768), device=dev, dtype=torch.bfloat16)
+    with pytest.raises(L.IcapError):
+        ops.gemm(A, B, C, workspace=torch.empty(1024, dtype=torch.float32, device=dev))

@@ -1,0 +1,20 @@
+#!/bin/bash
+# round-4 GPU pass: every -m gpu test, the default bench line (with the per-shape GEMM / attention table of its
+# eager roofline pass), and a rocprofv3 kernel-time table of the packed train step. Stops at the first failing step.
+# usage: tools/gpu_r04.sh TAG [skip-tests]
+set -o pipefail
+R=$(cd "$(dirname "$0")/.." && pwd); T=${1:-r4}; O=$R/gpurun_out/$T; mkdir -p $O; cd $R
+export PYTHONUNBUFFERED=1
+if [ "$2" != "skip-tests" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+  rc=$?; grep -E "FAIL|Error|passed|failed" $O/pytest.log | tail -6; [ $rc -eq 0 ] || exit $rc
+fi
+ICAP_GEMM_DETAIL=$O/gemm_detail.txt timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err
+rc=$?; tail -1 $O/bench.json | cut -c1-400; [ $rc -eq 0 ] || { tail -5 $O/bench.err; exit $rc; }
+cd /tmp; export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/p -o run -- python3 $R/bench.py --steps 8 --warmup 3 --no-decode --no-cpu-baseline --sweep "" > $O/prof_bench.json 2> $O/prof.err
+rc=$?; [ $rc -eq 0 ] || { tail -5 $O/prof.err; exit $rc; }
+cd $R && python tools/kstats.py $O/p/run_results.db "packed bench train step x (3 warm-up + 8 timed + 1 eager roofline pass)" > $O/kstats.txt && head -14 $O/kstats.txt | cut -c1-150
+rm -rf $O/p
+timeout -k 10 300 python -u tools/gemm_diag.py > $O/gemm_diag.txt 2>&1 || { tail -5 $O/gemm_diag.txt; exit 1; }
+cat $O/gemm_diag.txt
