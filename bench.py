@@ -477,10 +477,17 @@ def train_rate(trainer, B, steps, warmup, use_graph, world, dev):
     ops.GEMM_TIMER = timer
     torch.cuda.synchronize()
     te0 = time.perf_counter()
-    trainer._fwd_bwd(True, trainer.grad_scale())
+    segs = trainer._segments(True, trainer.grad_scale())
+    sev = [torch.cuda.Event(enable_timing=True) for _ in range(len(segs) + 1)]
+    sev[0].record()
+    for i, (rng, fn) in enumerate(segs):  # the data-parallel buckets' segments, timed (eager, with GEMM events)
+        fn()
+        sev[i + 1].record()
     trainer._optimizer()
     torch.cuda.synchronize()
     eager_ms = (time.perf_counter() - te0) * 1e3
+    seg_ms = [round(sev[i].elapsed_time(sev[i + 1]), 3) for i in range(len(segs))]
+    seg_bytes = [sum(hi - lo for lo, hi in rng) * 4 for rng, _ in segs]
     ops.GEMM_TIMER = None
     agg = timer.summary(os.environ.get("ICAP_GEMM_DETAIL"))
     dom = max(agg, key=lambda k: agg[k][2])
@@ -488,7 +495,7 @@ def train_rate(trainer, B, steps, warmup, use_graph, world, dev):
     achieved = fl / (ms * 1e-3) / 1e12
     bn, bfl, bms = timer.tagged("gpt2_block")
     return {"el": el, "loss": loss, "images_per_s": world * B * steps / el, "ms_per_step": el / steps * 1e3,
-            "median_ms": median_ms, "rank_ms": rank_ms,
+            "median_ms": median_ms, "rank_ms": rank_ms, "seg_ms": seg_ms, "seg_bytes": seg_bytes,
             "dom": dom, "n_l": n_l, "fl": fl, "ms": ms, "achieved": achieved,
             "frac": achieved / kernel_peak(dom), "gemm_ms": sum(v[2] for v in agg.values()),
             "all_fl": sum(v[1] for v in agg.values()), "eager_ms": eager_ms,
@@ -719,6 +726,11 @@ def main():
                          "alg_gflop_per_launch": round(fl / n_l / 1e9, 3),
                          "all_gemm_ms_per_step": round(gemm_ms, 3), "all_gemm_tflop_per_step": round(all_fl / 1e12, 4),
                          "eager_step_ms": round(eager_ms, 3),
+                         "dp_segments": {"ms": r["seg_ms"], "grad_bytes": r["seg_bytes"],
+                                         "what": "eager step cut at the data-parallel buckets (forward + GPT-2 "
+                                                 "backward, then one per mapper layer top first, then the mapper "
+                                                 "input projection): HIP-event time and fp32 gradient bytes each "
+                                                 "segment finalises (DESIGN.md §8(e) overlap arithmetic)"},
                          "gpt2_block": dict(r["block"], peak=BF16_PEAK_TFLOPS, unit="TFLOP/s",
                                             what="the 12 GPT-2 blocks' GEMMs (fwd + dX) and attention (fwd + bwd) of "
                                                  "one eager step: summed algorithmic FLOPs (live rows) / summed "

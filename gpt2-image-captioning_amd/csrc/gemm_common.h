@@ -171,6 +171,10 @@ __device__ __forceinline__ void unpack_bf16(const uint4 w, float v[8]) {
 // the specialised forms compile a single straight run (no dispatch, none of the other activations' code, fewer live
 // registers in the epilogue); the arithmetic per element is act_fwd / act_bwd in every form (bitwise the same).
 constexpr int ACT_OFF = 0, ACT_ANY = 1, ACT_FWD = 16, ACT_BWD = 32;
+// LayerNorm statistics hand-off of the tile kernels (icap_gemm_args.ln_stats_out / ln_stats_in), or-ed into the
+// kernel's ACT template int above its activation kind: ACT_LNS = the producer writes (mean, M2) per row and 32-column
+// group of C; ACT_LNF = the consumer folds the LayerNorm of its A operand into its epilogue.
+constexpr int ACT_LNS = 256, ACT_LNF = 512;
 template <int W, int ACT = ACT_ANY>
 __device__ __forceinline__ void epi_bwd_math(const icap_gemm_args& p, float x[W], const float a[W], uint64_t seed,
                                              uint64_t didx, uint32_t drop_thresh, float inv_keep) {

@@ -49,6 +49,7 @@ class GemmArgs(C.Structure):
         ("m_hint", i64),
         ("tickets", vp), ("tickets_len", i64),
         ("ln_wsum", vp),
+        ("ln_stats_out", vp), ("ln_stats_in", vp), ("ln_mean_out", vp), ("ln_rstd_out", vp),
     ]
 
 

@@ -22,6 +22,7 @@ import torch.nn as nn
 
 from . import _lib as L
 from . import ops
+from .gpt2 import fold_layernorm
 from .weights import det_tensor
 
 Tensor = torch.Tensor
@@ -189,6 +190,9 @@ class ClipCore:
     @torch.no_grad()
     def refresh(self):
         vm, dt = self.m.vision_model, self.dtype
+        # bf16: layer_norm1 (layers >= 1) / layer_norm2 (all but the last) folded into the QKV / fc1 tile GEMMs, the row
+        # statistics handed over from the producing GEMMs' epilogues (icap_gemm_args.ln_stats_out / ln_stats_in)
+        self.fold = dt == torch.bfloat16 and self.D % 32 == 0 and os.environ.get("ICAP_TRAIN_LN_FOLD", "1") != "0"
         # [D, C*p*p] (c, ky, kx) order, zero-padded to the 8-multiple row of icap_im2col_patches (p = 14: 592)
         wp = vm.embeddings.patch_embedding.weight.data.reshape(self.D, -1)
         self.Kp = (wp.shape[1] + 7) // 8 * 8
@@ -211,6 +215,10 @@ class ClipCore:
             w.fc2_w, w.fc2_b = self._cvt(lay.mlp.fc2.weight.data), lay.mlp.fc2.bias.data
             w.ln1 = (lay.layer_norm1.weight.data, lay.layer_norm1.bias.data)
             w.ln2 = (lay.layer_norm2.weight.data, lay.layer_norm2.bias.data)
+            if self.fold:  # layer_norm1 / layer_norm2 folded into the QKV / fc1 weights (frozen tower: once)
+                qkv32 = torch.cat([a.q_proj.weight.data, a.k_proj.weight.data, a.v_proj.weight.data], 0)
+                w.qkv_wf, w.qkv_ws, w.qkv_bf = fold_layernorm(qkv32, w.ln1[0], w.ln1[1], w.qkv_b, dt)
+                w.fc1_wf, w.fc1_ws, w.fc1_bf = fold_layernorm(lay.mlp.fc1.weight.data, w.ln2[0], w.ln2[1], w.fc1_b, dt)
             self.layers.append(w)
 
     def alloc(self, B: int) -> SimpleNamespace:
@@ -230,6 +238,10 @@ class ClipCore:
         ws.feat = e(B, c.projection_dim)
         ws.emb = e(B, c.projection_dim, dtype=torch.float32)
         ws.feat32 = e(B, c.projection_dim, dtype=torch.float32)
+        ws.st_x = ws.st_h = None
+        if self.fold:  # (mean, M2) per row and 32-column group of x / h1 (the LayerNorm statistics hand-off)
+            ws.st_x = e(M, D // 32, 2, dtype=torch.float32)
+            ws.st_h = e(M, D // 32, 2, dtype=torch.float32)
         self._ws = {B: ws}  # keep only the latest batch size
         return ws
 
@@ -243,9 +255,13 @@ class ClipCore:
         ops.layernorm_fwd(ws.h1, self.pre[0], self.pre[1], eps, ws.x, None, None)
         scale = self.hd ** -0.5
         nl = len(self.layers)
+        fold = ws.st_x is not None
         for i, w in enumerate(self.layers):
-            ops.layernorm_fwd(ws.x, w.ln1[0], w.ln1[1], eps, ws.a, None, None)
-            ops.gemm(ws.a, w.qkv_w, ws.qkv, bias=w.qkv_b)
+            if fold and i > 0:  # x's statistics come from the previous layer's fc2 epilogue
+                ops.gemm(ws.x, w.qkv_wf, ws.qkv, bias=w.qkv_bf, ln_fold=(w.qkv_ws, eps), ln_stats_in=ws.st_x)
+            else:
+                ops.layernorm_fwd(ws.x, w.ln1[0], w.ln1[1], eps, ws.a, None, None)
+                ops.gemm(ws.a, w.qkv_w, ws.qkv, bias=w.qkv_b)
             ops.attention_fwd(ws.qkv, ws.o, B=B, S=self.S, H=self.H, hd=self.hd, scale=scale, causal=False)
             if i == nl - 1:
                 # last layer: only the CLS rows reach the output (pooler_output = post_layernorm(last_hidden[:, 0]),
@@ -258,6 +274,12 @@ class ClipCore:
                 ops.gemm(a, w.fc1_w, f, bias=w.fc1_b, act=L.ACT_QUICK_GELU)
                 ops.gemm(f, w.fc2_w, ws.xc, bias=w.fc2_b, resid=h1)
                 break
+            if fold:
+                ops.gemm(ws.o, w.out_w, ws.h1, bias=w.out_b, resid=ws.x, ln_stats_out=ws.st_h)
+                ops.gemm(ws.h1, w.fc1_wf, ws.f, bias=w.fc1_bf, act=L.ACT_QUICK_GELU, ln_fold=(w.fc1_ws, eps),
+                         ln_stats_in=ws.st_h)
+                ops.gemm(ws.f, w.fc2_w, ws.x, bias=w.fc2_b, resid=ws.h1, ln_stats_out=ws.st_x)
+                continue
             ops.gemm(ws.o, w.out_w, ws.h1, bias=w.out_b, resid=ws.x)
             ops.layernorm_fwd(ws.h1, w.ln2[0], w.ln2[1], eps, ws.a, None, None)
             ops.gemm(ws.a, w.fc1_w, ws.f, bias=w.fc1_b, act=L.ACT_QUICK_GELU)

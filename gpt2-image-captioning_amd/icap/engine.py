@@ -136,6 +136,13 @@ class CaptionTrainer:
         self.gdr = self.gcore.drops(dropout, seed, self.counter, self.gws.M, B, self.gws.S)
         p_map = 0.1 if isinstance(self.mcore, TransformerMapperCore) else 0.0
         self.mdr = self.mcore.drops(dropout, p_map, seed, self.counter, B)
+        # the mapper's weight-gradient products on a side stream beside its dX chain (mapper.backward_steps):
+        # opt-in (ICAP_SIDE_DW=1) — measured nondeterministic under concurrency, so off
+        self._side = None
+        if (self.dev.type == "cuda" and isinstance(self.mcore, TransformerMapperCore)
+                and os.environ.get("ICAP_SIDE_DW", "0") == "1"):
+            self._side = torch.cuda.Stream(self.dev)
+            ops.register_side_stream(self._side)
 
     def share_state_with(self, other: "CaptionTrainer") -> None:
         """Use `other`'s optimizer step counter and dropout counter (same model, another batch shape)."""
@@ -182,7 +189,9 @@ class CaptionTrainer:
 
         segs = [(self._ranges_front, front)]
         if isinstance(mc, TransformerMapperCore):
-            steps = mc.backward_steps(self.mws, self.emb_c, self.mdr, self.mgrads, self.dwh)
+            # the side stream joins at each layer step's end only when the steps are data-parallel buckets
+            steps = mc.backward_steps(self.mws, self.emb_c, self.mdr, self.mgrads, self.dwh, side=self._side,
+                                      join_each=self.world > 1 or self.force_overlap)
             for (_, _, fn), rng in zip(steps, self._ranges_mapper):
                 segs.append((rng, fn))
         else:

@@ -28,6 +28,10 @@ from .weights import det_tensor
 # decode steps (M <= 128) of a frozen GPT-2: ln_1 / ln_2 folded into the QKV / c_fc weights (GPT2Core._fold_ln);
 # ICAP_LN_FOLD=0 keeps the LayerNorm-fused GEMMs (A/B measurements)
 LN_FOLD = os.environ.get("ICAP_LN_FOLD", "1") != "0"
+# training / inference forward of a frozen bf16 GPT-2: ln_1 (layers >= 1) and ln_2 folded into the QKV / c_fc tile
+# GEMMs, their row statistics handed over from the producing GEMMs' epilogues (icap_gemm_args.ln_stats_out /
+# ln_stats_in); ICAP_TRAIN_LN_FOLD=0 keeps the standalone LayerNorm launches (A/B)
+TRAIN_LN_FOLD = os.environ.get("ICAP_TRAIN_LN_FOLD", "1") != "0"
 
 Tensor = torch.Tensor
 
@@ -56,6 +60,31 @@ class GPT2Config:  # HF/models/gpt2/configuration_gpt2.py:84-103
 
 def pad_vocab(v: int) -> int:
     return (v + 127) // 128 * 128
+
+
+def fold_layernorm(wt: Tensor, gamma: Tensor, beta: Tensor, bias: Tensor, dtype: torch.dtype):
+    """LayerNorm(x) . W^T + b = rstd (x . (W*gamma)^T - mean * wsum) + (b + W . beta) for an fp32 weight wt [out,in]
+    (nn.Linear layout): returns (W*gamma [out,in] in the compute dtype, wsum [out] = row sums of those stored values,
+    b + W . beta [out]), all fp32 arithmetic on the MFMA GEMM (W*gamma = W . diag(gamma): one nonzero product per
+    output, exact before the rounding to the compute dtype). Used once per frozen model (the decode / training-forward
+    ln_1 / ln_2 folds of GPT-2, CLIP's layer_norm1 / layer_norm2)."""
+    nout, nin = wt.shape
+    dev = wt.device
+    dg = torch.zeros((nin, nin), dtype=torch.float32, device=dev)
+    dg.view(-1)[:: nin + 1].copy_(gamma)
+    wg = torch.empty((nout, nin), dtype=torch.float32, device=dev)
+    ops.gemm(wt.contiguous(), dg, wg, split_k=1)
+    if dtype == torch.float32:
+        wf = wg
+    else:
+        wf = torch.empty((nout, nin), dtype=dtype, device=dev)
+        ops.convert(wg, wf)
+    ones = torch.ones((1, nin), dtype=dtype, device=dev)
+    wsum = torch.empty((1, nout), dtype=torch.float32, device=dev)
+    ops.gemm(ones, wf, wsum, split_k=1)
+    bf = torch.empty((1, nout), dtype=torch.float32, device=dev)
+    ops.gemm(beta.reshape(1, nin).contiguous(), wt.contiguous(), bf, bias=bias, split_k=1)
+    return wf, wsum.view(nout), bf.view(nout)
 
 
 # --------------------------------------------------------------------------- parameter containers (HF names)
@@ -297,28 +326,11 @@ class GPT2Core:
             self.qwte_t = ops.quantize_mx(self.wte_t)
 
     def _fold_ln(self, w: Tensor, gamma: Tensor, beta: Tensor, bias: Tensor):
-        """LayerNorm(x) . W + b = rstd (x . (W*gamma) - mean * wsum) + (b + beta . W) for a Conv1D master w [in,out]
-        (fp32): returns (W*gamma as [out,in] in the compute dtype, wsum [out] = row sums of those stored values,
-        b + beta . W [out]), all fp32 arithmetic on the MFMA GEMM (W*gamma = W^T . diag(gamma): one nonzero
-        product per output, exact before the rounding to the compute dtype)."""
+        """fold_layernorm of a Conv1D master w [in,out] (fp32): its [out,in] transpose folded."""
         nin, nout = w.shape
         wt = torch.empty((nout, nin), dtype=torch.float32, device=self.dev)
         ops.transpose(w, wt)
-        dg = torch.zeros((nin, nin), dtype=torch.float32, device=self.dev)
-        dg.view(-1)[:: nin + 1].copy_(gamma)
-        wg = torch.empty((nout, nin), dtype=torch.float32, device=self.dev)
-        ops.gemm(wt, dg, wg, split_k=1)
-        if self.dtype == torch.float32:
-            wf = wg
-        else:
-            wf = torch.empty((nout, nin), dtype=self.dtype, device=self.dev)
-            ops.convert(wg, wf)
-        ones = torch.ones((1, nin), dtype=self.dtype, device=self.dev)
-        wsum = torch.empty((1, nout), dtype=torch.float32, device=self.dev)
-        ops.gemm(ones, wf, wsum, split_k=1)
-        bf = torch.empty((1, nout), dtype=torch.float32, device=self.dev)
-        ops.gemm(beta.reshape(1, nin).contiguous(), wt, bf, bias=bias, split_k=1)
-        return wf, wsum.view(nout), bf.view(nout)
+        return fold_layernorm(wt, gamma, beta, bias, self.dtype)
 
     @torch.no_grad()
     def bind_flat(self, flat) -> None:
@@ -394,6 +406,12 @@ class GPT2Core:
         ws.rstd2 = [e(M, dtype=torch.float32) for _ in range(nl)]
         ws.lse = [e(B * H * S, dtype=torch.float32) for _ in range(nl)]
         ws.meanf, ws.rstdf = e(M, dtype=torch.float32), e(M, dtype=torch.float32)
+        # LayerNorm statistics hand-off of the folded forward (GPT2Core._blocks_fwd_): per row and 32-column group
+        # (mean, M2) of x (produced by the MLP c_proj, consumed by the next QKV) and of h1 (attention c_proj -> c_fc)
+        ws.st_x = ws.st_h = None
+        if self._fold_train(keep_for_dw):
+            ws.st_x = e(M, D // 32, 2, dtype=torch.float32)
+            ws.st_h = e(M, D // 32, 2, dtype=torch.float32)
         if keep_for_dw:
             ws.a1 = [e(M, D) for _ in range(nl)]
             ws.o = [e(M, D) for _ in range(nl)]
@@ -424,6 +442,12 @@ class GPT2Core:
             ws.qD, ws.q3D, ws.q4D = mx(M, D), mx(M, 3 * D), mx(M, 4 * D)
             ws.qhf, ws.qdl = mx(Mh, D), mx(Mh, self.Vp)
         return ws
+
+    def _fold_train(self, keep_for_dw: bool) -> bool:
+        """Whether the forward folds ln_1 / ln_2 into the tile GEMMs: a frozen bf16 model (the folded weights exist),
+        not the fp8 path (its MX products have no LayerNorm epilogue), D % 32 == 0."""
+        return (TRAIN_LN_FOLD and not keep_for_dw and self.dtype == torch.bfloat16 and not self.fp8
+                and self.D % 32 == 0 and bool(self.layers) and getattr(self.layers[0], "wf_attn_t", None) is not None)
 
     def _bmm(self, ws, A: Tensor, qA, W: Tensor, qW, out: Tensor, **kw) -> Tensor:
         """A block GEMM over the token rows: with packed rows only rows < m_live are computed (m_dev)."""
@@ -513,19 +537,32 @@ class GPT2Core:
         rd = getattr(ws, "m_live", None)  # packed rows: device row count (None: every row)
         seqs = getattr(ws, "seqs", None)
         afl = self._attn_flops(ws, B, S)
+        fold = getattr(ws, "st_x", None) is not None  # ln_1 (l >= 1) / ln_2 folded into the QKV / c_fc GEMMs
+        nl = len(self.layers)
         for l, lw in enumerate(self.layers):
             x = ws.x[l]
             q = lw if self.fp8 else SimpleNamespace(qw_attn_t=None, qw_proj_t=None, qw_fc_t=None, qw_mp_t=None)
-            ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, ws.a1[l], ws.mean1[l], ws.rstd1[l], rows_dev=rd)
-            self._bmm(ws, ws.a1[l], ws.qD, lw.w_attn_t, q.qw_attn_t, ws.qkv[l], bias=lw.b_attn)
+            if fold and l > 0:  # rstd (x . (W gamma)^T - mean wsum) + b + W.beta, x's statistics from the producer
+                self._bmm(ws, x, None, lw.wf_attn_t, None, ws.qkv[l], bias=lw.bf_attn, ln_fold=(lw.ws_attn, self.eps),
+                          ln_stats_in=ws.st_x, ln_rows_out=(ws.mean1[l], ws.rstd1[l]))
+            else:
+                ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, ws.a1[l], ws.mean1[l], ws.rstd1[l], rows_dev=rd)
+                self._bmm(ws, ws.a1[l], ws.qD, lw.w_attn_t, q.qw_attn_t, ws.qkv[l], bias=lw.b_attn)
             ops.attention_fwd(ws.qkv[l], ws.o[l], B=B, S=S, H=H, hd=hd, scale=scale, causal=True, key_mask=causal_mask,
                               lse=ws.lse[l], drop=dr.attn(l), seqs=seqs, alg_flops=afl)
-            self._bmm(ws, ws.o[l], ws.qD, lw.w_proj_t, q.qw_proj_t, ws.h1[l], bias=lw.b_proj, resid=x, drop=dr.ra(l))
-            ops.layernorm_fwd(ws.h1[l], lw.ln2_g, lw.ln2_b, self.eps, ws.a2[l], ws.mean2[l], ws.rstd2[l], rows_dev=rd)
-            self._bmm(ws, ws.a2[l], ws.qD, lw.w_fc_t, q.qw_fc_t, ws.f[l], bias=lw.b_fc, act=L.ACT_GELU_NEW,
-                      aux=ws.z[l])
+            self._bmm(ws, ws.o[l], ws.qD, lw.w_proj_t, q.qw_proj_t, ws.h1[l], bias=lw.b_proj, resid=x, drop=dr.ra(l),
+                      **({"ln_stats_out": ws.st_h} if fold else {}))
+            if fold:
+                self._bmm(ws, ws.h1[l], None, lw.wf_fc_t, None, ws.f[l], bias=lw.bf_fc, act=L.ACT_GELU_NEW,
+                          aux=ws.z[l], ln_fold=(lw.ws_fc, self.eps), ln_stats_in=ws.st_h,
+                          ln_rows_out=(ws.mean2[l], ws.rstd2[l]))
+            else:
+                ops.layernorm_fwd(ws.h1[l], lw.ln2_g, lw.ln2_b, self.eps, ws.a2[l], ws.mean2[l], ws.rstd2[l],
+                                  rows_dev=rd)
+                self._bmm(ws, ws.a2[l], ws.qD, lw.w_fc_t, q.qw_fc_t, ws.f[l], bias=lw.b_fc, act=L.ACT_GELU_NEW,
+                          aux=ws.z[l])
             self._bmm(ws, ws.f[l], ws.q4D, lw.w_mp_t, q.qw_mp_t, ws.x[l + 1], bias=lw.b_mp, resid=ws.h1[l],
-                      drop=dr.rm(l))
+                      drop=dr.rm(l), **({"ln_stats_out": ws.st_x} if (fold and l + 1 < nl) else {}))
 
     # -- backward (dX through the frozen GPT-2; + dW when trainable) ---------------------------------------------
     def backward(self, ws, dr, causal_mask, dlogits: Tensor, grads=None, dw=None) -> Tensor:

@@ -9,6 +9,7 @@ explicit forward/backward kernel schedule of `TransformerMapperCore` /
 from __future__ import annotations
 
 import math
+import os
 from types import SimpleNamespace
 from typing import Optional
 
@@ -33,6 +34,18 @@ def _rup(x: int, m: int) -> int:
 def _kout_ok(t: Tensor) -> bool:
     """K-outer GEMM operand requirements: 16-byte aligned base, row stride a multiple of 8 elements."""
     return t.data_ptr() % 16 == 0 and t.stride(0) % 8 == 0 and t.stride(-1) == 1
+
+
+_SIDE_SERIAL = os.environ.get("ICAP_SIDE_SERIAL", "0") == "1"  # diagnostic only (mapper.backward_steps)
+_SIDE_DIAG = os.environ.get("ICAP_SIDE_DIAG", "")  # diagnostic only: "scratch" / "no_dw" / "no_db"
+_SCRATCH = {}
+
+
+def _scratch(t: Tensor) -> Tensor:
+    k = (tuple(t.shape), t.dtype)
+    if k not in _SCRATCH:
+        _SCRATCH[k] = torch.zeros_like(t)
+    return _SCRATCH[k]
 
 
 class DWHelper:
@@ -317,7 +330,16 @@ class TransformerMapperCore:
         ws.lse = [e(B * self.H * S, dtype=torch.float32) for _ in range(n_keep)]
         if train:
             ws.dout = torch.zeros((M, D), dtype=dt, device=dev)  # rows t < Hl stay zero
-            ws.dres, ws.dnew, ws.dmask = e(M, D), e(M, D), e(M, D)
+            ws.dres = e(M, D)  # d(mapper input rows): the head step reads it
+            # per-layer gradient buffers of the backward (mapper.backward_steps): every buffer a layer's
+            # weight-gradient products read is written once per step, so those products can trail the dX chain on
+            # a side stream with no write-after-read hazard (8 layers x 11 M x D x 2 B: 433 MB at B = 128)
+            ws.g_r = [e(M, D) for _ in range(nl)]      # residual grad entering layer l (LN#2 output of layer l+1)
+            ws.g_rm = [e(M, D) for _ in range(nl)]     # residual grad after layer l's MLP (its LN#1 output)
+            ws.g_m = [e(M, D) for _ in range(nl)]      # g_r[l] through the layer's output dropout (dy of linear2)
+            ws.g_mm = [e(M, D) for _ in range(nl)]     # g_rm[l] through the attention-output dropout (dy of out_proj)
+            ws.g_dz = [e(M, 4 * D) for _ in range(nl)]    # d(relu pre-activation) (dy of linear1)
+            ws.g_dqkv = [e(M, 3 * D) for _ in range(nl)]  # d(in_proj output) (dy of in_proj)
             ws.dz = e(M, 4 * D)
             ws.dqkv = e(M, 3 * D)
             ws.do, ws.da = e(M, D), e(M, D)
@@ -364,64 +386,92 @@ class TransformerMapperCore:
         return ws.out.view(-1)[self.Hl * self.D:], self.S * self.D
 
     # -- backward --------------------------------------------------------------------------------------------
-    def backward(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper) -> None:
+    def backward(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper, side=None) -> None:
         """Consumes ws.dout (d of the forward output, rows t<Hl zero); accumulates every parameter grad."""
-        for _, _, fn in self.backward_steps(ws, emb_c, dr, g, dwh):
+        for _, _, fn in self.backward_steps(ws, emb_c, dr, g, dwh, side=side, join_each=False):
             fn()
 
-    def backward_steps(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper):
+    def backward_steps(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper, side=None, join_each: bool = True):
         """The backward as [(name, module, fn)]: one step per layer (the top layer first), then the input
         projection ("head": linear + prefix_const). Run in order they are backward(); each step finalises the
         grads of its module's parameters, which is what engine.CaptionTrainer's data-parallel all-reduce buckets
-        key on."""
+        key on.
+        side: a CUDA stream (ops.register_side_stream) for the weight-gradient work — the four K-outer dW products
+        and bias column sums per layer, which feed only the optimizer — so it runs beside the dX chain (the dX
+        GEMMs, attention and LayerNorm backward). Every gradient buffer those products read is a per-layer buffer
+        written once per step (ws.g_*), so a product only has to be ordered after its producer (the fork); the
+        main stream joins the side stream at the end of each layer step (join_each: the data-parallel buckets are
+        final when their step ends) or only before the head step. Each gradient is the same kernel on the same
+        operands as the serial schedule: bitwise the same result."""
         B, M, S, D, Hl, P = ws.B, ws.M, self.S, self.D, self.Hl, self.P
         scale = 1.0 / math.sqrt(self.hd)
         st = SimpleNamespace()
-        bufs = [ws.dres, ws.dnew]
+
+        def order(waiter, signaller):
+            """waiter runs its later work after everything queued on signaller so far. The event object is kept
+            alive (ops.keep_event) until the work behind it has run."""
+            ev = torch.cuda.Event()
+            ev.record(signaller)
+            waiter.wait_event(ev)
+            ops.keep_event(ev)
+
+        def wgrad(dy, x, w_out, b_out):
+            """dW += dy^T x and db += colsum(dy): on the side stream, behind everything queued on the main stream."""
+            if side is None:
+                dwh.dW(dy, x, w_out, M=M)
+                dwh.db(dy, b_out, M=M)
+                return
+            main = torch.cuda.current_stream()
+            order(side, main)
+            with torch.cuda.stream(side):
+                if _SIDE_DIAG == "scratch":  # diagnostic: the same launches into scratch outputs
+                    w_out = _scratch(w_out)
+                    b_out = _scratch(b_out)
+                if _SIDE_DIAG != "no_dw":
+                    dwh.dW(dy, x, w_out, M=M)
+                if _SIDE_DIAG != "no_db":
+                    dwh.db(dy, b_out, M=M)
+            if _SIDE_SERIAL:  # diagnostic: the side stream, but joined after every fork (no concurrency)
+                order(main, side)
 
         def layer(l):
-            if l == self.nl - 1:  # start of the backward
-                st.dres = ws.dout
-                top = dr.d2(self.nl - 1)
-                if top.p > 0:
-                    ops.dropout_apply(st.dres, ws.dmask, top)
-                st.dmask_valid = top.p > 0
-                st.bi = 0
+            if l == self.nl - 1:  # start of the backward: d(output) enters the top layer
+                st.r = ws.dout
             w, gl = self.layers[l], g.layers[l]
-            dres = st.dres
-            dy = ws.dmask if st.dmask_valid else dres
-            dwh.dW(dy, ws.f[l], gl.l2_w, M=M)
-            dwh.db(dy, gl.l2_b, M=M)
-            ops.gemm(dy, w.l2_wt, ws.dz, dact=L.ACT_RELU, dact_src=ws.f[l], drop=dr.dff(l))
-            dwh.dW(ws.dz, ws.a2[l], gl.l1_w, M=M)
-            dwh.db(ws.dz, gl.l1_b, M=M)
-            ops.gemm(ws.dz, w.l1_wt, ws.da)
-            dnew = bufs[st.bi]; st.bi ^= 1
+            r = st.r
+            top = dr.d2(l)  # the layer's output dropout (x = h1 + drop(linear2(...)))
+            dy = r
+            if top.p > 0:
+                if l == self.nl - 1:
+                    ops.dropout_apply(r, ws.g_m[l], top)
+                dy = ws.g_m[l]  # (below the top layer: written by the LN backward above, as its dx_drop)
+            wgrad(dy, ws.f[l], gl.l2_w, gl.l2_b)
+            ops.gemm(dy, w.l2_wt, ws.g_dz[l], dact=L.ACT_RELU, dact_src=ws.f[l], drop=dr.dff(l))
+            wgrad(ws.g_dz[l], ws.a2[l], gl.l1_w, gl.l1_b)
+            ops.gemm(ws.g_dz[l], w.l1_wt, ws.da)
             d1 = dr.d1(l)
-            ops.layernorm_bwd(ws.h1[l], w.n2_g, ws.mean2[l], ws.rstd2[l], ws.da, dnew, dres=dres,
-                              dx_drop=ws.dmask if d1.p > 0 else None, drop=d1, dgamma=gl.n2_g, dbeta=gl.n2_b,
+            ops.layernorm_bwd(ws.h1[l], w.n2_g, ws.mean2[l], ws.rstd2[l], ws.da, ws.g_rm[l], dres=r,
+                              dx_drop=ws.g_mm[l] if d1.p > 0 else None, drop=d1, dgamma=gl.n2_g, dbeta=gl.n2_b,
                               workspace=dwh.ln_ws)
-            dres = dnew
-            dy = ws.dmask if d1.p > 0 else dres
-            dwh.dW(dy, ws.o[l], gl.out_w, M=M)
-            dwh.db(dy, gl.out_b, M=M)
-            ops.gemm(dy, w.out_wt, ws.do)
-            ops.attention_bwd(ws.qkv[l], ws.do, ws.lse[l], ws.dqkv, B=B, S=S, H=self.H, hd=self.hd, scale=scale,
-                              causal=False, drop=dr.attn(l), out=ws.o[l])
-            dwh.dW(ws.dqkv, ws.a1[l], gl.in_w, M=M)
-            dwh.db(ws.dqkv, gl.in_b, M=M)
-            ops.gemm(ws.dqkv, w.in_wt, ws.da)
-            dnew = bufs[st.bi]; st.bi ^= 1
+            dy2 = ws.g_mm[l] if d1.p > 0 else ws.g_rm[l]
+            wgrad(dy2, ws.o[l], gl.out_w, gl.out_b)
+            ops.gemm(dy2, w.out_wt, ws.do)
+            ops.attention_bwd(ws.qkv[l], ws.do, ws.lse[l], ws.g_dqkv[l], B=B, S=S, H=self.H, hd=self.hd,
+                              scale=scale, causal=False, drop=dr.attn(l), out=ws.o[l])
+            wgrad(ws.g_dqkv[l], ws.a1[l], gl.in_w, gl.in_b)
+            ops.gemm(ws.g_dqkv[l], w.in_wt, ws.da)
             nxt = dr.d2(l - 1) if l > 0 else Dropout()
-            ops.layernorm_bwd(ws.x[l], w.n1_g, ws.mean1[l], ws.rstd1[l], ws.da, dnew, dres=dres,
-                              dx_drop=ws.dmask if nxt.p > 0 else None, drop=nxt, dgamma=gl.n1_g, dbeta=gl.n1_b,
-                              workspace=dwh.ln_ws)
-            st.dres = dnew
-            st.dmask_valid = nxt.p > 0
+            out = ws.g_r[l - 1] if l > 0 else ws.dres  # d(layer input): the next layer's residual grad / the head's
+            ops.layernorm_bwd(ws.x[l], w.n1_g, ws.mean1[l], ws.rstd1[l], ws.da, out, dres=ws.g_rm[l],
+                              dx_drop=ws.g_m[l - 1] if (l > 0 and nxt.p > 0) else None, drop=nxt, dgamma=gl.n1_g,
+                              dbeta=gl.n1_b, workspace=dwh.ln_ws)
+            st.r = out
+            if side is not None and (join_each or l == 0):  # the layer's grads are final when its step ends
+                order(torch.cuda.current_stream(), side)
 
         def head():
             # x0 = [linear(emb) ; prefix_const]
-            dres = st.dres
+            dres = st.r
             d_lin = dres.view(B, S * D)[:, : Hl * D]
             dwh.dW(d_lin, emb_c, g.lin_w, M=B)
             dwh.db(d_lin, g.lin_b, M=B)

@@ -152,7 +152,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None,
          trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None,
          tile_only: bool = False, g256: bool = False, m_hint: Optional[int] = None,
-         ln_fold: Optional[tuple] = None) -> Tensor:
+         ln_fold: Optional[tuple] = None, ln_stats_out: Optional[Tensor] = None,
+         ln_stats_in: Optional[Tensor] = None, ln_rows_out: Optional[tuple] = None) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
     workspace: fp32 split-K scratch; by default one buffer per (device, stream), so GEMMs issued on different
     streams never share slabs (gemm_workspace). The split count depends on the shape alone, so the result is
@@ -166,7 +167,11 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     m_dev: device int32 row count <= M (rows past it are neither computed nor stored); m_hint: its expected value
     (kernel choice only).
     tile_only: the 128-row tile kernels only; g256: the 256 x 256 kernel wherever eligible (A/B measurements,
-    path-equality tests)."""
+    path-equality tests).
+    ln_stats_out: fp32 [M, N/32, 2] — this (producer) launch also writes (mean, M2) of each row's 32-column groups of
+    the stored C; ln_stats_in (with ln_fold = (wsum, eps)): the LayerNorm of A folded into the epilogue from the
+    producer's statistics (tile kernels, any M); ln_rows_out: (mean, rstd) fp32 [M] of that LayerNorm (for its
+    backward). include/icap.h icap_gemm_args.ln_stats_out."""
     mx = isinstance(A, MXTensor)
     if mx != isinstance(B, MXTensor):
         raise L.IcapError("gemm: A and B must both be MXTensor (fp8 MX) or both plain tensors")
@@ -220,6 +225,12 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
         a.ln_gamma, a.ln_beta, a.ln_eps = ln[0].data_ptr(), ln[1].data_ptr(), float(ln[2])
     if ln_fold is not None:
         a.ln_wsum, a.ln_eps = ln_fold[0].data_ptr(), float(ln_fold[1])
+    if ln_stats_out is not None:
+        a.ln_stats_out = ln_stats_out.data_ptr()
+    if ln_stats_in is not None:
+        a.ln_stats_in = ln_stats_in.data_ptr()
+    if ln_rows_out is not None:
+        a.ln_mean_out, a.ln_rstd_out = ln_rows_out[0].data_ptr(), ln_rows_out[1].data_ptr()
     if GEMM_TIMER is None:
         call("icap_gemm", C.byref(a), _stream())
     else:  # per-launch HIP-event timing (bench.py kernel roofline pass; never inside a captured graph)
@@ -227,7 +238,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
         key = (name.decode() if name else "?",
                f"{M}x{N}x{K} act{act} dact{dact} drop{int(drop.p > 0)} res{int(resid is not None)} "
                f"aux{int(aux is not None)} beta{beta:g}{' m_dev' if m_dev is not None else ''}"
-               f"{' kout' if trans_ab else ''}{' ln' if ln is not None else ''}{' lnfold' if ln_fold is not None else ''}")
+               f"{' kout' if trans_ab else ''}{' ln' if ln is not None else ''}{' lnfold' if ln_fold is not None else ''}"
+               f"{' lnS' if ln_stats_out is not None else ''}{' lnF' if ln_stats_in is not None else ''}")
         GEMM_TIMER.launch(key, 2.0 * M * N * K if alg_flops is None else alg_flops,
                           lambda: call("icap_gemm", C.byref(a), _stream()))
     return out
@@ -254,14 +266,18 @@ def gemm_workspace(device, stream=None) -> Tensor:
     here and aborts the allocator when that graph is destroyed), so every capture uses one per-device graph
     buffer, allocated with the device's first eager buffer: graphs replayed one after another (the trainer's step
     / segment graphs, decode chunks) share it as eager launches on one stream share theirs; two graphs that
-    contain split-K GEMMs must not be replayed concurrently on different streams."""
+    contain split-K GEMMs must not be replayed concurrently on different streams. A side stream registered with
+    register_side_stream (a concurrent branch inside one captured graph: the trainer's weight-gradient stream)
+    has a graph buffer of its own."""
+    sid = 0 if stream is None else int(stream.cuda_stream)
     if stream is not None and torch.cuda.is_current_stream_capturing():
-        ws = _gemm_ws.get((device.type, device.index, "graph"))
+        ws = _gemm_ws.get((device.type, device.index, "graph", sid))
+        if ws is None:
+            ws = _gemm_ws.get((device.type, device.index, "graph"))
         if ws is None:
             raise L.IcapError("gemm: a split-K workspace is needed inside graph capture; run one eager GEMM on "
                               "this device first (or pass workspace=)")
         return ws
-    sid = 0 if stream is None else int(stream.cuda_stream)
     key = (device.type, device.index, sid)
     ws = _gemm_ws.get(key)
     if ws is None:
@@ -271,6 +287,29 @@ def gemm_workspace(device, stream=None) -> Tensor:
         if stream is not None and gkey not in _gemm_ws:
             _gemm_ws[gkey] = _new_workspace(device)
     return ws
+
+
+_KEPT_EVENTS = []
+KEEP_EVENTS = 4096  # events kept alive (a few steps' worth of the trainer's cross-stream waits)
+
+
+def keep_event(ev) -> None:
+    """Hold a reference to a cross-stream event until KEEP_EVENTS newer ones exist: destroying a HIP event while a
+    stream's wait on it is still queued can let that wait go early, so the trainer's fork / join events outlive
+    the work they order (a step records ~70; this keeps dozens of steps)."""
+    _KEPT_EVENTS.append(ev)
+    if len(_KEPT_EVENTS) > KEEP_EVENTS:
+        del _KEPT_EVENTS[: KEEP_EVENTS // 2]
+
+
+def register_side_stream(stream) -> None:
+    """Give `stream` its own eager and graph-capture split-K workspaces (allocated now, outside any capture), so
+    GEMMs it runs concurrently with the capture stream's inside one graph never share slabs or tickets."""
+    dev = stream.device
+    gemm_workspace(dev, stream)
+    gkey = (dev.type, dev.index, "graph", int(stream.cuda_stream))
+    if gkey not in _gemm_ws:
+        _gemm_ws[gkey] = _new_workspace(dev)
 
 
 GEMM_TIMER = None  # set to an object with .launch(key, flops, fn) to time every GEMM (and attention) launch

@@ -136,6 +136,16 @@ typedef struct {
   /* (eps = ln_eps) taken inside the launch from the A fragments it already reads; the product runs on raw A  */
   /* (the decode step's ln_1 / ln_2, frozen GPT-2: HF/models/gpt2/modeling_gpt2.py:281,301).                 */
   const float* ln_wsum;
+  /* LayerNorm statistics handed from one tile-kernel GEMM to the next (the frozen forward's ln_1 / ln_2 folded     */
+  /* into the QKV / c_fc products: HF/models/gpt2/modeling_gpt2.py:281,301; CLIP layer_norm1/2                     */
+  /* modeling_clip.py:365-384). ln_stats_out (producer, bf16 C, N % 32 == 0): per row and 32-column group of the   */
+  /* stored C values, (mean, M2 = sum of squared deviations) as fp32 pairs [M][N/32][2]. ln_stats_in (consumer,    */
+  /* with ln_wsum, bias = b + W.beta, B = W*gamma, ln_eps; K % 32 == 0): the producer's statistics of A            */
+  /* [M][K/32][2], combined per row (two-pass: mean of the group means, then M2 + 32 (mean_g - mean)^2) into mean  */
+  /* and rstd = 1/sqrt(M2/K + eps), and C = rstd (A.B^T - mean ln_wsum) + bias, then the epilogue. ln_mean_out /   */
+  /* ln_rstd_out (optional, consumer): those row statistics (fp32 [M]) for the LayerNorm backward. bf16 inputs,   */
+  /* tile kernels only (M > 128 or not), no trans_ab; a split product must be able to combine inside the launch.  */
+  float* ln_stats_out; const float* ln_stats_in; float* ln_mean_out; float* ln_rstd_out;
 } icap_gemm_args;
 /* MX block quantisation (the A / B operands of an ICAP_FP8_MX GEMM): x [R, K] (f32 or bf16, row stride ldx) */
 /* -> q [R, K] OCP e4m3fn bytes (row stride ldq % 16 == 0) + the E8M0 scales in icap_gemm_args.a_scale      */

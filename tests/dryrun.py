@@ -43,7 +43,9 @@ def accesses(name, args):
                 ("resid", g.resid, _rows(g.M, g.ldr, g.N, ec)), ("seed_ptr", g.seed_ptr, 8),
                 ("workspace", g.workspace, g.workspace_bytes), ("m_dev", g.m_dev, 4),
                 ("ln_gamma", g.ln_gamma, g.K * 4), ("ln_beta", g.ln_beta, g.K * 4),
-                ("tickets", g.tickets, g.tickets_len * 4), ("ln_wsum", g.ln_wsum, g.N * 4)]
+                ("tickets", g.tickets, g.tickets_len * 4), ("ln_wsum", g.ln_wsum, g.N * 4),
+                ("ln_stats_out", g.ln_stats_out, g.M * (g.N // 32) * 8), ("ln_stats_in", g.ln_stats_in, g.M * (g.K // 32) * 8),
+                ("ln_mean_out", g.ln_mean_out, g.M * 4), ("ln_rstd_out", g.ln_rstd_out, g.M * 4)]
         if g.in_dtype == 2:  # MX block scales (include/icap.h a_scale / b_scale layout)
             out += [("a_scale", g.a_scale, ops.mx_scale_bytes(g.M, g.K)), ("b_scale", g.b_scale, ops.mx_scale_bytes(g.N, g.K))]
     elif name in ("icap_attention_fwd", "icap_attention_bwd"):

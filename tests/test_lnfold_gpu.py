@@ -76,3 +76,143 @@ def test_greedy_fold_vs_fused(dev, monkeypatch):
         del model
     agree = float((outs[0] == outs[1]).float().mean())
     assert agree >= 0.9, agree
+
+
+# ------------------------------------------------------------------------------------- the training-forward fold
+# (round 4: icap_gemm_args.ln_stats_out / ln_stats_in — the producer GEMM's epilogue writes (mean, M2) per row and
+# 32-column group of its stored output; the consumer tile GEMM folds the LayerNorm of its A operand from them)
+
+
+def _group_stats(c):
+    """(mean, M2) per row and 32-column group of a [M, N] tensor, fp64 -> fp32 [M, N/32, 2]"""
+    M, N = c.shape
+    g = c.double().reshape(M, N // 32, 32)
+    mean = g.mean(-1)
+    m2 = ((g - mean[..., None]) ** 2).sum(-1)
+    return torch.stack([mean, m2], -1).float()
+
+
+@pytest.mark.parametrize("M,live,N,K,form", [(8320, 3584, 768, 3072, "resid_drop"), (8320, 3584, 768, 768, "resid_drop"),
+                                             (6400, None, 768, 768, "resid"), (6400, None, 768, 3072, "resid"),
+                                             (300, None, 1024, 1024, "resid")])
+def test_ln_stats_producer(dev, M, live, N, K, form):
+    """The producer's statistics equal those of the C it stored (the rounded bf16 values), rows < the device count."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = (torch.randn((M, K), generator=g) * 0.5).to(dev, torch.bfloat16)
+    B = (torch.randn((N, K), generator=g) * 0.05).to(dev, torch.bfloat16)
+    C = torch.zeros((M, N), device=dev, dtype=torch.bfloat16)
+    st = torch.full((M, N // 32, 2), float("nan"), device=dev)
+    kw = dict(bias=torch.randn(N, generator=g).to(dev), resid=(torch.randn((M, N), generator=g) * 3 + 1).to(dev, torch.bfloat16))
+    if form == "resid_drop":
+        kw["drop"] = ops.Dropout(0.1, 5)
+    if live is not None:
+        kw.update(m_dev=torch.tensor([live], dtype=torch.int32, device=dev), m_hint=live)
+    ops.gemm(A, B, C, ln_stats_out=st, **kw)
+    C2 = torch.zeros_like(C)
+    ops.gemm(A, B, C2, **kw)  # the same product without the statistics: identical C
+    torch.cuda.synchronize()
+    rows = live or M
+    assert torch.equal(C[:rows], C2[:rows])
+    ref = _group_stats(C[:rows])
+    got = st[:rows]
+    assert torch.isfinite(got).all()
+    assert float((got[..., 0] - ref[..., 0]).abs().max()) < 1e-5 * float(ref[..., 0].abs().max() + 1)
+    assert float((got[..., 1] - ref[..., 1]).abs().max()) < 1e-4 * float(ref[..., 1].abs().max())
+    if live is not None:
+        assert torch.isnan(st[rows:]).all()  # rows past the device count: not written
+
+
+@pytest.mark.parametrize("M,N,K,act", [(8320, 2304, 768, L.ACT_NONE), (8320, 3072, 768, L.ACT_GELU_NEW),
+                                       (6400, 2304, 768, L.ACT_NONE), (6400, 3072, 768, L.ACT_QUICK_GELU),
+                                       (300, 4096, 1024, L.ACT_GELU_NEW)])
+def test_ln_fold_consumer(dev, M, N, K, act):
+    """The consumer's rstd (x.(W gamma)^T - mean wsum) + b + W.beta from handed-over statistics against fp32 torch
+    LN(x).W^T + b (bf16 bound) and against the standalone LayerNorm + GEMM path; its row mean / rstd outputs against
+    torch's."""
+    from icap.gpt2 import fold_layernorm
+
+    g = torch.Generator().manual_seed(M + N + K + act)
+    x32 = torch.randn((M, K), generator=g) * 2 + 0.5
+    x32[:, 7] += 30.0  # a large-magnitude feature (GPT-2's residual stream has them)
+    x = x32.to(dev, torch.bfloat16)
+    w = (torch.randn((N, K), generator=g) * 0.05).to(dev)
+    gamma = (1 + 0.2 * torch.randn(K, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(K, generator=g)).to(dev)
+    bias = (0.1 * torch.randn(N, generator=g)).to(dev)
+    eps = 1e-5
+    wf, wsum, bf = fold_layernorm(w, gamma, beta, bias, torch.bfloat16)
+    st = _group_stats(x).to(dev)
+    out = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+    mean_o = torch.empty(M, device=dev)
+    rstd_o = torch.empty(M, device=dev)
+    ops.gemm(x, wf, out, bias=bf, act=act, ln_fold=(wsum, eps), ln_stats_in=st, ln_rows_out=(mean_o, rstd_o))
+    a = torch.empty_like(x)
+    ops.layernorm_fwd(x, gamma, beta, eps, a, None, None)
+    out_ln = torch.empty_like(out)
+    ops.gemm(a, w.to(torch.bfloat16), out_ln, bias=bias, act=act)
+    torch.cuda.synchronize()
+    xd = x.double()
+    mu = xd.mean(-1)
+    rs = 1.0 / torch.sqrt(xd.var(-1, unbiased=False) + eps)
+    assert float((mean_o.double() - mu).abs().max()) < 1e-5 * float(mu.abs().max())
+    assert float(((rstd_o.double() - rs) / rs).abs().max()) < 1e-5
+    ref = torch.nn.functional.layer_norm(x.float(), (K,), gamma, beta, eps) @ w.t() + bias
+    if act == L.ACT_GELU_NEW:
+        ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    elif act == L.ACT_QUICK_GELU:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    scale = float(ref.abs().max())
+    ef = float((out.float() - ref).abs().max()) / scale
+    el = float((out_ln.float() - ref).abs().max()) / scale
+    assert ef < 2e-2, (ef, el)
+    assert ef < 2.5 * el + 2e-3, (ef, el)  # no worse than LayerNorm kernel + GEMM
+
+
+def test_gpt2_train_forward_fold_vs_layernorm(dev, monkeypatch):
+    """The packed bf16 train step (GPT-2 small frozen, B = 32, dropout off) with ln_1 / ln_2 folded vs the standalone
+    LayerNorm launches: losses within bf16 rounding (|d| <= 1e-2), the LN backward's saved row statistics within
+    1e-4, the mapper gradient's direction (cosine >= 0.99)."""
+    from icap import CaptionTrainer
+    from icap import gpt2 as G
+    from oracle import icap_oracle as O
+    from test_model_gpu import build
+
+    ids, mask, labels, _ = O.synthetic_batch(32, 50, 13, seed=3)
+    emb = torch.randn((32, 512), generator=torch.Generator().manual_seed(4))
+    batch = (ids.to(dev), mask.to(dev), labels.to(dev), (emb / emb.norm(dim=-1, keepdim=True)).to(dev))
+    res = {}
+    for fold in (True, False):
+        monkeypatch.setattr(G, "TRAIN_LN_FOLD", fold)
+        model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
+        t = CaptionTrainer(model, 32, 50, lr=1e-4, num_training_steps=10, dropout=False)
+        assert (t.gws.st_x is not None) == fold
+        t.load_batch(*batch)
+        t._fwd_bwd(True, 1.0)
+        torch.cuda.synchronize()
+        n = int(t.gws.m_live.item())
+        res[fold] = (float(t.gws.loss.item()), t.gws.mean1[5][:n].clone(), t.gws.rstd2[7][:n].clone(),
+                     t.flat.flat_grad.clone())
+        del t, model
+    (l1, m1, r1, g1), (l0, m0, r0, g0) = res[True], res[False]
+    assert abs(l1 - l0) < 1e-2, (l1, l0)
+    assert float((m1 - m0).abs().max()) < 1e-4 * float(m0.abs().max() + 1)
+    assert float(((r1 - r0) / r0).abs().max()) < 1e-3
+    cos = float((g1.double() @ g0.double()) / (g1.double().norm() * g0.double().norm()))
+    assert cos > 0.99, cos
+
+
+def test_clip_fold_vs_layernorm(dev, monkeypatch):
+    """CLIP ViT-B/32 bf16 embeddings with layer_norm1 / 2 folded vs standalone: cosine >= 0.999 per image."""
+    from icap.clip import CLIPVisionTower
+
+    px = torch.randn((64, 3, 224, 224), generator=torch.Generator().manual_seed(9)).to(dev)
+    embs = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("ICAP_TRAIN_LN_FOLD", fold)
+        tower = CLIPVisionTower.random_init(None, seed=0).to(dev)
+        core = tower.core(torch.bfloat16)
+        assert core.fold == (fold == "1")
+        embs[fold] = core.features(px).double()
+        del tower, core
+    cos = torch.nn.functional.cosine_similarity(embs["1"], embs["0"])
+    assert float(cos.min()) > 0.999, float(cos.min())

@@ -189,12 +189,10 @@ def test_packed_step_with_dropout_runs(dev):
 @pytest.mark.parametrize("N,K,epi", [(768, 3072, "resid_drop"), (768, 2304, "plain"), (768, 1160, "f32"),
                                      (640, 3072, "plain")])
 def test_ring_gemm_equals_tile_kernel(dev, N, K, epi, monkeypatch):
-    """The 4-stage ring (icap_gemm variant for long K over ~one tile per CU, chosen through m_hint when no split-K
-    tickets are given) runs the same MFMA chain as the double-buffered tile kernel: bitwise-equal outputs on the live
+    """The 4-stage ring (icap_gemm variant for long K over ~one tile per CU, chosen through m_hint when split-K is
+    off: split_k = 1) runs the same MFMA chain as the double-buffered tile kernel: bitwise-equal outputs on the live
     rows; close to fp32 torch."""
     from icap import _lib as L
-
-    monkeypatch.setattr(ops, "FUSED_SPLIT_K", False)  # no tickets: the ring instead of the in-launch split-K
 
     mcap, mlive = 8320, 3584
     g = torch.Generator().manual_seed(K + N)
@@ -209,13 +207,13 @@ def test_ring_gemm_equals_tile_kernel(dev, N, K, epi, monkeypatch):
     outs, names = [], []
     for hint in (mlive, None):
         C = torch.zeros((mcap, N), device=dev, dtype=cdt)
-        a = ops.gemm(A, B, C, m_dev=mdev, m_hint=hint, **kw)
+        a = ops.gemm(A, B, C, m_dev=mdev, m_hint=hint, split_k=1, **kw)
         outs.append(a)
         ga = L.GemmArgs()
         ga.M, ga.N, ga.K, ga.in_dtype, ga.c_dtype = mcap, N, K, L.BF16, ops.dtype_code(cdt)
         ga.A, ga.lda, ga.B, ga.ldb, ga.C, ga.ldc = A.data_ptr(), K, B.data_ptr(), K, C.data_ptr(), N
         ga.m_dev, ga.m_hint = mdev.data_ptr(), hint or 0
-        ga.alpha = 1.0
+        ga.alpha, ga.split_k = 1.0, 1
         names.append(L.load().icap_gemm_kernel_name(ga).decode())
     torch.cuda.synchronize()
     assert "4, 1, 2, 2, 4, 4" in names[0] and "4, 1, 2, 2" not in names[1], names
