@@ -663,6 +663,16 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
     pl.variant = tiles < 256 ? 12 : 13;
   }
   if (p.trans_ab) pl.variant = nk_split > 16 ? 14 : 15;  // K-outer forms of variants 0 / 4
+  // ICAP_FORCE_TILE = 0 / 4 / 5 / 12 / 13 / 16: that tile variant for unsplit bf16 row-major launches (A/B only; read
+  // per call so one process can interleave the forms)
+  if (const char* fv = getenv("ICAP_FORCE_TILE")) {
+    const int v = atoi(fv);
+    if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 && (v == 0 || v == 4 || v == 5 || v == 12 || v == 13 || v == 16)) {
+      pl.variant = v;
+      tiles_n = (v == 12 || v == 13) ? (p.N + 63) / 64 : (p.N + GBN - 1) / GBN;
+      tiles = tiles_m * tiles_n;
+    }
+  }
   pl.tiles_n = (int)tiles_n;
   const bool any_act = (splits == 1 || pl.fused) && (p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE);
   pl.actk = any_act ? ACT_ANY : ACT_OFF;

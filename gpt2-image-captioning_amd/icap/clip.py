@@ -383,6 +383,12 @@ class DeviceCLIPProcessor(CLIPProcessor):
         arrs = [np.asarray(im.convert("RGB")) if hasattr(im, "convert") else np.asarray(im) for im in images]
         return SimpleNamespace(pixel_values=ops.clip_preprocess(arrs, self.device, self.size, self.size))
 
+    def preprocess_packed(self, packed: Tensor, sizes) -> Tensor:
+        """pixel_values of a batch the loader already packed (icap.images: one host buffer per batch, pinned)."""
+        from . import ops
+
+        return ops.clip_preprocess_packed(packed, sizes, self.device, self.size, self.size)
+
 
 @torch.no_grad()
 def extract_clip_embedding_from_image(image, clip_model: CLIPVisionTower, clip_processor: CLIPProcessor,

@@ -43,6 +43,16 @@ class ImageDirectoryDataset(Dataset):
         names, images = zip(*batch)
         return list(names), list(images)
 
+    @staticmethod
+    def packed_collate(batch) -> Tuple[List[str], torch.Tensor, torch.Tensor]:
+        """(names, uint8 [sum H*W*3] with the images back to back, int64 [n, 2] (H, W)): the packing runs in the
+        worker, so the main process receives one shared-memory buffer per batch (not one per image), which the
+        DataLoader's pin-memory thread pins for an asynchronous host-to-device copy."""
+        names, images = zip(*batch)
+        sizes = torch.tensor([im.shape[:2] for im in images], dtype=torch.int64).reshape(-1, 2)
+        packed = torch.cat([im.reshape(-1) for im in images]) if images else torch.empty(0, dtype=torch.uint8)
+        return list(names), packed, sizes
+
 
 @torch.no_grad()
 def extract_directory(image_dir: str, output_path: str, embed: Callable, processor, out_dim: int,
@@ -52,17 +62,28 @@ def extract_directory(image_dir: str, output_path: str, embed: Callable, process
     feature: an extra "feature" string naming what the embeddings are (readers that index "filenames" /
     "embeddings", src/dataset.py:127-137, ignore it). Returns the number of images."""
     ds = ImageDirectoryDataset(image_dir)
-    dl = DataLoader(ds, batch_size=batch_size, shuffle=False, num_workers=num_workers,
-                    collate_fn=ImageDirectoryDataset.collate_fn, persistent_workers=False)
+    packed = hasattr(processor, "preprocess_packed")  # the device processor: one packed, pinned buffer per batch
+    dev = torch.device(device) if device is not None else None
+    pin = packed and dev is not None and dev.type == "cuda"
+    dl = DataLoader(ds, batch_size=batch_size, shuffle=False, num_workers=num_workers, pin_memory=pin,
+                    collate_fn=ImageDirectoryDataset.packed_collate if packed else ImageDirectoryDataset.collate_fn,
+                    persistent_workers=False)
     names: List[str] = []
     embs: List[torch.Tensor] = []
-    for batch_names, batch_images in dl:
-        px = processor(images=batch_images).pixel_values
-        if device is not None:
-            px = px.to(device, non_blocking=True)
-        embs.append(embed(px).cpu())
+    for batch in dl:
+        if packed:
+            batch_names, buf, sizes = batch
+            px = processor.preprocess_packed(buf, sizes.tolist())
+        else:
+            batch_names, batch_images = batch
+            px = processor(images=batch_images).pixel_values
+            if device is not None:
+                px = px.to(device, non_blocking=True)
+        # the embeddings stay on the device until the end (one copy back, src/embeddings/clip.py:140 copies per
+        # batch): no per-batch synchronisation, so the next batch's host work overlaps this batch's kernels
+        embs.append(embed(px))
         names.extend(batch_names)
-    final = torch.cat(embs, 0) if embs else torch.empty((0, out_dim))
+    final = torch.cat([e.float() for e in embs], 0).cpu() if embs else torch.empty((0, out_dim))
     out = {"filenames": names, "embeddings": final}
     if feature is not None:
         out["feature"] = feature

@@ -750,19 +750,33 @@ def clip_preprocess(images, device, size: int = 224, crop: int = 224, mean=None,
     equal to CLIPImageProcessor(images).pixel_values (src/embeddings/clip.py:129; PIL-backed HF processor)."""
     import numpy as np
 
-    from .clip import CLIP_MEAN, CLIP_STD
-
     arrs = [np.ascontiguousarray(np.asarray(im, dtype=np.uint8)) for im in images]
     for a in arrs:
         if a.ndim != 3 or a.shape[2] != 3:
             raise L.IcapError("clip_preprocess: images must be RGB uint8 [H, W, 3]")
-    n = len(arrs)
+    if not arrs:
+        return torch.empty((0, 3, crop, crop), dtype=torch.float32, device=device)
+    packed = torch.from_numpy(np.concatenate([a.reshape(-1) for a in arrs]))
+    return clip_preprocess_packed(packed, [a.shape[:2] for a in arrs], device, size, crop, mean, std)
+
+
+def clip_preprocess_packed(packed: Tensor, sizes, device, size: int = 224, crop: int = 224, mean=None,
+                           std=None) -> Tensor:
+    """clip_preprocess of images already packed back to back: `packed` uint8 [sum H*W*3] (host — pinned for an
+    asynchronous copy — or device), `sizes` [(H, W)] in order. The extraction loop's workers pack each batch
+    (icap.images.ImageDirectoryDataset.packed_collate), so the main process makes one copy per batch."""
+    from .clip import CLIP_MEAN, CLIP_STD
+
+    sizes = [(int(h), int(w)) for h, w in sizes]
+    n = len(sizes)
     out = torch.empty((n, 3, crop, crop), dtype=torch.float32, device=device)
     if n == 0:
         return out
-    geo, tmp_bytes = clip_preprocess_geometry([a.shape[:2] for a in arrs], size, crop)
+    if packed.dtype != torch.uint8 or packed.numel() != sum(h * w * 3 for h, w in sizes):
+        raise L.IcapError("clip_preprocess_packed: packed must be uint8 holding every image's H*W*3 bytes")
+    geo, tmp_bytes = clip_preprocess_geometry(sizes, size, crop)
     max_rows = max(g[9] for g in geo)
-    px = torch.from_numpy(np.concatenate([a.reshape(-1) for a in arrs])).to(device, non_blocking=True)
+    px = packed.to(device, non_blocking=True)
     geo_t = torch.tensor(geo, dtype=torch.int64).to(device, non_blocking=True)
     tmp = torch.empty(tmp_bytes, dtype=torch.uint8, device=device)
     m = torch.tensor(CLIP_MEAN if mean is None else mean, dtype=torch.float32).to(device)

@@ -204,3 +204,46 @@ def test_val_metrics_summary_written_by_train(tmp_path):
     assert path.read_text().startswith("[\n  {")  # json.dump(..., indent=2)
     for e in (1, 2):
         assert (tmp_path / "out" / "eval_results" / f"epoch_{e}_val_predictions.json").exists()
+
+
+def test_extraction_packed_batches(tmp_path):
+    """The device processor's loader path (icap.images: ImageDirectoryDataset.packed_collate in the workers, one
+    packed uint8 buffer per batch): with a host stand-in for preprocess_packed, every image arrives byte-exact and in
+    the reference's os.listdir order, over 2 worker processes."""
+    import numpy as np
+    from PIL import Image
+
+    from icap.images import ImageDirectoryDataset, extract_directory
+
+    d = tmp_path / "imgs"
+    d.mkdir()
+    rng = np.random.default_rng(0)
+    arrays = {}
+    for i in range(7):
+        a = rng.integers(0, 256, (20 + 3 * i, 30 + i, 3), dtype=np.uint8)
+        name = f"COCO_val2014_{100 + i:012d}.png"  # lossless, so the decoded bytes are the array
+        Image.fromarray(a).save(d / name)
+        arrays[name] = a
+    seen = []
+
+    class PackedStandIn:
+        def preprocess_packed(self, packed, sizes):
+            off = 0
+            feats = []
+            for h, w in sizes:
+                img = packed[off: off + h * w * 3].view(h, w, 3)
+                off += h * w * 3
+                seen.append(img.numpy().copy())
+                feats.append(img.float().mean(dim=(0, 1)))
+            assert off == packed.numel()
+            return torch.stack(feats)
+
+    out = tmp_path / "emb.pt"
+    n = extract_directory(str(d), str(out), lambda px: px, PackedStandIn(), 3, batch_size=3, num_workers=2)
+    assert n == 7
+    names = ImageDirectoryDataset(str(d)).filenames
+    data = torch.load(str(out), weights_only=True)
+    assert data["filenames"] == names
+    for name, img, row in zip(names, seen, data["embeddings"]):
+        assert np.array_equal(img, arrays[name])
+        assert torch.allclose(row, torch.from_numpy(arrays[name]).float().mean(dim=(0, 1)))
