@@ -466,6 +466,10 @@ static int gemm_acquire() {
   const char* e = getenv("ICAP_FUSED_ACQUIRE");
   return e && e[0] == '1' ? 1 : 0;
 }
+static bool kout_fused_on() {  // ICAP_KOUT_FUSED=1: K-outer weight-gradient splits combine in the launch (A/B)
+  const char* e = getenv("ICAP_KOUT_FUSED");
+  return e && e[0] == '1';
+}
 static int gemm_diag() {  // (read per launch: an A/B driver toggles it in one process)
   const char* e = getenv("ICAP_GEMM_DIAG");
   return e ? (atoi(e) & 3) : 0;
@@ -617,6 +621,13 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
     // against 33.9 / 24.7 / 40.3 / 40.2 with the 512-block rule below (profiles/r03_dw_bench.txt)
     splits = (320 + tiles - 1) / tiles;
     if (splits > 6) splits = 6;
+    if (kout_fused_on() && splits >= 2) {  // A/B only (ICAP_KOUT_FUSED=1): in-launch combine, at most 4 splits
+      if (splits > 4) splits = 4;
+      const int64_t pbytes = (int64_t)GBM * GBN * (int64_t)sizeof(float);
+      const int64_t nks_ = (nk + splits - 1) / splits;
+      const int64_t sreal = (nk + nks_ - 1) / nks_;
+      pl.fused = p.tickets && p.tickets_len >= 2 * tiles && p.workspace_bytes >= tiles * sreal * pbytes;
+    }
   } else if (p.split_k == 0 && p.workspace && (p.N & 3) == 0 && nk >= 2 && (tiles <= 64 || (tiles < 256 && nk >= 16))) {
     // the count depends on the shape alone — never on the workspace a caller passes — so a product computed on
     // another stream with its own scratch sums its K ranges in the same order and rounds identically (a

@@ -81,5 +81,31 @@ def main():
         print(f"{desc:52s} " + " ".join(f"{statistics.median(times[f[0]]):13.1f}" for f in FORMS), flush=True)
 
 
+def kout():
+    """The mapper's K-outer weight-gradient products (fp32 C, beta 1): slab + reduce pass vs in-launch combine."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    reps = int(os.environ.get("REPS", "10"))
+    print(f"{'K-outer dW (rows 3200)':40s} {'slab+reduce':>12s} {'in-launch':>12s}")
+    for N_out, K_in in ((768, 3072), (3072, 768), (2304, 768), (768, 768)):
+        dY = (torch.rand((3200, N_out), generator=g) * 2 - 1).to(dev, torch.bfloat16)
+        X = (torch.rand((3200, K_in), generator=g) * 2 - 1).to(dev, torch.bfloat16)
+        C = torch.zeros((N_out, K_in), device=dev)
+        t = {0: [], 1: []}
+        for r in range(reps + 2):
+            for f in (0, 1):
+                os.environ["ICAP_KOUT_FUSED"] = str(f)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ops.gemm(dY, X, C, beta=1.0, M=N_out, N=K_in, K=3200, trans_ab=True)
+                e1.record()
+                torch.cuda.synchronize()
+                if r >= 2:
+                    t[f].append(e0.elapsed_time(e1) * 1e3)
+        os.environ.pop("ICAP_KOUT_FUSED", None)
+        print(f"{N_out}x{K_in}x3200{'':25s} {statistics.median(t[0]):12.1f} {statistics.median(t[1]):12.1f}", flush=True)
+
+
 if __name__ == "__main__":
     main()
+    kout()

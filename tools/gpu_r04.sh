@@ -5,7 +5,10 @@
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd); T=${1:-r4}; O=$R/gpurun_out/$T; mkdir -p $O; cd $R
 export PYTHONUNBUFFERED=1
-if [ "$2" != "skip-tests" ]; then
+if [ "$2" = "quick" ]; then  # the tests of this round's changes only
+  timeout -k 10 600 python -u -m pytest tests/test_lnfold_gpu.py tests/test_fused_splitk_gpu.py tests/test_configs3_gpu.py tests/test_pack_gpu.py tests/test_determinism_gpu.py tests/test_bench_shape_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+  rc=$?; grep -E "FAIL|Error|passed|failed" $O/pytest.log | tail -6; [ $rc -eq 0 ] || exit $rc
+elif [ "$2" != "skip-tests" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
   rc=$?; grep -E "FAIL|Error|passed|failed" $O/pytest.log | tail -6; [ $rc -eq 0 ] || exit $rc
 fi
