@@ -685,6 +685,79 @@ __global__ __launch_bounds__(1024) void colsum_reduce_kernel(int64_t N, int nchu
   }
 }
 
+// Batched column sums: the items' columns are laid end to end (item i at column base[i] of the partial rows);
+// block (x, y) sums 256 columns of one item over row chunk y with the colsum4 loop, so each column's partial is
+// the same float sequence as icap_colsum's.
+struct ColsumBatch {
+  int n;
+  int64_t blk[ICAP_COLSUM_BATCH + 1];   // first x-block of each item (256 columns per block)
+  int64_t base[ICAP_COLSUM_BATCH + 1];  // first partial column of each item; base[n] = total columns
+  const void* src[ICAP_COLSUM_BATCH];
+  int64_t ld[ICAP_COLSUM_BATCH], N[ICAP_COLSUM_BATCH];
+  float* out[ICAP_COLSUM_BATCH];
+};
+template <typename T>
+__global__ __launch_bounds__(256) void colsum4_batch_kernel(ColsumBatch b, int64_t M, int64_t rows_per_chunk,
+                                                           float* __restrict__ partial) {
+  __shared__ float4 red[4][64];
+  const int64_t bx = blockIdx.x;
+  int i = 0;
+  while (i + 1 < b.n && bx >= b.blk[i + 1]) ++i;  // block-uniform
+  const T* __restrict__ src = reinterpret_cast<const T*>(b.src[i]);
+  const int64_t N = b.N[i], ld = b.ld[i];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = ((bx - b.blk[i]) * 64 + lane) * 4;
+  const int64_t m0 = (int64_t)blockIdx.y * rows_per_chunk;
+  int64_t m1 = m0 + rows_per_chunk;
+  if (m1 > M) m1 = M;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+#pragma unroll 4
+    for (int64_t m = m0 + w; m < m1; m += 4) {
+      float v[4];
+      io<T>::ld4(src + m * ld + c, v);
+      a[0] += v[0]; a[1] += v[1]; a[2] += v[2]; a[3] += v[3];
+    }
+  }
+  red[w][lane] = make_float4(a[0], a[1], a[2], a[3]);
+  __syncthreads();
+  if (w == 0 && c < N) {
+    float4 t = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 u = red[k][lane];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    *reinterpret_cast<float4*>(partial + (int64_t)blockIdx.y * b.base[b.n] + b.base[i] + c) = t;
+  }
+}
+
+// colsum_reduce_kernel over the concatenated columns; each column finds its item (the items' N are multiples of 4,
+// not of 64, so a block may straddle two items)
+__global__ __launch_bounds__(1024) void colsum_reduce_batch_kernel(ColsumBatch b, int nchunks,
+                                                                  const float* __restrict__ partial, int acc) {
+  __shared__ float red[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t Nt = b.base[b.n];
+  const int64_t c = (int64_t)blockIdx.x * 64 + tx;
+  float a = 0.f;
+  if (c < Nt) {
+#pragma unroll 4
+    for (int k = ty; k < nchunks; k += 16) a += partial[(int64_t)k * Nt + c];
+  }
+  red[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && c < Nt) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][tx];
+    int i = 0;
+    while (i + 1 < b.n && c >= b.base[i + 1]) ++i;
+    float* o = b.out[i] + (c - b.base[i]);
+    *o = acc ? *o + s : s;
+  }
+}
+
 template <typename TS, typename TD>
 __global__ void map2d_kernel(int64_t M, int64_t N, const TS* __restrict__ src, int64_t lds, TD* __restrict__ dst,
                              int64_t ldd, uint32_t thr, float inv_keep, uint64_t seed0, const uint64_t* seed_ptr,
@@ -1357,6 +1430,39 @@ extern "C" int icap_colsum(int32_t dtype, int64_t M, int64_t N, const void* src,
   hipLaunchKernelGGL(colsum_reduce_kernel, dim3((unsigned)((N + 63) / 64)), dim3(1024), 0, S_(stream), N, (int)ch,
                      partial, out, accumulate);
   return check_launch("icap_colsum(reduce)");
+}
+
+extern "C" int icap_colsum_batch(int32_t dtype, int64_t M, int32_t n, const icap_colsum_item* items,
+                                 int32_t accumulate, void* workspace, void* stream) {
+  ICAP_REQUIRE(n >= 0 && n <= ICAP_COLSUM_BATCH, "icap_colsum_batch: 0 <= n <= ICAP_COLSUM_BATCH");
+  ICAP_REQUIRE(n == 0 || (items && workspace), "icap_colsum_batch: null pointer");
+  ICAP_REQUIRE(M >= 0, "icap_colsum_batch: M < 0");
+  const int es = dtype == ICAP_BF16 ? 2 : 4;
+  ColsumBatch b{};
+  b.n = 0;
+  for (int i = 0; i < n; ++i) {
+    const icap_colsum_item& it = items[i];
+    ICAP_REQUIRE(it.src && it.out, "icap_colsum_batch: null item pointer");
+    ICAP_REQUIRE(it.N >= 0 && it.N % 4 == 0 && it.ld % 4 == 0 && it.ld >= it.N &&
+                     reinterpret_cast<uintptr_t>(it.src) % (4 * es) == 0,
+                 "icap_colsum_batch: items need N % 4 == 0, ld % 4 == 0, ld >= N and a 4-element aligned src");
+    if (it.N == 0) continue;
+    const int k = b.n++;
+    b.src[k] = it.src; b.ld[k] = it.ld; b.N[k] = it.N; b.out[k] = it.out;
+    b.blk[k + 1] = b.blk[k] + (it.N + 255) / 256;
+    b.base[k + 1] = b.base[k] + it.N;
+  }
+  if (b.n == 0) return ICAP_OK;
+  const int64_t ch = colsum_chunks(M);
+  const int64_t rpc = (M + ch - 1) / ch;
+  float* partial = reinterpret_cast<float*>(workspace);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(colsum4_batch_kernel<T>, dim3((unsigned)b.blk[b.n], (unsigned)ch), dim3(256),
+                                       0, S_(stream), b, M, rpc > 0 ? rpc : 1, partial));
+  int rc = check_launch("icap_colsum_batch");
+  if (rc) return rc;
+  hipLaunchKernelGGL(colsum_reduce_batch_kernel, dim3((unsigned)((b.base[b.n] + 63) / 64)), dim3(1024), 0,
+                     S_(stream), b, (int)ch, partial, accumulate);
+  return check_launch("icap_colsum_batch(reduce)");
 }
 
 extern "C" int icap_dropout_apply(int32_t dtype, int64_t M, int64_t N, const void* src, int64_t lds, void* dst,

@@ -664,8 +664,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // per-split K of 16 stages would pick; profiles/r03_fused_ab.txt); ICAP_FUSED_NST=1 restores the variant rule
   if (pl.fused && fused_nst_override() != 1) pl.variant = 0;
   // Long K over at most one 128 x 128 tile per CU and no split (no tickets given): the 4-stage ring at one block per
-  // CU (the double-buffered loop at 2 blocks per CU only pays when a CU holds two tiles).
-  if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 && nk_split > 16 && tiles_plan <= cus)
+  // CU (the double-buffered loop at 2 blocks per CU only pays when a CU holds two tiles). Not for the LayerNorm
+  // statistics hand-off (the ring has no such epilogue: GPT-2 large's 1280 x 1280 products at small batch).
+  if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 && nk_split > 16 && tiles_plan <= cus && !lnx)
     pl.variant = 16;
   if (mx && pl.variant == 5) pl.variant = 4;  // MX at 4 blocks / CU (128 VGPRs) spills: 3 blocks / CU
   if (narrow) {
@@ -678,12 +679,15 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // per call so one process can interleave the forms)
   if (const char* fv = getenv("ICAP_FORCE_TILE")) {
     const int v = atoi(fv);
-    if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 && (v == 0 || v == 4 || v == 5 || v == 12 || v == 13 || v == 16)) {
+    if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 &&
+        (v == 0 || v == 4 || v == 5 || v == 12 || v == 13 || (v == 16 && !lnx))) {
       pl.variant = v;
       tiles_n = (v == 12 || v == 13) ? (p.N + 63) / 64 : (p.N + GBN - 1) / GBN;
       tiles = tiles_m * tiles_n;
     }
   }
+  // the LayerNorm-folded quick_gelu consumer (CLIP c_fc) exists at 3 blocks / CU only (gemm_tile_ln.hip)
+  if (lnx && pl.variant == 0 && p.act == ICAP_ACT_QUICK_GELU) pl.variant = 4;
   pl.tiles_n = (int)tiles_n;
   const bool any_act = (splits == 1 || pl.fused) && (p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE);
   pl.actk = any_act ? ACT_ANY : ACT_OFF;

@@ -57,6 +57,10 @@ class TransposeItem(C.Structure):
     _fields_ = [("src", vp), ("lds", i64), ("dst", vp), ("ldd", i64), ("rows", i64), ("cols", i64)]
 
 
+class ColsumItem(C.Structure):
+    _fields_ = [("src", vp), ("ld", i64), ("N", i64), ("out", vp)]
+
+
 class AttnArgs(C.Structure):
     _fields_ = [
         ("dtype", i32),
@@ -139,6 +143,7 @@ SIGNATURES = {
     "icap_transpose_batch": (C.c_int, [i32, vp, vp]),
     "icap_colsum_workspace_bytes": (sz, [i64, i64]),
     "icap_colsum": (C.c_int, [i32, i64, i64, vp, i64, vp, i32, vp, vp]),
+    "icap_colsum_batch": (C.c_int, [i32, i64, i32, vp, i32, vp, vp]),
     "icap_dropout_apply": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, f32, u64, u64, vp, vp]),
     "icap_counter_increment": (C.c_int, [vp, vp]),
     "icap_convert": (C.c_int, [i32, i32, i64, i64, vp, i64, vp, i64, vp]),

@@ -92,6 +92,21 @@ class DWHelper:
     def db(self, dY: Tensor, out: Tensor, M: int, N: Optional[int] = None) -> None:
         ops.colsum(dY, out, self.cs_ws, accumulate=True, M=M, N=N)
 
+    def db_batch(self, items, M: int) -> None:
+        """db += colsum(dY) for every (dY, db) over the same M rows: two launches (icap_colsum_batch) instead of
+        two per item; bitwise what db() gives. The workspace holds colsum_cols columns of partials: a call with
+        more columns runs in column groups that fit."""
+        group, cols = [], 0
+        for dy, out in items:
+            n = dy.shape[1]
+            if group and cols + n > self.cs_cols:
+                ops.colsum_batch(group, M, self.cs_ws)
+                group, cols = [], 0
+            group.append((dy, out, None))
+            cols += n
+        if group:
+            ops.colsum_batch(group, M, self.cs_ws)
+
 
 # --------------------------------------------------------------------------- modules (reference names)
 
@@ -415,11 +430,15 @@ class TransformerMapperCore:
             waiter.wait_event(ev)
             ops.keep_event(ev)
 
+        st.db = []
+
         def wgrad(dy, x, w_out, b_out):
-            """dW += dy^T x and db += colsum(dy): on the side stream, behind everything queued on the main stream."""
+            """dW += dy^T x now; db += colsum(dy) is queued for the layer's one batched column sum (flush_db: every
+            dy is a per-layer buffer, alive until the step ends). With a side stream the dW runs there, behind
+            everything queued on the main stream."""
             if side is None:
                 dwh.dW(dy, x, w_out, M=M)
-                dwh.db(dy, b_out, M=M)
+                st.db.append((dy, b_out))
                 return
             main = torch.cuda.current_stream()
             order(side, main)
@@ -429,10 +448,22 @@ class TransformerMapperCore:
                     b_out = _scratch(b_out)
                 if _SIDE_DIAG != "no_dw":
                     dwh.dW(dy, x, w_out, M=M)
-                if _SIDE_DIAG != "no_db":
-                    dwh.db(dy, b_out, M=M)
+            if _SIDE_DIAG != "no_db":
+                st.db.append((dy, b_out))
             if _SIDE_SERIAL:  # diagnostic: the side stream, but joined after every fork (no concurrency)
                 order(main, side)
+
+        def flush_db():
+            """The layer's bias gradients in one icap_colsum_batch (2 launches instead of 2 per bias)."""
+            if not st.db:
+                return
+            if side is None:
+                dwh.db_batch(st.db, M)
+            else:
+                order(side, torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    dwh.db_batch(st.db, M)
+            st.db = []
 
         def layer(l):
             if l == self.nl - 1:  # start of the backward: d(output) enters the top layer
@@ -466,6 +497,7 @@ class TransformerMapperCore:
                               dx_drop=ws.g_m[l - 1] if (l > 0 and nxt.p > 0) else None, drop=nxt, dgamma=gl.n1_g,
                               dbeta=gl.n1_b, workspace=dwh.ln_ws)
             st.r = out
+            flush_db()
             if side is not None and (join_each or l == 0):  # the layer's grads are final when its step ends
                 order(torch.cuda.current_stream(), side)
 

@@ -613,6 +613,31 @@ def colsum(src: Tensor, out: Tensor, workspace: Tensor, accumulate: bool = True,
     return out
 
 
+COLSUM_BATCH = 16  # include/icap.h ICAP_COLSUM_BATCH
+
+
+def colsum_batch(items, M: int, workspace: Tensor, accumulate: bool = True) -> None:
+    """out (+)= colsum(src[:M, :N]) for every (src, out, N) (N None = src.shape[1]) over the same M rows, in two
+    launches (icap_colsum_batch; bitwise what icap_colsum gives per item). Items the batched kernel cannot take
+    (N or ld not a multiple of 4, a misaligned src, mixed dtypes) go through icap_colsum one by one."""
+    items = [(s, o, s.shape[1] if n is None else n) for s, o, n in items]
+    if not items:
+        return
+    dt = items[0][0].dtype
+    ok = [it for it in items if it[0].dtype == dt and it[2] % 4 == 0 and _ld(it[0]) % 4 == 0
+          and it[0].data_ptr() % (4 * it[0].element_size()) == 0]
+    for s, o, n in items:
+        if not any(s is t[0] and o is t[1] for t in ok):
+            colsum(s, o, workspace, accumulate=accumulate, M=M, N=n)
+    for i in range(0, len(ok), COLSUM_BATCH):
+        part = ok[i: i + COLSUM_BATCH]
+        arr = (L.ColsumItem * len(part))()
+        for it, (s, o, n) in zip(arr, part):
+            it.src, it.ld, it.N, it.out = s.data_ptr(), _ld(s), n, o.data_ptr()
+        call("icap_colsum_batch", dtype_code(dt), M, len(part), C.cast(arr, C.c_void_p), 1 if accumulate else 0,
+             workspace.data_ptr(), _stream())
+
+
 def dropout_apply(src: Tensor, dst: Tensor, drop: Dropout, M: Optional[int] = None,
                   N: Optional[int] = None) -> Tensor:
     M = src.shape[0] if M is None else M

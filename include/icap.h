@@ -348,6 +348,17 @@ int icap_transpose_batch(int32_t n, const icap_transpose_item* items, void* stre
 size_t icap_colsum_workspace_bytes(int64_t M, int64_t N);
 int icap_colsum(int32_t dtype, int64_t M, int64_t N, const void* src, int64_t ld, float* out,
                 int32_t accumulate, void* workspace, void* stream);
+/* Several column sums over the same M rows in two launches (partials + reduce) instead of two each: the trained  */
+/* mapper's four bias gradients per layer (src/models.py:100-107 TransformerMapper -> nn.TransformerEncoderLayer    */
+/* linear1 / linear2 / in_proj / out_proj biases). Every item needs N % 4 == 0, ld % 4 == 0 and a src aligned to   */
+/* 4 elements; at most ICAP_COLSUM_BATCH items. Each out equals what icap_colsum gives for the same item (same     */
+/* chunking and summation order: bitwise). Workspace: icap_colsum_workspace_bytes(M, sum of the items' N).          */
+#define ICAP_COLSUM_BATCH 16
+typedef struct {
+  const void* src; int64_t ld; int64_t N; float* out;
+} icap_colsum_item;
+int icap_colsum_batch(int32_t dtype, int64_t M, int32_t n, const icap_colsum_item* items, int32_t accumulate,
+                      void* workspace, void* stream);
 /* dst[m, n] = src[m, n] * dropmask(p, seed, offset + m*N + n) (or plain copy) */
 int icap_dropout_apply(int32_t dtype, int64_t M, int64_t N, const void* src, int64_t lds,
                        void* dst, int64_t ldd, float drop_p, uint64_t seed, uint64_t offset,

@@ -131,6 +131,14 @@ def accesses(name, args):
     elif name == "icap_colsum":
         dt, M, N, src, ld, o, _acc, ws, _s = a
         out += [("src", src, _rows(M, ld, N, ES[dt])), ("out", o, N * 4), ("ws", ws, ops.colsum_workspace(M, N))]
+    elif name == "icap_colsum_batch":
+        dt, M, n, ptr, _acc, ws, _s = a
+        from icap import _lib as _L
+        addr = ptr.value if hasattr(ptr, "value") else ptr
+        items = list((_L.ColsumItem * n).from_address(addr))
+        for it in items:
+            out += [("src", it.src, _rows(M, it.ld, it.N, ES[dt])), ("out", it.out, it.N * 4)]
+        out.append(("ws", ws, ops.colsum_workspace(M, sum(it.N for it in items))))
     elif name == "icap_dropout_apply":
         dt, M, N, src, lds, dst, ldd, _p, _sd, _o, sp, _s = a
         out += [("src", src, _rows(M, lds, N, ES[dt])), ("dst", dst, _rows(M, ldd, N, ES[dt])), ("seed_ptr", sp, 8)]

@@ -503,6 +503,28 @@ def test_transpose_colsum_bf16_vector_paths(dev, rows, cols, rows_pad):
     assert rel_err(cs, x.double().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_colsum_batch_bitwise(dev, dtype):
+    """icap_colsum_batch (the mapper's four bias gradients per layer in two launches) stores, per item, exactly
+    what icap_colsum gives for it (same chunking and summation order), accumulating and not; items the batched
+    kernel cannot take (N % 4 != 0, here 130) go through icap_colsum inside ops.colsum_batch."""
+    M = 3200
+    widths = [768, 3072, 768, 2304, 132, 130]
+    src = [rnd((M, n + 4), dev, dtype, seed=60 + i)[:, 2:2 + n] if i == 4 else rnd((M, n), dev, dtype, seed=60 + i)
+           for i, n in enumerate(widths)]  # item 4: strided rows, src offset by 2 elements (misaligned -> fallback)
+    ws = torch.empty(ops.colsum_workspace(M, sum(widths)), dtype=torch.uint8, device=dev)
+    for acc in (False, True):
+        init = [torch.randn(n, generator=torch.Generator().manual_seed(70 + i)).to(dev) for i, n in enumerate(widths)]
+        want = [t.clone() for t in init]
+        got = [t.clone() for t in init]
+        for s, o in zip(src, want):
+            ops.colsum(s, o, ws, accumulate=acc)
+        ops.colsum_batch([(s, o, None) for s, o in zip(src, got)], M, ws, accumulate=acc)
+        for i, (a, b) in enumerate(zip(want, got)):
+            assert torch.equal(a, b), (acc, i)
+        assert rel_err(got[1] - (init[1] if acc else 0), src[1].double().sum(0)) < 1e-5
+
+
 def test_caption_prep_target_compaction(dev):
     """row_slot / labels_compact / n_valid vs a host restatement of the shifted-label rule
     (HF/loss/loss_utils.py:49-71 shift, src/models.py:296-317 prefix labels -100)."""

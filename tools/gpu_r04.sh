@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-4 GPU pass: every -m gpu test, the default bench line (with the per-shape GEMM / attention table of its
 # eager roofline pass), and a rocprofv3 kernel-time table of the packed train step. Stops at the first failing step.
-# usage: tools/gpu_r04.sh TAG [skip-tests]
+# usage: tools/gpu_r04.sh TAG [quick|skip-tests|full] [bench-only]
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd); T=${1:-r4}; O=$R/gpurun_out/$T; mkdir -p $O; cd $R
 export PYTHONUNBUFFERED=1
@@ -14,6 +14,7 @@ elif [ "$2" != "skip-tests" ]; then
 fi
 ICAP_GEMM_DETAIL=$O/gemm_detail.txt timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err
 rc=$?; tail -1 $O/bench.json | cut -c1-400; [ $rc -eq 0 ] || { tail -5 $O/bench.err; exit $rc; }
+[ "$3" = "bench-only" ] && exit 0
 cd /tmp; export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/p -o run -- python3 $R/bench.py --steps 8 --warmup 3 --no-decode --no-cpu-baseline --sweep "" > $O/prof_bench.json 2> $O/prof.err
 rc=$?; [ $rc -eq 0 ] || { tail -5 $O/prof.err; exit $rc; }
@@ -25,6 +26,7 @@ timeout -k 10 300 python -u tools/gemm_tiles_ab.py > $O/gemm_tiles_ab.txt 2>&1 |
 cat $O/gemm_tiles_ab.txt
 # side-stream determinism probes (diagnostic; failures here do not stop the pass)
 for d in none scratch no_dw no_db; do
-  ICAP_SIDE_DW=1 ICAP_SIDE_DIAG=$d timeout -k 10 200 python -u tools/ab/det_probe2.py > $O/det_$d.txt 2>&1 || true
-  echo "== side diag $d"; grep "^call" $O/det_$d.txt | cut -c1-200
+  ICAP_SIDE_DW=1 ICAP_SIDE_DIAG=$d timeout -k 10 200 python -u tools/ab/det_probe2.py > $O/det_$d.txt 2>&1
+  rc=$?; echo "== side diag $d (rc $rc)"; grep "^call" $O/det_$d.txt | cut -c1-200
+  [ $rc -eq 0 ] || exit $rc  # a probe that crashed or timed out ends the pass
 done
