@@ -663,6 +663,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // packed 3584 x 768 x 3072 / x 2304 products: 36.6 / 30.4 vs 40.1 / 32.4 µs with the single-stage form the
   // per-split K of 16 stages would pick; profiles/r03_fused_ab.txt); ICAP_FUSED_NST=1 restores the variant rule
   if (pl.fused && fused_nst_override() != 1) pl.variant = 0;
+  // (A/B only) ICAP_FUSED_NST=4: the in-launch split-K on the 4-stage ring at one block per CU (three stages in
+  // flight per CU instead of the double-buffered pair's two)
+  if (pl.fused && fused_nst_override() == 4 && p.in_dtype == ICAP_BF16 && !p.trans_ab && !lnx) pl.variant = 16;
   // Long K over at most one 128 x 128 tile per CU and no split (no tickets given): the 4-stage ring at one block per
   // CU (the double-buffered loop at 2 blocks per CU only pays when a CU holds two tiles). Not for the LayerNorm
   // statistics hand-off (the ring has no such epilogue: GPT-2 large's 1280 x 1280 products at small batch).
