@@ -172,8 +172,10 @@ def test_ln_fold_consumer(dev, M, N, K, act):
 
 def test_gpt2_train_forward_fold_vs_layernorm(dev, monkeypatch):
     """The packed bf16 train step (GPT-2 small frozen, B = 32, dropout off) with ln_1 / ln_2 folded vs the standalone
-    LayerNorm launches: losses within bf16 rounding (|d| <= 1e-2), the LN backward's saved row statistics within
-    1e-4, the mapper gradient's direction (cosine >= 0.99)."""
+    LayerNorm launches: losses within bf16 rounding (|d| <= 1e-2), the mapper gradient's direction (cosine >= 0.99);
+    and the row statistics the folded run saves for the LayerNorm backward equal those of its own LN inputs (fp64
+    over the stored bf16 rows: mean within 1e-5 of max |x|, rstd rel 1e-4) — the two runs' inputs differ by bf16
+    rounding (folded weights), so their statistics are not compared with each other."""
     from icap import CaptionTrainer
     from icap import gpt2 as G
     from oracle import icap_oracle as O
@@ -192,13 +194,16 @@ def test_gpt2_train_forward_fold_vs_layernorm(dev, monkeypatch):
         t._fwd_bwd(True, 1.0)
         torch.cuda.synchronize()
         n = int(t.gws.m_live.item())
-        res[fold] = (float(t.gws.loss.item()), t.gws.mean1[5][:n].clone(), t.gws.rstd2[7][:n].clone(),
-                     t.flat.flat_grad.clone())
+        if fold:
+            for x, mean, rstd in ((t.gws.x[5], t.gws.mean1[5], t.gws.rstd1[5]), (t.gws.h1[7], t.gws.mean2[7], t.gws.rstd2[7])):
+                xd = x[:n].double()
+                mu, rs = xd.mean(-1), 1.0 / torch.sqrt(xd.var(-1, unbiased=False) + 1e-5)
+                assert float((mean[:n].double() - mu).abs().max()) < 1e-5 * float(xd.abs().max())
+                assert float(((rstd[:n].double() - rs) / rs).abs().max()) < 1e-4
+        res[fold] = (float(t.gws.loss.item()), t.flat.flat_grad.clone())
         del t, model
-    (l1, m1, r1, g1), (l0, m0, r0, g0) = res[True], res[False]
+    (l1, g1), (l0, g0) = res[True], res[False]
     assert abs(l1 - l0) < 1e-2, (l1, l0)
-    assert float((m1 - m0).abs().max()) < 1e-4 * float(m0.abs().max() + 1)
-    assert float(((r1 - r0) / r0).abs().max()) < 1e-3
     cos = float((g1.double() @ g0.double()) / (g1.double().norm() * g0.double().norm()))
     assert cos > 0.99, cos
 
