@@ -437,7 +437,7 @@ def kernel_peak(name: str) -> float:
     return FP8_PEAK_TFLOPS if "fp8_t" in name else BF16_PEAK_TFLOPS
 
 
-def train_rate(trainer, B, steps, warmup, use_graph, world, dev):
+def train_rate(trainer, B, steps, warmup, use_graph, world, dev, detail=False):
     """images/s over `steps` graph-replayed steps after `warmup` (barrier + synchronize on both sides, max over
     ranks), the per-step median (HIP events between the steps on the launch stream), and the GEMM roofline of one
     eager step (HIP events around every GEMM / GPT-2-block attention launch)."""
@@ -489,7 +489,7 @@ def train_rate(trainer, B, steps, warmup, use_graph, world, dev):
     seg_ms = [round(sev[i].elapsed_time(sev[i + 1]), 3) for i in range(len(segs))]
     seg_bytes = [sum(hi - lo for lo, hi in rng) * 4 for rng, _ in segs]
     ops.GEMM_TIMER = None
-    agg = timer.summary(os.environ.get("ICAP_GEMM_DETAIL"))
+    agg = timer.summary(os.environ.get("ICAP_GEMM_DETAIL") if detail else None)  # the headline step's shapes only
     dom = max(agg, key=lambda k: agg[k][2])
     n_l, fl, ms = agg[dom]
     achieved = fl / (ms * 1e-3) / 1e12
@@ -630,7 +630,7 @@ def main():
     trainer.gws.seq_sq_hint = live_rows(labels, trainer.P, squares=True) if packed else None
     use_graph = not args.no_graph
     # timed region + the kernel roofline pass (every GEMM launch of one eager step, timed with HIP events)
-    r = train_rate(trainer, B, args.steps, args.warmup, use_graph, world, dev)
+    r = train_rate(trainer, B, args.steps, args.warmup, use_graph, world, dev, detail=True)
     el, loss, imgs_per_s = r["el"], r["loss"], r["images_per_s"]
     dom, n_l, fl, ms, achieved = r["dom"], r["n_l"], r["fl"], r["ms"], r["achieved"]
     gemm_ms, all_fl, eager_ms = r["gemm_ms"], r["all_fl"], r["eager_ms"]

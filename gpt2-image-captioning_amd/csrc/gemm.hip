@@ -441,8 +441,8 @@ static bool g256_pick(const icap_gemm_args& p) {
 
 static bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
-// A/B switches for the in-launch split-K (read once): ICAP_FUSED_S = forced split count, ICAP_FUSED_NST = 1 gives
-// its K ranges the variant rule (default: the double-buffered kernel)
+// A/B switches for the in-launch split-K: ICAP_FUSED_S = forced split count (read once), ICAP_FUSED_NST = 1 gives
+// its K ranges the variant rule, 4 the 4-stage ring (default: the double-buffered kernel)
 static int fused_s_override() {
   static const int v = [] { const char* e = getenv("ICAP_FUSED_S"); return e ? atoi(e) : 0; }();
   return v;
@@ -478,9 +478,14 @@ static bool spec_act_on() {  // ICAP_SPEC_ACT=0: the runtime-dispatch epilogue e
   static const bool v = [] { const char* e = getenv("ICAP_SPEC_ACT"); return !(e && e[0] == '0'); }();
   return v;
 }
-static int fused_nst_override() {
-  static const int v = [] { const char* e = getenv("ICAP_FUSED_NST"); return e ? atoi(e) : 0; }();
-  return v;
+static int fused_min_nk() {  // (A/B only, read per call) ICAP_FUSED_MINK: fewest K stages for the in-launch split
+  const char* e = getenv("ICAP_FUSED_MINK");
+  const int v = e ? atoi(e) : 0;
+  return v >= 2 ? v : 24;
+}
+static int fused_nst_override() {  // (read per call: tools/gemm_tiles_ab.py toggles it in one process)
+  const char* e = getenv("ICAP_FUSED_NST");
+  return e ? atoi(e) : 0;
 }
 
 
@@ -595,7 +600,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // (not for the K-outer weight-gradient products: measured, their in-launch combine ran 6-7 µs slower than the
   // slab + reduce pass — 768x3072x3200 53 vs 47 µs, profiles/r03_gemm_detail_fused.txt — since the last arriver of
   // a 3-block-per-CU tile reads its partials one accumulator row at a time)
-  if (p.split_k == 0 && p.workspace && !p.trans_ab && (p.N & 3) == 0 && nk >= 24 && tiles_plan < cus) {
+  if (p.split_k == 0 && p.workspace && !p.trans_ab && (p.N & 3) == 0 && nk >= fused_min_nk() && tiles_plan < cus) {
     int64_t sf = (2 * cus + tiles_plan / 2) / tiles_plan;
     if (sf > 4) sf = 4;
     while (sf > 2 && nk / sf < 8) --sf;

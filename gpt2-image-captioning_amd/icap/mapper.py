@@ -37,6 +37,7 @@ def _kout_ok(t: Tensor) -> bool:
 
 
 _SIDE_SERIAL = os.environ.get("ICAP_SIDE_SERIAL", "0") == "1"  # diagnostic only (mapper.backward_steps)
+_DB_BATCH = os.environ.get("ICAP_DB_BATCH", "1") != "0"  # A/B: 0 = one icap_colsum per bias (two launches each)
 _SIDE_DIAG = os.environ.get("ICAP_SIDE_DIAG", "")  # diagnostic only: "scratch" / "no_dw" / "no_db"
 _SCRATCH = {}
 
@@ -457,7 +458,10 @@ class TransformerMapperCore:
             """The layer's bias gradients in one icap_colsum_batch (2 launches instead of 2 per bias)."""
             if not st.db:
                 return
-            if side is None:
+            if not _DB_BATCH:
+                for dy, b_out in st.db:
+                    dwh.db(dy, b_out, M=M)
+            elif side is None:
                 dwh.db_batch(st.db, M)
             else:
                 order(side, torch.cuda.current_stream())

@@ -32,7 +32,7 @@ SHAPES = [  # (M capacity, live rows or None, N, K, epilogue, what)
     (8320, 3584, 768, 2304, "plain", "gpt2 c_attn dX"),
     (6400, None, 768, 3072, "resid", "clip fc2"),
 ]
-FORMS = [("auto", None, 0), ("nosplit", None, 1), ("v0", "0", 1), ("v4", "4", 1), ("v5", "5", 1), ("v12", "12", 1),
+FORMS = [("auto", None, 0), ("auto_ring", "ring", 0), ("split_k8", "mink", 0), ("nosplit", None, 1), ("v0", "0", 1), ("v4", "4", 1), ("v5", "5", 1), ("v12", "12", 1),
          ("v13", "13", 1), ("v16", "16", 1)]
 
 
@@ -64,8 +64,16 @@ def main():
         times = {f[0]: [] for f in FORMS}
         for r in range(reps + 2):
             for name, fv, sk in FORMS:
+                os.environ.pop("ICAP_FUSED_NST", None)
+                os.environ.pop("ICAP_FUSED_MINK", None)
                 if fv is None:
                     os.environ.pop("ICAP_FORCE_TILE", None)
+                elif fv == "ring":  # the automatic plan, its in-launch split-K on the 4-stage ring (ICAP_FUSED_NST=4)
+                    os.environ.pop("ICAP_FORCE_TILE", None)
+                    os.environ["ICAP_FUSED_NST"] = "4"
+                elif fv == "mink":  # in-launch split-K down to 8 K stages (the short-K N = 768 products: S = 2)
+                    os.environ.pop("ICAP_FORCE_TILE", None)
+                    os.environ["ICAP_FUSED_MINK"] = "8"
                 else:
                     os.environ["ICAP_FORCE_TILE"] = fv
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -76,6 +84,8 @@ def main():
                 if r >= 2:
                     times[name].append(e0.elapsed_time(e1) * 1e3)
         os.environ.pop("ICAP_FORCE_TILE", None)
+        os.environ.pop("ICAP_FUSED_NST", None)
+        os.environ.pop("ICAP_FUSED_MINK", None)
         rows = live or M
         desc = f"{what} {rows}x{N}x{K}"
         print(f"{desc:52s} " + " ".join(f"{statistics.median(times[f[0]]):13.1f}" for f in FORMS), flush=True)
