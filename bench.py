@@ -609,9 +609,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # ICAP_BENCH_DP_REHEARSAL=1 (checks only, never a reported line): every rank on cuda:0 over gloo, so the N > 1
+    # path (launcher, buckets, max-over-ranks timing, the data_parallel fields) runs on a one-GPU box
+    rehearsal = dist and os.environ.get("ICAP_BENCH_DP_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     if dist:
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     B = args.batch
@@ -667,6 +675,8 @@ def main():
               "allreduce_bytes_per_step": flat_n * bpe, "allreduce_dtype": "bf16" if trainer.dp_bf16 else "fp32",
               "buckets": len(trainer._ranges_mapper) + 1 if trainer.dp_overlap else 1,
               "overlapped": bool(trainer.dp_overlap)}
+        if rehearsal:
+            dp["rehearsal"] = "all ranks on cuda:0 over gloo (path check, not a measurement)"
     if sweep_b or want_padded or want_unfrozen:
         del model, tower, trainer
         torch.cuda.empty_cache()

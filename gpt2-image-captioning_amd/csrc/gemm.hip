@@ -694,6 +694,12 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
       tiles = tiles_m * tiles_n;
     }
   }
+  // (A/B only, read per call) ICAP_LN_VAR = 0 / 4 / 5: that 128 x 128 variant for the LayerNorm hand-off launches
+  if (lnx && (pl.variant == 0 || pl.variant == 4 || pl.variant == 5)) {
+    const char* e = getenv("ICAP_LN_VAR");
+    const int lv = e ? atoi(e) : -1;
+    if (lv == 0 || lv == 4 || lv == 5) pl.variant = lv;
+  }
   // the LayerNorm-folded quick_gelu consumer (CLIP c_fc) exists at 3 blocks / CU only (gemm_tile_ln.hip)
   if (lnx && pl.variant == 0 && p.act == ICAP_ACT_QUICK_GELU) pl.variant = 4;
   pl.tiles_n = (int)tiles_n;

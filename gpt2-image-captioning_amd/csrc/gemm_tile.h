@@ -96,7 +96,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   static_assert(NW * EPR * ELD * 4 <= NST * STB, "epilogue staging must fit the stage buffers");
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "each wave stages whole 8-row DMA pieces");
   constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW);  // DMA instructions per wave per stage
-  __shared__ __attribute__((aligned(16))) char smem[NST * STB];
+  // (+ the consumer's LayerNorm row table, LNX == 2: its own 8 BM bytes past the stage buffers)
+  __shared__ __attribute__((aligned(16))) char smem[NST * STB + (LNX == 2 ? 8 * BM : 0)];
   constexpr int ES = sizeof(TI);
   constexpr int EPC = 16 / ES;         // elements per 16-byte chunk
   constexpr int BKE = GROWB / ES;      // K elements per stage
@@ -189,6 +190,43 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
 #pragma unroll
     for (int i = 0; i < BPW; ++i) dma16(rb_rsrc, Bs + (wave * BPW + i) * 8 * GROWB, kin ? b_off[i] + kb : OOB);
   };
+
+  // ---- LayerNorm fold (consumer, LNX == 2): the row statistics of A from the producer's per-32-column (mean, M2)
+  // pairs, two threads per row: the mean of the group means, then M2 = sum M2_g + 32 (mean_g - mean)^2 (two passes
+  // over the loaded pairs, no E[x^2] - mean^2 cancellation); rstd = 1 / sqrt(M2 / K + eps). Computed in the prologue,
+  // right after the first stage's DMA is issued (its loads overlap that DMA instead of adding a dependent round
+  // trip to the epilogue), into an LDS table of its own that the epilogue rows read after the main loop's barriers.
+  float* lnr = reinterpret_cast<float*>(smem + NST * STB);
+  auto ln_prologue = [&]() __attribute__((always_inline)) {
+    if constexpr (LNX == 2) {
+      static_assert(NW * 64 == 2 * BM, "two threads per LN table row");
+      const int rr = tid >> 1, hf = tid & 1;
+      const int64_t grow = m0 + rr < Mv ? m0 + rr : Mv - 1;
+      const int G = (int)(K >> 5);
+      const float2* st = reinterpret_cast<const float2*>(p.ln_stats_in) + grow * G;
+      float sm = 0.f;
+      for (int g = hf; g < G; g += 2) sm += st[g].x;
+      sm += __shfl_xor(sm, 1, 64);
+      const float mean = sm / (float)G;
+      float m2 = 0.f;
+      for (int g = hf; g < G; g += 2) {
+        const float2 v = st[g];
+        const float d = v.x - mean;
+        m2 += v.y + 32.f * d * d;
+      }
+      m2 += __shfl_xor(m2, 1, 64);
+      const float rs = 1.f / sqrtf(m2 / (float)K + p.ln_eps);
+      if (hf == 0) {
+        lnr[2 * rr] = mean;
+        lnr[2 * rr + 1] = rs;
+        if (p.ln_mean_out && tn == 0 && split == 0 && m0 + rr < Mv) {  // for the LayerNorm backward (one block)
+          p.ln_mean_out[m0 + rr] = mean;
+          p.ln_rstd_out[m0 + rr] = rs;
+        }
+      }
+    }
+  };
+  static_assert(LNX != 2 || NST != 4, "the ring has no LayerNorm-fold prologue");
 
   f32x4_t acc[TM][TN];
 #pragma unroll
@@ -349,6 +387,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   } else if (NST == 2) {
     load_stage(kbase + kstep(0), 0);
     load_scales(kt0, sca_cur, scb_cur);
+    ln_prologue();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
@@ -378,6 +417,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       if (kt > 0) __syncthreads();  // every wave has finished reading the previous stage
       load_stage(kbase + kstep(kt), 0);
       load_scales(kt0 + kt, sca_cur, scb_cur);
+      if (kt == 0) ln_prologue();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       frag_t af[KS][TM], bfr[KS][TN];
@@ -541,44 +581,13 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
                (p.ldc % EW) == 0 && (reinterpret_cast<uintptr_t>(p.C) & 15) == 0;
     prefetch(std::integral_constant<int, 0>{});
   }
-  // ---- LayerNorm fold (consumer, LNX == 2): the row statistics of A from the producer's per-32-column (mean, M2)
-  // pairs, two threads per row: the mean of the group means, then M2 = sum M2_g + 32 (mean_g - mean)^2 (two passes
-  // over the loaded pairs, no E[x^2] - mean^2 cancellation); rstd = 1 / sqrt(M2 / K + eps). Kept in an LDS table at
-  // the end of the stage buffers (past the accumulator staging) until the epilogue rows read it.
-  float ln_mean = 0.f, ln_rs = 0.f, wsumw[EW];
-  float* lnr = reinterpret_cast<float*>(smem + NST * STB) - 2 * BM;
+  // the consumer's epilogue factor: wsum of W gamma per output column (its row table came from the prologue)
+  float wsumw[EW];
   if constexpr (LNX == 2) {
-    static_assert(NW * EPR * ELD * 4 + 8 * BM <= NST * STB && NW * 64 == 2 * BM, "LN table must fit past the staging");
 #pragma unroll
     for (int e = 0; e < EW; ++e) wsumw[e] = (col + e < N) ? p.ln_wsum[col + e] : 0.f;
-    const int rr = tid >> 1, hf = tid & 1;
-    const int64_t grow = m0 + rr < Mv ? m0 + rr : Mv - 1;
-    const int G = (int)(K >> 5);
-    const float2* st = reinterpret_cast<const float2*>(p.ln_stats_in) + grow * G;
-    float sm = 0.f;
-    for (int g = hf; g < G; g += 2) sm += st[g].x;
-    sm += __shfl_xor(sm, 1, 64);
-    ln_mean = sm / (float)G;
-    float m2 = 0.f;
-    for (int g = hf; g < G; g += 2) {
-      const float2 v = st[g];
-      const float d = v.x - ln_mean;
-      m2 += v.y + 32.f * d * d;
-    }
-    m2 += __shfl_xor(m2, 1, 64);
-    ln_rs = 1.f / sqrtf(m2 / (float)K + p.ln_eps);
-    if (whole && hf == 0 && p.ln_mean_out && tn == 0 && m0 + rr < Mv) {  // for the LayerNorm backward
-      p.ln_mean_out[m0 + rr] = ln_mean;
-      p.ln_rstd_out[m0 + rr] = ln_rs;
-    }
   }
   if (NST == 1) __syncthreads();  // the single stage buffer is still being read by other waves
-  if constexpr (LNX == 2) {  // (published by the barrier after the first staging pass)
-    if ((tid & 1) == 0) {
-      lnr[2 * (tid >> 1)] = ln_mean;
-      lnr[2 * (tid >> 1) + 1] = ln_rs;
-    }
-  }
   // rows [EPR h, EPR h + EPR) of this wave's accumulator tile -> LDS (h compile-time: it indexes acc[])
   auto stage_rows = [&](auto hc) __attribute__((always_inline)) {
     constexpr int h = decltype(hc)::value;

@@ -24,7 +24,7 @@ timeout -k 10 300 python -u tools/gemm_diag.py > $O/gemm_diag.txt 2>&1 || { tail
 cat $O/gemm_diag.txt
 timeout -k 10 300 python -u tools/gemm_tiles_ab.py > $O/gemm_tiles_ab.txt 2>&1 || { tail -5 $O/gemm_tiles_ab.txt; exit 1; }
 cat $O/gemm_tiles_ab.txt
-bash tools/ab/train_ab.sh $O/train_ab "base=" "fold0=ICAP_TRAIN_LN_FOLD=0" "dbloop=ICAP_DB_BATCH=0" | tee $O/train_ab.txt || exit 1
+bash tools/ab/train_ab.sh $O/train_ab "base=" "fold0=ICAP_TRAIN_LN_FOLD=0" "lnvar4=ICAP_LN_VAR=4" "dbloop=ICAP_DB_BATCH=0" | tee $O/train_ab.txt || exit 1
 # side-stream determinism probes (diagnostic; failures here do not stop the pass)
 for d in none scratch no_dw no_db; do
   ICAP_SIDE_DW=1 ICAP_SIDE_DIAG=$d timeout -k 10 200 python -u tools/ab/det_probe2.py > $O/det_$d.txt 2>&1
