@@ -389,8 +389,10 @@ static int gemm_variant(const icap_gemm_args& p, int64_t nk_per_block) {
   const bool heavy = p.dact != ICAP_ACT_NONE || p.aux;
   const bool act = p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE;
   // (A/B) ICAP_VAR_HEAVY / ICAP_VAR_ACT / ICAP_VAR_LIGHT: variant for short-K launches with dact / aux, with an
-  // activation only, and with neither
-  static const int vh = env_int("ICAP_VAR_HEAVY", 5), va = env_int("ICAP_VAR_ACT", 4), vl = env_int("ICAP_VAR_LIGHT", 4);
+  // activation only, and with neither. Round 4: dact / aux launches at 3 blocks / CU too — the 4-block form (128
+  // VGPRs) spills with those epilogues (profiles/r04_gemm_tiles_ab.txt: GPT-2 c_fc gelu + aux 42.2 vs 46.2 us,
+  // mlp c_proj dgelu 43.4 vs 43.5)
+  static const int vh = env_int("ICAP_VAR_HEAVY", 4), va = env_int("ICAP_VAR_ACT", 4), vl = env_int("ICAP_VAR_LIGHT", 4);
   return heavy ? vh : act ? va : vl;
 }
 
@@ -544,9 +546,10 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
                  "icap_gemm: ln_stats_out / ln_stats_in: bf16 A/B/C, no trans_ab / ln_gamma / path 3 / beta, not both");
     ICAP_REQUIRE(!p.ln_stats_out || (p.N % 32 == 0 && p.act == ICAP_ACT_NONE && p.dact == ICAP_ACT_NONE),
                  "icap_gemm: ln_stats_out needs N % 32 == 0 and no activation");
-    ICAP_REQUIRE(!p.ln_stats_in || (p.ln_wsum && p.K % 32 == 0 && p.dact == ICAP_ACT_NONE &&
-                                    (p.ln_mean_out == nullptr) == (p.ln_rstd_out == nullptr)),
-                 "icap_gemm: ln_stats_in needs ln_wsum, K % 32 == 0, no dact, ln_mean_out with ln_rstd_out");
+    ICAP_REQUIRE(!p.ln_stats_in || (p.ln_wsum && p.K % 128 == 0 && p.K <= 1280 && p.dact == ICAP_ACT_NONE &&
+                                    al16(p.ln_stats_in) && (p.ln_mean_out == nullptr) == (p.ln_rstd_out == nullptr)),
+                 "icap_gemm: ln_stats_in needs ln_wsum, K % 128 == 0, K <= 1280, 16-byte aligned statistics, no dact, "
+                 "ln_mean_out with ln_rstd_out");
   }
   const bool fold_ln = p.ln_wsum != nullptr && !p.ln_stats_in;  // (the skinny decode form: stats from A fragments)
   ICAP_REQUIRE(!fold_ln || (!fuse_ln && p.M <= 128 && p.split_k == 0 && !p.trans_ab && !mx && p.K <= 4096),

@@ -200,20 +200,30 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   auto ln_prologue = [&]() __attribute__((always_inline)) {
     if constexpr (LNX == 2) {
       static_assert(NW * 64 == 2 * BM, "two threads per LN table row");
+      // each thread of the pair holds one half of the row's G pairs: G / 4 16-byte loads issued together (the host
+      // guarantees G % 4 == 0 and G <= 4 LNQ), both passes from registers
+      constexpr int LNQ = 10;  // 16-byte loads per thread at most: K <= 1280
       const int rr = tid >> 1, hf = tid & 1;
       const int64_t grow = m0 + rr < Mv ? m0 + rr : Mv - 1;
-      const int G = (int)(K >> 5);
-      const float2* st = reinterpret_cast<const float2*>(p.ln_stats_in) + grow * G;
+      const int G = (int)(K >> 5), nq = G >> 2;
+      const float4* st = reinterpret_cast<const float4*>(p.ln_stats_in) + grow * (G >> 1) + hf * nq;
+      float4 v[LNQ];
+#pragma unroll
+      for (int q = 0; q < LNQ; ++q)
+        if (q < nq) v[q] = st[q];
       float sm = 0.f;
-      for (int g = hf; g < G; g += 2) sm += st[g].x;
+#pragma unroll
+      for (int q = 0; q < LNQ; ++q)
+        if (q < nq) sm += v[q].x + v[q].z;
       sm += __shfl_xor(sm, 1, 64);
       const float mean = sm / (float)G;
       float m2 = 0.f;
-      for (int g = hf; g < G; g += 2) {
-        const float2 v = st[g];
-        const float d = v.x - mean;
-        m2 += v.y + 32.f * d * d;
-      }
+#pragma unroll
+      for (int q = 0; q < LNQ; ++q)
+        if (q < nq) {
+          const float d0 = v[q].x - mean, d1 = v[q].z - mean;
+          m2 += (v[q].y + 32.f * d0 * d0) + (v[q].w + 32.f * d1 * d1);
+        }
       m2 += __shfl_xor(m2, 1, 64);
       const float rs = 1.f / sqrtf(m2 / (float)K + p.ln_eps);
       if (hf == 0) {

@@ -140,7 +140,8 @@ typedef struct {
   /* into the QKV / c_fc products: HF/models/gpt2/modeling_gpt2.py:281,301; CLIP layer_norm1/2                     */
   /* modeling_clip.py:365-384). ln_stats_out (producer, bf16 C, N % 32 == 0): per row and 32-column group of the   */
   /* stored C values, (mean, M2 = sum of squared deviations) as fp32 pairs [M][N/32][2]. ln_stats_in (consumer,    */
-  /* with ln_wsum, bias = b + W.beta, B = W*gamma, ln_eps; K % 32 == 0): the producer's statistics of A            */
+  /* with ln_wsum, bias = b + W.beta, B = W*gamma, ln_eps; K % 128 == 0, K <= 1280, 16-byte aligned): the        */
+  /* producer's statistics of A                                                                                      */
   /* [M][K/32][2], combined per row (two-pass: mean of the group means, then M2 + 32 (mean_g - mean)^2) into mean  */
   /* and rstd = 1/sqrt(M2/K + eps), and C = rstd (A.B^T - mean ln_wsum) + bias, then the epilogue. ln_mean_out /   */
   /* ln_rstd_out (optional, consumer): those row statistics (fp32 [M]) for the LayerNorm backward. bf16 inputs,   */

@@ -10,6 +10,9 @@ B = 32
 model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
 t = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10, dropout=False)
 print("side", t._side)
+if os.environ.get("PROBE_DW_SPLIT"):  # force the K-outer dW split count (1: no slab workspace on the side stream)
+    t.dwh.split_k = int(os.environ["PROBE_DW_SPLIT"])
+    print("dW split_k", t.dwh.split_k)
 t.load_batch(*_batch(B, dev))
 w = t.mws
 def snap():

@@ -20,14 +20,18 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/p -o run -- python3 $R/
 rc=$?; [ $rc -eq 0 ] || { tail -5 $O/prof.err; exit $rc; }
 cd $R && python tools/kstats.py $O/p/run_results.db "packed bench train step x (3 warm-up + 8 timed + 1 eager roofline pass)" > $O/kstats.txt && head -14 $O/kstats.txt | cut -c1-150
 rm -rf $O/p
-timeout -k 10 300 python -u tools/gemm_diag.py > $O/gemm_diag.txt 2>&1 || { tail -5 $O/gemm_diag.txt; exit 1; }
-cat $O/gemm_diag.txt
-timeout -k 10 300 python -u tools/gemm_tiles_ab.py > $O/gemm_tiles_ab.txt 2>&1 || { tail -5 $O/gemm_tiles_ab.txt; exit 1; }
-cat $O/gemm_tiles_ab.txt
-bash tools/ab/train_ab.sh $O/train_ab "base=" "fold0=ICAP_TRAIN_LN_FOLD=0" "lnvar4=ICAP_LN_VAR=4" "dbloop=ICAP_DB_BATCH=0" | tee $O/train_ab.txt || exit 1
+if [ -z "$SKIP_DIAG" ]; then
+  timeout -k 10 300 python -u tools/gemm_diag.py > $O/gemm_diag.txt 2>&1 || { tail -5 $O/gemm_diag.txt; exit 1; }
+  cat $O/gemm_diag.txt
+  timeout -k 10 300 python -u tools/gemm_tiles_ab.py > $O/gemm_tiles_ab.txt 2>&1 || { tail -5 $O/gemm_tiles_ab.txt; exit 1; }
+  cat $O/gemm_tiles_ab.txt
+fi
+if [ -n "$TRAIN_AB" ]; then  # e.g. TRAIN_AB='base= fold0=ICAP_TRAIN_LN_FOLD=0'
+  bash tools/ab/train_ab.sh $O/train_ab $TRAIN_AB | tee $O/train_ab.txt || exit 1
+fi
 # side-stream determinism probes (diagnostic; failures here do not stop the pass)
-for d in none scratch no_dw no_db; do
-  ICAP_SIDE_DW=1 ICAP_SIDE_DIAG=$d timeout -k 10 200 python -u tools/ab/det_probe2.py > $O/det_$d.txt 2>&1
+for d in ${DET_DIAGS:-none scratch no_dw no_db}; do
+  ICAP_SIDE_DW=1 ICAP_SIDE_DIAG=${d%%+*} PROBE_DW_SPLIT=$([ "${d#*+}" = "split1" ] && echo 1) timeout -k 10 200 python -u tools/ab/det_probe2.py > $O/det_$d.txt 2>&1
   rc=$?; echo "== side diag $d (rc $rc)"; grep "^call" $O/det_$d.txt | cut -c1-200
   [ $rc -eq 0 ] || exit $rc  # a probe that crashed or timed out ends the pass
 done
