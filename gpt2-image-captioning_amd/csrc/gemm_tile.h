@@ -33,6 +33,20 @@
 #pragma once
 #include "gemm_common.h"
 
+// Diagnostic builds only (make stamps: -DICAP_STAMPS): phase timestamps per workgroup into icap_gemm_args.diag_stamps
+// (8 uint64 per blockIdx.x; s_memrealtime, 100 MHz): [0] split | order << 8 | tile << 32, [1] start, [2] first stage
+// landed, [3] main loop done, [4] split-K publish / combine done, [5] epilogue done. Not compiled otherwise.
+#ifdef ICAP_STAMPS
+#define ICAP_STAMP(i, v)                                                                                         \
+  do {                                                                                                         \
+    if (p.diag_stamps && threadIdx.x == 0) p.diag_stamps[(int64_t)blockIdx.x * 8 + (i)] = (uint64_t)(v);       \
+  } while (0)
+#define ICAP_NOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define ICAP_STAMP(i, v) do {} while (0)
+#define ICAP_NOW() 0ull
+#endif
+
 namespace icap {
 
 // ---- K-outer operand images (trans_ab): [64 k-rows][128 columns] bf16, 256-byte rows, 16-byte chunk ch of row r
@@ -127,6 +141,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   if (m0 >= Mv) return;
+  ICAP_STAMP(1, ICAP_NOW());
   // tile-relative buffer descriptors: rows past M / N fall beyond num_records and load zeros
   // (K-outer: k-rows past K do; columns past M / N read neighbouring data that only reaches unstored outputs)
   const char* Ab = reinterpret_cast<const char*>(p.A) + (KOUT ? m0 : m0 * p.lda) * ES;
@@ -400,6 +415,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     ln_prologue();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    ICAP_STAMP(2, ICAP_NOW());
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       // all fragment reads of this stage first: hipcc waits vmcnt(0) before any LDS read that follows an
@@ -430,6 +446,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       if (kt == 0) ln_prologue();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (kt == 0) ICAP_STAMP(2, ICAP_NOW());
       frag_t af[KS][TM], bfr[KS][TN];
       read_frags(smem, af, bfr);
       mfmas(af, bfr);
@@ -443,6 +460,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   // so the sum is deterministic), resets the tile's two counters for the next launch, and runs the whole epilogue.
   // Nobody waits on a block that has not taken its ticket, so there is no residency assumption
   // (cdna_hip_programming.md §5 "In-launch split-K reduction", §6 Guideline 16 R1 with sc1 loads).
+  ICAP_STAMP(3, ICAP_NOW());
   const bool fused = splits > 1 && p.tickets != nullptr;
   if (fused) {
     typedef uint32_t u32x4f_t __attribute__((ext_vector_type(4)));
@@ -466,6 +484,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload has left
       __syncthreads();
       if (tid == 0) __hip_atomic_fetch_add(cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ICAP_STAMP(0, (uint64_t)split | ((uint64_t)order << 8) | ((uint64_t)tile << 32));
+      ICAP_STAMP(4, ICAP_NOW());
       return;
     }
     if (tid == 0) {
@@ -526,6 +546,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
         }
     }
   }
+  ICAP_STAMP(0, (uint64_t)split | ((uint64_t)(fused ? splits - 1 : 0) << 8) | ((uint64_t)tile << 32));
+  ICAP_STAMP(4, ICAP_NOW());
   const bool whole = splits == 1 || fused;  // this block applies the full epilogue
 
   uint64_t seed = 0;
@@ -682,6 +704,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       __syncthreads();
     });
   }
+  ICAP_STAMP(5, ICAP_NOW());
 }
 
 }  // namespace icap

@@ -13,7 +13,8 @@ import os
 import torch  # noqa: F401  (must be imported first: the .so binds to torch's HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libicap_hip.so")
+# ICAP_LIB: another build of the same ABI (diagnostic builds for tools/: the -DICAP_STAMPS library)
+LIB_PATH = os.environ.get("ICAP_LIB") or os.path.join(_HERE, "libicap_hip.so")
 
 F32, BF16, FP8_MX = 0, 1, 2
 ACT_NONE, ACT_GELU_NEW, ACT_RELU, ACT_QUICK_GELU, ACT_TANH, ACT_GELU_ERF = 0, 1, 2, 3, 4, 5
@@ -50,6 +51,7 @@ class GemmArgs(C.Structure):
         ("tickets", vp), ("tickets_len", i64),
         ("ln_wsum", vp),
         ("ln_stats_out", vp), ("ln_stats_in", vp), ("ln_mean_out", vp), ("ln_rstd_out", vp),
+        ("diag_stamps", vp),
     ]
 
 

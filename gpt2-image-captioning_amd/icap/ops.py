@@ -153,7 +153,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None,
          tile_only: bool = False, g256: bool = False, m_hint: Optional[int] = None,
          ln_fold: Optional[tuple] = None, ln_stats_out: Optional[Tensor] = None,
-         ln_stats_in: Optional[Tensor] = None, ln_rows_out: Optional[tuple] = None) -> Tensor:
+         ln_stats_in: Optional[Tensor] = None, ln_rows_out: Optional[tuple] = None,
+         diag_stamps: Optional[Tensor] = None) -> Tensor:
     """out[M,N] = epi(alpha * A[M,K] @ B[N,K]^T) — see icap_gemm in include/icap.h.
     workspace: fp32 split-K scratch; by default one buffer per (device, stream), so GEMMs issued on different
     streams never share slabs (gemm_workspace). The split count depends on the shape alone, so the result is
@@ -231,6 +232,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
         a.ln_stats_in = ln_stats_in.data_ptr()
     if ln_rows_out is not None:
         a.ln_mean_out, a.ln_rstd_out = ln_rows_out[0].data_ptr(), ln_rows_out[1].data_ptr()
+    if diag_stamps is not None:  # (read only by a -DICAP_STAMPS build: tools/gemm_stamps.py)
+        a.diag_stamps = diag_stamps.data_ptr()
     if GEMM_TIMER is None:
         call("icap_gemm", C.byref(a), _stream())
     else:  # per-launch HIP-event timing (bench.py kernel roofline pass; never inside a captured graph)

@@ -147,6 +147,9 @@ typedef struct {
   /* ln_rstd_out (optional, consumer): those row statistics (fp32 [M]) for the LayerNorm backward. bf16 inputs,   */
   /* tile kernels only (M > 128 or not), no trans_ab; a split product must be able to combine inside the launch.  */
   float* ln_stats_out; const float* ln_stats_in; float* ln_mean_out; float* ln_rstd_out;
+  /* Diagnostic builds only (compiled with -DICAP_STAMPS; ignored otherwise, keep NULL): 8 uint64 per tile-kernel   */
+  /* workgroup (blockIdx.x) — phase timestamps (s_memrealtime, 100 MHz) for tools/gemm_stamps.py.                  */
+  uint64_t* diag_stamps;
 } icap_gemm_args;
 /* MX block quantisation (the A / B operands of an ICAP_FP8_MX GEMM): x [R, K] (f32 or bf16, row stride ldx) */
 /* -> q [R, K] OCP e4m3fn bytes (row stride ldq % 16 == 0) + the E8M0 scales in icap_gemm_args.a_scale      */
