@@ -335,7 +335,8 @@ def extraction_rate(tower, dev, n_images: int = 512):
     import numpy as np
     from PIL import Image
 
-    from icap.clip import DeviceCLIPProcessor, extract_clip_embeddings
+    from icap.clip import DeviceCLIPProcessor
+    from icap.images import extract_directory
 
     d = tempfile.mkdtemp(prefix="icap_extract_")
     try:
@@ -348,14 +349,20 @@ def extraction_rate(tower, dev, n_images: int = 512):
             Image.fromarray(img).save(os.path.join(d, f"COCO_val2014_{i:012d}.jpg"), quality=90)
         proc = DeviceCLIPProcessor(device=dev)
         out = os.path.join(d, "emb.pt")
-        res = {}
-        for workers in (4, 16):
-            extract_clip_embeddings(d, out, tower, proc, batch_size=64, num_workers=workers, device=dev)  # warm-up
+        res, split = {}, {}
+        dim = tower.config.projection_dim
+        for workers in (4, 8, 16):
+            extract_directory(d, out, tower.embed, proc, dim, 64, workers, dev)  # warm-up (page cache, kernels)
             torch.cuda.synchronize()
+            st = {}
             t0 = time.perf_counter()
-            extract_clip_embeddings(d, out, tower, proc, batch_size=64, num_workers=workers, device=dev)
+            extract_directory(d, out, tower.embed, proc, dim, 64, workers, dev, stats=st)
             torch.cuda.synchronize()
             res[f"images_per_s_{workers}_workers"] = round(n_images / (time.perf_counter() - t0), 1)
+            split[f"{workers}_workers"] = st
+        # where the main process's time goes (s): worker start-up + first batch, waiting on the loader, issuing
+        # the device work, the final copy + save (icap.images.extract_directory stats)
+        res["main_process_split_s"] = split
         res.update({"images": n_images, "image": "640x480 JPEG q90", "batch": 64,
                     "reference_published_images_per_s": 65.0,
                     "includes": "JPEG decode (PIL, DataLoader workers) + device preprocess + CLIP-B/32 bf16 + .pt save"})

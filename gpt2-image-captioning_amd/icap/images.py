@@ -55,22 +55,48 @@ class ImageDirectoryDataset(Dataset):
 
 
 @torch.no_grad()
+def _worker_init(_):
+    """DataLoader worker: one intra-op thread (PIL decodes single-threaded; torch's default of one thread per core
+    in each of N workers oversubscribes the host N-fold)."""
+    torch.set_num_threads(1)
+
+
 def extract_directory(image_dir: str, output_path: str, embed: Callable, processor, out_dim: int,
-                      batch_size: int = 32, num_workers: int = 4, device=None, feature: Optional[str] = None) -> int:
+                      batch_size: int = 32, num_workers: int = 4, device=None, feature: Optional[str] = None,
+                      stats: Optional[dict] = None) -> int:
     """Every image of `image_dir` -> {"filenames": [...], "embeddings": fp32 [N, out_dim]} saved with torch.save
     (src/embeddings/clip.py:147-149 format). `embed(pixel_values)` returns L2-normalised features on the device.
     feature: an extra "feature" string naming what the embeddings are (readers that index "filenames" /
-    "embeddings", src/dataset.py:127-137, ignore it). Returns the number of images."""
+    "embeddings", src/dataset.py:127-137, ignore it). Returns the number of images.
+    stats: filled with the main process's wall-time split (s): first_batch (worker start-up + first decode),
+    wait (blocked on the loader after the first batch), issue (preprocess + embed launches), final (the one copy
+    back + torch.save) — what bounds the loop (bench.py clip_extraction)."""
+    import time
+
+    t_start = time.perf_counter()
     ds = ImageDirectoryDataset(image_dir)
     packed = hasattr(processor, "preprocess_packed")  # the device processor: one packed, pinned buffer per batch
     dev = torch.device(device) if device is not None else None
     pin = packed and dev is not None and dev.type == "cuda"
     dl = DataLoader(ds, batch_size=batch_size, shuffle=False, num_workers=num_workers, pin_memory=pin,
                     collate_fn=ImageDirectoryDataset.packed_collate if packed else ImageDirectoryDataset.collate_fn,
-                    persistent_workers=False)
+                    persistent_workers=False, worker_init_fn=_worker_init if num_workers > 0 else None)
     names: List[str] = []
     embs: List[torch.Tensor] = []
-    for batch in dl:
+    t_wait = t_issue = 0.0
+    t_first = None
+    it = iter(dl)
+    while True:
+        t0 = time.perf_counter()
+        try:
+            batch = next(it)
+        except StopIteration:
+            break
+        t1 = time.perf_counter()
+        if t_first is None:
+            t_first = t1 - t_start
+        else:
+            t_wait += t1 - t0
         if packed:
             batch_names, buf, sizes = batch
             px = processor.preprocess_packed(buf, sizes.tolist())
@@ -83,9 +109,14 @@ def extract_directory(image_dir: str, output_path: str, embed: Callable, process
         # batch): no per-batch synchronisation, so the next batch's host work overlaps this batch's kernels
         embs.append(embed(px))
         names.extend(batch_names)
+        t_issue += time.perf_counter() - t1
+    t2 = time.perf_counter()
     final = torch.cat([e.float() for e in embs], 0).cpu() if embs else torch.empty((0, out_dim))
     out = {"filenames": names, "embeddings": final}
     if feature is not None:
         out["feature"] = feature
     torch.save(out, output_path)
+    if stats is not None:
+        stats.update(first_batch=round(t_first or 0.0, 3), wait=round(t_wait, 3), issue=round(t_issue, 3),
+                     final=round(time.perf_counter() - t2, 3), total=round(time.perf_counter() - t_start, 3))
     return len(names)

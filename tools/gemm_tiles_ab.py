@@ -32,7 +32,7 @@ SHAPES = [  # (M capacity, live rows or None, N, K, epilogue, what)
     (8320, 3584, 768, 2304, "plain", "gpt2 c_attn dX"),
     (6400, None, 768, 3072, "resid", "clip fc2"),
 ]
-FORMS = [("auto", None, 0), ("auto_ring", "ring", 0), ("split_k8", "mink", 0), ("nosplit", None, 1), ("v0", "0", 1), ("v4", "4", 1), ("v5", "5", 1), ("v12", "12", 1),
+FORMS = [("auto", None, 0), ("g256", "g256", 0), ("auto_ring", "ring", 0), ("split_k8", "mink", 0), ("nosplit", None, 1), ("v0", "0", 1), ("v4", "4", 1), ("v5", "5", 1), ("v12", "12", 1),
          ("v13", "13", 1), ("v16", "16", 1)]
 
 
@@ -41,7 +41,10 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     reps = int(os.environ.get("REPS", "10"))
     print(f"{'shape':52s} " + " ".join(f"{f[0]:>13s}" for f in FORMS) + "   (median us; * = auto's kernel)")
+    only = os.environ.get("SHAPES")  # comma-separated substrings of the shape names to run (default: all)
     for M, live, N, K, epi, what in SHAPES:
+        if only and not any(o in what for o in only.split(",")):
+            continue
         A = (torch.rand((M, K), generator=g) * 2 - 1).to(dev, torch.bfloat16)
         B = (torch.rand((N, K), generator=g) * 2 - 1).to(dev, torch.bfloat16)
         C = torch.zeros((M, N), device=dev, dtype=torch.bfloat16)
@@ -66,7 +69,8 @@ def main():
             for name, fv, sk in FORMS:
                 os.environ.pop("ICAP_FUSED_NST", None)
                 os.environ.pop("ICAP_FUSED_MINK", None)
-                if fv is None:
+                g256 = fv == "g256"  # the 256 x 256 8-phase kernel wherever eligible (ops.gemm g256=True)
+                if fv is None or g256:
                     os.environ.pop("ICAP_FORCE_TILE", None)
                 elif fv == "ring":  # the automatic plan, its in-launch split-K on the 4-stage ring (ICAP_FUSED_NST=4)
                     os.environ.pop("ICAP_FORCE_TILE", None)
@@ -78,7 +82,7 @@ def main():
                     os.environ["ICAP_FORCE_TILE"] = fv
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                ops.gemm(A, B, C, split_k=sk, **kw)
+                ops.gemm(A, B, C, split_k=sk, g256=g256, **kw)
                 e1.record()
                 torch.cuda.synchronize()
                 if r >= 2:
@@ -118,4 +122,5 @@ def kout():
 
 if __name__ == "__main__":
     main()
-    kout()
+    if not os.environ.get("SHAPES"):
+        kout()
