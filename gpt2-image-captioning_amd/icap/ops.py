@@ -788,6 +788,18 @@ def clip_preprocess(images, device, size: int = 224, crop: int = 224, mean=None,
     return clip_preprocess_packed(packed, [a.shape[:2] for a in arrs], device, size, crop, mean, std)
 
 
+_NORM_CONSTS = {}
+
+
+def _norm_consts(device, mean: tuple, std: tuple):
+    """(mean, std) fp32 device tensors, uploaded once per (device, values)."""
+    key = (str(torch.device(device)), mean, std)
+    if key not in _NORM_CONSTS:
+        _NORM_CONSTS[key] = (torch.tensor(mean, dtype=torch.float32).to(device),
+                             torch.tensor(std, dtype=torch.float32).to(device))
+    return _NORM_CONSTS[key]
+
+
 def clip_preprocess_packed(packed: Tensor, sizes, device, size: int = 224, crop: int = 224, mean=None,
                            std=None) -> Tensor:
     """clip_preprocess of images already packed back to back: `packed` uint8 [sum H*W*3] (host — pinned for an
@@ -805,10 +817,12 @@ def clip_preprocess_packed(packed: Tensor, sizes, device, size: int = 224, crop:
     geo, tmp_bytes = clip_preprocess_geometry(sizes, size, crop)
     max_rows = max(g[9] for g in geo)
     px = packed.to(device, non_blocking=True)
-    geo_t = torch.tensor(geo, dtype=torch.int64).to(device, non_blocking=True)
+    # no host-blocking copies per batch (a pageable copy waits for the stream, i.e. for the previous batch's
+    # kernels): the geometry table from pinned memory, mean / std uploaded once per device
+    geo_h = torch.tensor(geo, dtype=torch.int64)
+    geo_t = (geo_h.pin_memory() if torch.device(device).type == "cuda" else geo_h).to(device, non_blocking=True)
     tmp = torch.empty(tmp_bytes, dtype=torch.uint8, device=device)
-    m = torch.tensor(CLIP_MEAN if mean is None else mean, dtype=torch.float32).to(device)
-    s = torch.tensor(CLIP_STD if std is None else std, dtype=torch.float32).to(device)
+    m, s = _norm_consts(device, tuple(CLIP_MEAN if mean is None else mean), tuple(CLIP_STD if std is None else std))
     call("icap_clip_preprocess", n, px.data_ptr(), geo_t.data_ptr(), crop, max_rows, tmp.data_ptr(), m.data_ptr(),
          s.data_ptr(), out.data_ptr(), _stream())
     return out
