@@ -26,6 +26,16 @@ snaps = []
 for i in range(4):
     t._fwd_bwd(True, 1.0); torch.cuda.synchronize()
     snaps.append(snap())
+def ndiff(a, b):
+    """(elements that differ as values — NaN == NaN, never-written NaN garbage is not a difference —, max |d|)"""
+    same = (a == b) | (a.isnan() & b.isnan())
+    n = int((~same).sum())
+    d = (a.float() - b.float()).abs()
+    d = d[(~same) & d.isfinite()]
+    return n, float(d.max()) if d.numel() else 0.0
+
+
 for i in range(1, 4):
-    diff = [k for k in snaps[0] if not torch.equal(snaps[i][k], snaps[i - 1][k])]
+    diff = {k: ndiff(snaps[i][k], snaps[i - 1][k]) for k in snaps[0]}
+    diff = {k: v for k, v in diff.items() if v[0]}
     print(f"call {i+1} vs call {i}: differing {diff}", flush=True)
