@@ -317,12 +317,6 @@ class GPT2Core:
                                                                      lw.ln1_b, lw.b_attn)
                 lw.wf_fc_t, lw.ws_fc, lw.bf_fc = self._fold_ln(blk.mlp.c_fc.weight.data, lw.ln2_g, lw.ln2_b,
                                                                lw.b_fc)
-            # ln_f folded into the tied LM head of the decode steps (one launch per token instead of LN + GEMM)
-            wt = torch.zeros((Vp, D), dtype=torch.float32, device=self.dev)
-            wt[:V].copy_(t.wte.weight.data)
-            self.wtef, self.ws_head, self.bf_head = fold_layernorm(
-                wt, self.lnf_g, self.lnf_b, torch.zeros(Vp, dtype=torch.float32, device=self.dev), self.dtype)
-            del wt
         if self.fp8:  # MX e4m3 copies of every frozen product's weight operand, both orientations
             for lw in self.layers:
                 for nm in ("w_attn", "w_proj", "w_fc", "w_mp"):
@@ -748,12 +742,11 @@ class GPT2Core:
         D = self.D
         B = ds.B
         a = ds.a[:B]
-        if B <= 128 and getattr(self, "wtef", None) is not None:  # ln_f folded into the LM head (skinny GEMM)
-            ops.gemm(x_last, self.wtef, ds.logits, bias=self.bf_head, M=B, ln_fold=(self.ws_head, self.eps),
-                     alg_flops=2.0 * B * self.V * D)
-        else:
-            ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
-            self._head_mm(ds, a, B)
+        # (ln_f stays a launch of its own: folded into the tied LM head's skinny GEMM — W*gamma_f, row sums, W.beta_f
+        # — the decode ran 3381 vs 3853 captions/s, profiles/r04_bench_lnf_fold_3381.json: the 50304-column launch
+        # re-derives each row's statistics in every one of its workgroups)
+        ops.layernorm_fwd(x_last, self.lnf_g, self.lnf_b, self.eps, a, None, None, rows=B)
+        self._head_mm(ds, a, B)
         forced = None
         if samp is not None:
             temperature, top_p, seed_dev, forced = samp
