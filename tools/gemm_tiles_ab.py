@@ -95,6 +95,31 @@ def main():
         print(f"{desc:52s} " + " ".join(f"{statistics.median(times[f[0]]):13.1f}" for f in FORMS), flush=True)
 
 
+def kout_splits():
+    """The mapper's K-outer weight-gradient products (fp32 C, beta 1, slab + reduce): forced split counts 1-4 and 6 vs
+    the automatic rule."""
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(2)
+    reps = int(os.environ.get("REPS", "10"))
+    forms = [0, 1, 2, 3, 4, 6]
+    print(f"{'K-outer dW (rows 3200), split_k':40s} " + " ".join(f"{('auto' if f == 0 else f):>8}" for f in forms))
+    for N_out, K_in in ((768, 3072), (3072, 768), (2304, 768), (768, 768)):
+        dY = (torch.rand((3200, N_out), generator=g) * 2 - 1).to(dev, torch.bfloat16)
+        X = (torch.rand((3200, K_in), generator=g) * 2 - 1).to(dev, torch.bfloat16)
+        C = torch.zeros((N_out, K_in), device=dev)
+        t = {f: [] for f in forms}
+        for r in range(reps + 2):
+            for f in forms:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ops.gemm(dY, X, C, beta=1.0, M=N_out, N=K_in, K=3200, trans_ab=True, split_k=f)
+                e1.record()
+                torch.cuda.synchronize()
+                if r >= 2:
+                    t[f].append(e0.elapsed_time(e1) * 1e3)
+        print(f"{N_out}x{K_in}x3200{'':27s} " + " ".join(f"{statistics.median(t[f]):8.1f}" for f in forms), flush=True)
+
+
 def kout():
     """The mapper's K-outer weight-gradient products (fp32 C, beta 1): slab + reduce pass vs in-launch combine."""
     dev = torch.device("cuda", 0)
@@ -124,3 +149,5 @@ if __name__ == "__main__":
     main()
     if not os.environ.get("SHAPES"):
         kout()
+    if os.environ.get("KOUT_SPLITS", "1") == "1":
+        kout_splits()
