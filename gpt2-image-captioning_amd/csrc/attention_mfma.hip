@@ -819,6 +819,8 @@ amfma::Geo mfma_geo(const icap_attn_args* a) {
 // at most SHORT_S tokens with LDS and waves sized for SHORT_S (many blocks per CU: one round over the grid), then the
 // longer ones with the launch's sizing (the short ones exit at once). The caption batches of the train step are all
 // short (prefix + caption up to its last target); the split only changes which blocks run, never the arithmetic.
+// icap_attn_args.short_only: the caller knows no sequence is longer (the trainer, from the batch's labels on the
+// host), so the second pass — ~3-4 us of workgroups that only exit (tools/ab/ln_attn_probe.py) — is not launched.
 constexpr int SHORT_S = 32;
 static bool packed_split(const icap_attn_args* a) { return a->seq_len != nullptr && a->S > SHORT_S; }
 static amfma::Geo short_geo(amfma::Geo g) {
@@ -915,9 +917,11 @@ int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float
     };
     if (packed_split(a)) {
       go(short_geo(g));
-      amfma::Geo gl = g;
-      gl.slo = SHORT_S;
-      go(gl);
+      if (!a->short_only) {
+        amfma::Geo gl = g;
+        gl.slo = SHORT_S;
+        go(gl);
+      }
     } else {
       go(g);
     }
@@ -946,9 +950,11 @@ int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float
       };
       if (packed_split(a)) {
         go(short_geo(g));
-        amfma::Geo gl = g;
-        gl.slo = SHORT_S;
-        go(gl);
+        if (!a->short_only) {
+          amfma::Geo gl = g;
+          gl.slo = SHORT_S;
+          go(gl);
+        }
       } else {
         go(g);
       }

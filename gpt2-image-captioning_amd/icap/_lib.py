@@ -79,6 +79,7 @@ class AttnArgs(C.Structure):
         ("dout", vp), ("ld_dout", i64),
         ("dqkv", vp), ("ld_dqkv", i64),
         ("seq_off", vp), ("seq_len", vp),
+        ("short_only", i32),
     ]
 
 

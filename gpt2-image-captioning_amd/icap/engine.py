@@ -20,6 +20,10 @@ from . import ops
 from .mapper import DWHelper, MLPMapperCore, TransformerMapperCore
 from .models import _embedding_grads
 
+# packed attention launches skip their long-sequence pass when every sequence of the batch is short (set per batch in
+# load_batch); ICAP_SHORT_ONLY=0 always launches both passes (A/B)
+SHORT_ONLY = os.environ.get("ICAP_SHORT_ONLY", "1") != "0"
+
 Tensor = torch.Tensor
 
 
@@ -160,6 +164,11 @@ class CaptionTrainer:
             # expected live rows (icap_gemm_args.m_hint); the device count of every batch is what bounds the work
             self.gws.live_rows_hint = live_rows(labels, self.P)
             self.gws.seq_sq_hint = live_rows(labels, self.P, squares=True)
+        if self.gws.pack and SHORT_ONLY:
+            # every packed sequence of THIS batch <= 32 tokens: the attention launches skip their long-sequence pass
+            # (icap_attn_args.short_only — a guarantee, so it is taken from each batch's labels, and the captured
+            # graphs are keyed on it)
+            self.gws.short_only = max_seq_len(labels, self.P) <= 32
         self.ids.copy_(ids, non_blocking=True)
         self.mask.copy_(mask, non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)
@@ -317,7 +326,7 @@ class CaptionTrainer:
         works = []
         self._pending16 = []
         if use_graph:
-            graphs = self.seg_graphs.get(zero)
+            graphs = self.seg_graphs.get((zero, self.gws.short_only))
             if graphs is None:
                 graphs = self._capture_segments(zero)
             for (rng, _), g in zip(self._segments(zero, self.grad_scale()), graphs):
@@ -346,7 +355,7 @@ class CaptionTrainer:
             with ops.graph_capture(g):
                 fn()
             graphs.append(g)
-        self.seg_graphs[zero] = graphs
+        self.seg_graphs[(zero, self.gws.short_only)] = graphs
         return graphs
 
     def grad_scale(self) -> float:
@@ -375,7 +384,7 @@ class CaptionTrainer:
             self._eager_steps += 1
         elif use_graph and self._eager_steps >= 1:
             with_opt = step and self.world == 1
-            g = self.graphs.get((zero, with_opt))
+            g = self.graphs.get((zero, with_opt, self.gws.short_only))
             if g is None:
                 g = self._capture(zero, with_opt)
             g.replay()
@@ -415,7 +424,7 @@ class CaptionTrainer:
             self._fwd_bwd(zero, self.grad_scale())
             if with_opt:
                 self._optimizer()
-        self.graphs[(zero, with_opt)] = g
+        self.graphs[(zero, with_opt, self.gws.short_only)] = g
         return g
 
     def _capture_opt(self):
@@ -442,6 +451,14 @@ class CaptionTrainer:
 
 
 @torch.no_grad()
+def max_seq_len(labels: Tensor, P: int) -> int:
+    """The longest packed sequence of a batch (icap_caption_pack's seq_len, restated on the host side of the copy)."""
+    valid = (labels != -100).to(torch.int64)
+    pos = torch.arange(1, labels.shape[1] + 1, device=labels.device, dtype=torch.int64)
+    last = (valid * pos).max(dim=1).values
+    return int((P + (last - 1).clamp_min(0)).max().item()) if labels.shape[0] else 0
+
+
 def live_rows(labels: Tensor, P: int, squares: bool = False) -> int:
     """Packed token rows of a batch (icap_caption_pack's m_live, computed on the host side of the copy):
     sum over captions of max(P, P + last caption index with a target); squares: the sum of their squares (the

@@ -389,6 +389,7 @@ class GPT2Core:
         ws.pack = bool(pack and ws.compact)
         ws.live_rows_hint = None  # host-known number of packed rows (roofline bookkeeping only)
         ws.seq_sq_hint = None  # host-known sum of squared packed sequence lengths (attention FLOPs, bookkeeping only)
+        ws.short_only = False  # every packed sequence of the loaded batch <= 32 tokens (set per batch by the trainer)
         ws.seqs = ws.m_live = None
         if ws.pack:
             ws.seq_off = e(B, dtype=torch.int32)
@@ -536,6 +537,7 @@ class GPT2Core:
         scale = 1.0 / math.sqrt(hd)
         rd = getattr(ws, "m_live", None)  # packed rows: device row count (None: every row)
         seqs = getattr(ws, "seqs", None)
+        so = bool(getattr(ws, "short_only", False))  # every packed sequence <= 32 tokens (engine.load_batch)
         afl = self._attn_flops(ws, B, S)
         fold = getattr(ws, "st_x", None) is not None  # ln_1 (l >= 1) / ln_2 folded into the QKV / c_fc GEMMs
         nl = len(self.layers)
@@ -549,7 +551,7 @@ class GPT2Core:
                 ops.layernorm_fwd(x, lw.ln1_g, lw.ln1_b, self.eps, ws.a1[l], ws.mean1[l], ws.rstd1[l], rows_dev=rd)
                 self._bmm(ws, ws.a1[l], ws.qD, lw.w_attn_t, q.qw_attn_t, ws.qkv[l], bias=lw.b_attn)
             ops.attention_fwd(ws.qkv[l], ws.o[l], B=B, S=S, H=H, hd=hd, scale=scale, causal=True, key_mask=causal_mask,
-                              lse=ws.lse[l], drop=dr.attn(l), seqs=seqs, alg_flops=afl)
+                              lse=ws.lse[l], drop=dr.attn(l), seqs=seqs, alg_flops=afl, short_only=so)
             self._bmm(ws, ws.o[l], ws.qD, lw.w_proj_t, q.qw_proj_t, ws.h1[l], bias=lw.b_proj, resid=x, drop=dr.ra(l),
                       **({"ln_stats_out": ws.st_h} if fold else {}))
             if fold:
@@ -586,6 +588,7 @@ class GPT2Core:
         if grads is not None:  # d(wte) from the tied LM head: dW[V,D] += dlogits^T . hf
             dw.dW(dlogits, ws.hf, grads.wte, M=M, N=self.V)
         rd, seqs = ws.m_live, ws.seqs  # packed rows (None: every row)
+        so = bool(getattr(ws, "short_only", False))
         ops.layernorm_bwd(ws.x[-1], self.lnf_g, ws.meanf, ws.rstdf, ws.dhf, ws.dx, dx_drop=ws.dxd,
                           drop=dr.rm(nl - 1), dgamma=grads.lnf_g if grads else None,
                           dbeta=grads.lnf_b if grads else None, workspace=dw.ln_ws if dw else None,
@@ -617,7 +620,8 @@ class GPT2Core:
                 dw.db(dy, g.b_proj, M=M)
             self._bmm(ws, dy, ws.qD, lw.w_proj, q.qw_proj, ws.do)
             ops.attention_bwd(ws.qkv[l], ws.do, ws.lse[l], ws.dqkv, B=B, S=S, H=H, hd=hd, scale=scale, causal=True,
-                              key_mask=causal_mask, drop=dr.attn(l), out=ws.o[l], seqs=seqs, alg_flops=afl)
+                              key_mask=causal_mask, drop=dr.attn(l), out=ws.o[l], seqs=seqs, alg_flops=afl,
+                              short_only=so)
             if g is not None:
                 dw.dW(ws.dqkv, ws.a1[l], g.w_attn, M=M, transpose_out=True)
                 dw.db(ws.dqkv, g.b_attn, M=M)

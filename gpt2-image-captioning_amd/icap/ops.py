@@ -370,10 +370,12 @@ def layernorm_bwd(x: Tensor, gamma: Tensor, mean: Tensor, rstd: Tensor, dy: Tens
 
 
 def _attn_args(qkv: Tensor, B: int, S: int, H: int, hd: int, rsb: int, rss: int, scale: float, causal: bool,
-               key_mask: Optional[Tensor], lse: Optional[Tensor], drop: Dropout, seqs=None) -> AttnArgs:
+               key_mask: Optional[Tensor], lse: Optional[Tensor], drop: Dropout, seqs=None,
+               short_only: bool = False) -> AttnArgs:
     a = AttnArgs()
     if seqs is not None:  # packed sequences: (seq_off, seq_len) int32 [B] (icap_caption_pack)
         a.seq_off, a.seq_len = seqs[0].data_ptr(), seqs[1].data_ptr()
+        a.short_only = 1 if short_only else 0
     a.dtype = dtype_code(qkv.dtype)
     a.B, a.S, a.H, a.hd = B, S, H, hd
     a.row_stride_b, a.row_stride_s = rsb, rss
@@ -389,10 +391,12 @@ def _attn_args(qkv: Tensor, B: int, S: int, H: int, hd: int, rsb: int, rss: int,
 def attention_fwd(qkv: Tensor, out: Tensor, *, B: int, S: int, H: int, hd: int, scale: float,
                   causal: bool = False, key_mask: Optional[Tensor] = None, lse: Optional[Tensor] = None,
                   drop: Dropout = NO_DROP, rsb: Optional[int] = None, rss: int = 1, seqs=None,
-                  alg_flops: Optional[float] = None) -> Tensor:
+                  alg_flops: Optional[float] = None, short_only: bool = False) -> Tensor:
     """seqs: (seq_off, seq_len) device int32 [B] — packed sequences (include/icap.h icap_attn_args).
+    short_only (packed): the caller guarantees every seq_len <= 32 — only the short-sequence pass is launched.
     alg_flops: algorithmic FLOPs of the launch (bench timing only; None: not timed)."""
-    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop, seqs)
+    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop, seqs,
+                   short_only)
     a.out, a.ld_out = out.data_ptr(), _ld(out)
     _timed("attn_fwd", f"B{B} S{S} H{H} hd{hd}{' packed' if seqs is not None else ''}", alg_flops,
            lambda: call("icap_attention_fwd", C.byref(a), _stream()))
@@ -402,9 +406,11 @@ def attention_fwd(qkv: Tensor, out: Tensor, *, B: int, S: int, H: int, hd: int, 
 def attention_bwd(qkv: Tensor, dout: Tensor, lse: Tensor, dqkv: Tensor, *, B: int, S: int, H: int, hd: int,
                   scale: float, causal: bool = False, key_mask: Optional[Tensor] = None, drop: Dropout = NO_DROP,
                   rsb: Optional[int] = None, rss: int = 1, out: Optional[Tensor] = None, seqs=None,
-                  alg_flops: Optional[float] = None) -> Tensor:
-    """out: the forward's O (optional; enables the transpose-free bf16 MFMA backward). seqs: as attention_fwd."""
-    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop, seqs)
+                  alg_flops: Optional[float] = None, short_only: bool = False) -> Tensor:
+    """out: the forward's O (optional; enables the transpose-free bf16 MFMA backward). seqs, short_only: as
+    attention_fwd."""
+    a = _attn_args(qkv, B, S, H, hd, S if rsb is None else rsb, rss, scale, causal, key_mask, lse, drop, seqs,
+                   short_only)
     if out is not None:
         a.out, a.ld_out = out.data_ptr(), _ld(out)
     a.dout, a.ld_dout = dout.data_ptr(), _ld(dout)

@@ -230,6 +230,10 @@ typedef struct {
   /* that packed row. lse and the dropout index keep the padded [B, H, S(, S)] numbering, so a packed and a   */
   /* padded call draw the same masks for the same (b, h, q, k).                                                */
   const int32_t* seq_off; const int32_t* seq_len;
+  /* packed only: 1 = the caller guarantees every seq_len[b] <= 32, so only the pass over short sequences runs   */
+  /* (the launch over S > 32 tokens is otherwise split into a short pass and a pass for the longer ones, whose  */
+  /* blocks the short sequences exit; a longer sequence under short_only = 1 would be left unwritten). 0 = both. */
+  int32_t short_only;
 } icap_attn_args;
 int icap_attention_fwd(const icap_attn_args* a, void* stream);
 int icap_attention_bwd(const icap_attn_args* a, void* stream);

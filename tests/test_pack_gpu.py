@@ -222,3 +222,61 @@ def test_ring_gemm_equals_tile_kernel(dev, N, K, epi, monkeypatch):
     if epi != "resid_drop":
         ref = A[:mlive].float() @ B.float().t()
         assert float((outs[0][:mlive].float() - ref).abs().max() / ref.abs().max()) < 1e-2
+
+
+def test_attention_short_only_equals_both_passes(dev):
+    """icap_attn_args.short_only: with every packed sequence <= 32 tokens in a launch of S = 65, the short pass alone
+    stores what the two passes store (the long pass only exits), forward and backward, bitwise."""
+    B, P, L, H, hd = 9, 15, 50, 12, 64
+    S, D = P + L, H * hd
+    _, mask, labels, _ = ragged_batch(B, L, 100, 99, 8, seed=5)
+    labels[:, 17:] = -100  # every caption's last target within the first 17 positions: sequences <= 15 + 16 = 31
+    mask[:, 18:] = 0
+    from icap.engine import max_seq_len
+    assert max_seq_len(labels, P) <= 32
+    so, sl, km = _pack_dev(B, P, L, mask, labels, dev)
+    g = torch.Generator().manual_seed(12)
+    qkv = torch.randn((B * S, 3 * D), generator=g).to(dev, torch.bfloat16)
+    dout = torch.randn((B * S, D), generator=g).to(dev, torch.bfloat16)
+    kw = dict(B=B, S=S, H=H, hd=hd, scale=hd ** -0.5, causal=True, key_mask=km, seqs=(so, sl))
+    res = []
+    for short in (False, True):
+        o = torch.zeros((B * S, D), dtype=torch.bfloat16, device=dev)
+        lse = torch.full((B * H * S,), 7.0, device=dev)
+        ops.attention_fwd(qkv, o, lse=lse, short_only=short, **kw)
+        d = torch.zeros_like(qkv)
+        ops.attention_bwd(qkv, dout, lse, d, out=o, short_only=short, **kw)
+        torch.cuda.synchronize()
+        res.append((o, lse, d))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_trainer_short_only_switches_graphs(dev, monkeypatch):
+    """The trainer takes short_only from each batch's labels and keys its captured graphs on it: a short batch, then
+    one with a sequence past 32 tokens, then the short one again (graph replay) give the losses of a trainer that
+    always launches both passes (ICAP_SHORT_ONLY=0), bitwise."""
+    import icap.engine as E
+    short = ragged_batch(6, 30, TINY_G.vocab_size, TINY_G.eos, TINY_M.embed_dim, seed=21)
+    ids, mask, labels, emb = short
+    labels[:, 12:] = -100
+    mask[:, 13:] = 0
+    long_ = ragged_batch(6, 30, TINY_G.vocab_size, TINY_G.eos, TINY_M.embed_dim, seed=22)
+    long_[2][0, :] = torch.arange(30) % TINY_G.vocab_size  # caption 0 has targets up to position 30
+    long_[1][0, :] = 1
+    out = {}
+    for flag in (True, False):
+        monkeypatch.setattr(E, "SHORT_ONLY", flag)
+        model = build(TINY_G, TINY_M, torch.float32, dev)
+        t = CaptionTrainer(model, 6, 30, lr=1e-3, num_training_steps=8, dropout=False, seed=5)
+        P = t.P
+        assert E.max_seq_len(labels, P) <= 32 and E.max_seq_len(long_[2], P) > 32
+        losses = []
+        for ids_, mask_, labels_, emb_ in (short, long_, short, long_, short):
+            t.load_batch(ids_.to(dev), mask_.to(dev), labels_.to(dev), emb_.to(dev))
+            t.micro_step(use_graph=True)
+            losses.append(t.last_loss.item())
+        out[flag] = losses
+        if flag:
+            assert {k[2] for k in t.graphs} == {True, False}
+    assert out[True] == out[False], out
