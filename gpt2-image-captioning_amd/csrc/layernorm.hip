@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int64_t rows, int D, const 
 // grid (ceil(D/64), 2): blockIdx.y selects dgamma / dbeta; 16 waves split the partial rows (fixed order, so the
 // result is deterministic), 64 lanes = 64 columns
 __global__ __launch_bounds__(1024) void ln_param_reduce(int nblk, int D, const float* __restrict__ partial,
-                                                       float* dgamma, float* dbeta) {
+                                                       float* dgamma, float* dbeta, int acc) {
   __shared__ float red[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(1024) void ln_param_reduce(int nblk, int D, const f
 #pragma unroll
     for (int k = 0; k < 16; ++k) s += red[k][tx];
     float* dst = which ? dbeta : dgamma;
-    if (dst) dst[c] += s;
+    if (dst) dst[c] = acc ? dst[c] + s : s;
   }
 }
 
@@ -463,7 +463,7 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
                                   void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
                                   uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
                                   void* workspace, const int32_t* dy_rowmap, const int32_t* rows_dev,
-                                  void* stream) {
+                                  int32_t param_accumulate, void* stream) {
   ICAP_REQUIRE(x && gamma && mean && rstd && dy && dx, "icap_layernorm_bwd: null pointer");
   const bool wide8 = ln8_ok(dtype, D, x, ldx) && ln8_ok(dtype, D, dy, lddy) && ln8_ok(dtype, D, dx, lddx) &&
                      (dres == nullptr || ln8_ok(dtype, D, dres, lddres)) &&
@@ -508,6 +508,6 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
   int rc = check_launch("icap_layernorm_bwd");
   if (rc != ICAP_OK || !want_params) return rc;
   hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 63) / 64), 2), dim3(1024), 0, s, nb, (int)D, partial,
-                     dgamma, dbeta);
+                     dgamma, dbeta, param_accumulate ? 1 : 0);
   return check_launch("icap_layernorm_bwd(reduce)");
 }

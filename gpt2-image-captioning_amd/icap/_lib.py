@@ -121,7 +121,7 @@ SIGNATURES = {
     "icap_layernorm_fwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, f32, vp, i64, vp, vp, vp, vp, vp]),
     "icap_layernorm_bwd_workspace_bytes": (sz, [i64, i64]),
     "icap_layernorm_bwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, vp,
-                                     f32, u64, u64, vp, vp, vp, vp, vp, vp, vp]),
+                                     f32, u64, u64, vp, vp, vp, vp, vp, vp, i32, vp]),
     "icap_attention_fwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_bwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_decode": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, i64, f32, vp]),

@@ -23,6 +23,10 @@ from .models import _embedding_grads
 # packed attention launches skip their long-sequence pass when every sequence of the batch is short (set per batch in
 # load_batch); ICAP_SHORT_ONLY=0 always launches both passes (A/B)
 SHORT_ONLY = os.environ.get("ICAP_SHORT_ONLY", "1") != "0"
+# the first micro-batch of an accumulation cycle writes the trained mapper's gradients (each is produced once per
+# micro-batch) instead of zeroing the flat gradient buffer and accumulating into it; ICAP_GRAD_OVERWRITE=0 restores
+# the zero_() + accumulate form (A/B)
+GRAD_OVERWRITE = os.environ.get("ICAP_GRAD_OVERWRITE", "1") != "0"
 
 Tensor = torch.Tensor
 
@@ -200,7 +204,8 @@ class CaptionTrainer:
         if isinstance(mc, TransformerMapperCore):
             # the side stream joins at each layer step's end only when the steps are data-parallel buckets
             steps = mc.backward_steps(self.mws, self.emb_c, self.mdr, self.mgrads, self.dwh, side=self._side,
-                                      join_each=self.world > 1 or self.force_overlap)
+                                      join_each=self.world > 1 or self.force_overlap,
+                                      overwrite=zero and self._overwrite_ok())
             for (_, _, fn), rng in zip(steps, self._ranges_mapper):
                 segs.append((rng, fn))
         else:
@@ -220,11 +225,18 @@ class CaptionTrainer:
         segs[-1] = (last_rng, last)
         return segs
 
+    def _overwrite_ok(self) -> bool:
+        """Every flat-gradient element is written exactly once per micro-batch (transformer mapper + optional task
+        prefix; GPT-2 frozen — its trained form accumulates several products into the tied wte gradient), so a new
+        cycle can overwrite instead of zeroing the 243 MB buffer first (the alignment gaps between tensors stay zero
+        from allocation: nothing writes them)."""
+        return GRAD_OVERWRITE and isinstance(self.mcore, TransformerMapperCore) and not self.gpt_trainable
+
     def _front(self, zero: bool, grad_scale: float):
         """Forward, LM head + CE, GPT-2 backward and the mapper's output gradient; returns d(inputs_embeds)."""
         B, P, D = self.B, self.P, self.gcore.D
         model = self.model
-        if zero:
+        if zero and not self._overwrite_ok():
             self.flat.flat_grad.zero_()
         if self.clip is not None:
             emb = self.clip.run(self.cws, self.pixels)
@@ -252,7 +264,7 @@ class CaptionTrainer:
         Pm = mc.P
         if model.task_prefix_embeds is not None:
             ops.colsum(d_emb.view(B, S * D)[:, Pm * D: P * D], self.task_grad.view(-1), self.dwh.cs_ws,
-                       accumulate=True, M=B, N=(P - Pm) * D)
+                       accumulate=not (zero and self._overwrite_ok()), M=B, N=(P - Pm) * D)
         if isinstance(mc, TransformerMapperCore):
             Hl, Sm = mc.Hl, mc.S
             ops.convert(d_pre[:, : Pm * D], self.mws.dout.view(B, Sm * D)[:, Hl * D:])

@@ -72,28 +72,30 @@ class DWHelper:
         return dst
 
     def dW(self, dY: Tensor, X: Tensor, out: Tensor, M: int, N: Optional[int] = None, K: Optional[int] = None,
-           transpose_out: bool = False) -> None:
+           transpose_out: bool = False, accumulate: bool = True) -> None:
+        """accumulate=False overwrites out (the first micro-batch of a cycle: beta 0, no read of the old value)."""
         N = dY.shape[1] if N is None else N
         K = X.shape[1] if K is None else K
+        beta = 1.0 if accumulate else 0.0
         if self.dtype == torch.bfloat16 and _kout_ok(dY) and _kout_ok(X):
             # bf16: one K-outer GEMM reads dY and X in place (icap_gemm_args.trans_ab), no transposes
             if transpose_out:
-                ops.gemm(X, dY, out, beta=1.0, M=K, N=N, K=M, trans_ab=True, split_k=self.split_k)
+                ops.gemm(X, dY, out, beta=beta, M=K, N=N, K=M, trans_ab=True, split_k=self.split_k)
             else:
-                ops.gemm(dY, X, out, beta=1.0, M=N, N=K, K=M, trans_ab=True, split_k=self.split_k)
+                ops.gemm(dY, X, out, beta=beta, M=N, N=K, K=M, trans_ab=True, split_k=self.split_k)
             return
         Mp = _rup(M, 64)
         a = self._t(self.tA, dY, M, N, Mp)  # [N][Mp]
         b = self._t(self.tB, X, M, K, Mp)   # [K][Mp]
         if transpose_out:  # out[K,N] (HF Conv1D grad layout)
-            ops.gemm(b, a, out, beta=1.0, M=K, N=N, K=Mp, alg_flops=2.0 * M * N * K)
+            ops.gemm(b, a, out, beta=beta, M=K, N=N, K=Mp, alg_flops=2.0 * M * N * K)
         else:              # out[N,K] (nn.Linear grad layout)
-            ops.gemm(a, b, out, beta=1.0, M=N, N=K, K=Mp, alg_flops=2.0 * M * N * K)
+            ops.gemm(a, b, out, beta=beta, M=N, N=K, K=Mp, alg_flops=2.0 * M * N * K)
 
-    def db(self, dY: Tensor, out: Tensor, M: int, N: Optional[int] = None) -> None:
-        ops.colsum(dY, out, self.cs_ws, accumulate=True, M=M, N=N)
+    def db(self, dY: Tensor, out: Tensor, M: int, N: Optional[int] = None, accumulate: bool = True) -> None:
+        ops.colsum(dY, out, self.cs_ws, accumulate=accumulate, M=M, N=N)
 
-    def db_batch(self, items, M: int) -> None:
+    def db_batch(self, items, M: int, accumulate: bool = True) -> None:
         """db += colsum(dY) for every (dY, db) over the same M rows: two launches (icap_colsum_batch) instead of
         two per item; bitwise what db() gives. The workspace holds colsum_cols columns of partials: a call with
         more columns runs in column groups that fit."""
@@ -101,12 +103,12 @@ class DWHelper:
         for dy, out in items:
             n = dy.shape[1]
             if group and cols + n > self.cs_cols:
-                ops.colsum_batch(group, M, self.cs_ws)
+                ops.colsum_batch(group, M, self.cs_ws, accumulate=accumulate)
                 group, cols = [], 0
             group.append((dy, out, None))
             cols += n
         if group:
-            ops.colsum_batch(group, M, self.cs_ws)
+            ops.colsum_batch(group, M, self.cs_ws, accumulate=accumulate)
 
 
 # --------------------------------------------------------------------------- modules (reference names)
@@ -402,12 +404,14 @@ class TransformerMapperCore:
         return ws.out.view(-1)[self.Hl * self.D:], self.S * self.D
 
     # -- backward --------------------------------------------------------------------------------------------
-    def backward(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper, side=None) -> None:
-        """Consumes ws.dout (d of the forward output, rows t<Hl zero); accumulates every parameter grad."""
-        for _, _, fn in self.backward_steps(ws, emb_c, dr, g, dwh, side=side, join_each=False):
+    def backward(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper, side=None, overwrite: bool = False) -> None:
+        """Consumes ws.dout (d of the forward output, rows t<Hl zero); accumulates every parameter grad (writes
+        it, with overwrite)."""
+        for _, _, fn in self.backward_steps(ws, emb_c, dr, g, dwh, side=side, join_each=False, overwrite=overwrite):
             fn()
 
-    def backward_steps(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper, side=None, join_each: bool = True):
+    def backward_steps(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper, side=None, join_each: bool = True,
+                       overwrite: bool = False):
         """The backward as [(name, module, fn)]: one step per layer (the top layer first), then the input
         projection ("head": linear + prefix_const). Run in order they are backward(); each step finalises the
         grads of its module's parameters, which is what engine.CaptionTrainer's data-parallel all-reduce buckets
@@ -418,8 +422,12 @@ class TransformerMapperCore:
         written once per step (ws.g_*), so a product only has to be ordered after its producer (the fork); the
         main stream joins the side stream at the end of each layer step (join_each: the data-parallel buckets are
         final when their step ends) or only before the head step. Each gradient is the same kernel on the same
-        operands as the serial schedule: bitwise the same result."""
+        operands as the serial schedule: bitwise the same result.
+        overwrite: every parameter gradient is produced exactly once by these steps, so the first micro-batch of an
+        accumulation cycle WRITES them (dW beta 0, column sums and LayerNorm parameter sums stored, not added) and
+        the trainer skips zeroing the flat gradient buffer first; the stored values equal 0 + the sum bitwise."""
         B, M, S, D, Hl, P = ws.B, ws.M, self.S, self.D, self.Hl, self.P
+        acc = not overwrite
         scale = 1.0 / math.sqrt(self.hd)
         st = SimpleNamespace()
 
@@ -438,7 +446,7 @@ class TransformerMapperCore:
             dy is a per-layer buffer, alive until the step ends). With a side stream the dW runs there, behind
             everything queued on the main stream."""
             if side is None:
-                dwh.dW(dy, x, w_out, M=M)
+                dwh.dW(dy, x, w_out, M=M, accumulate=acc)
                 st.db.append((dy, b_out))
                 return
             main = torch.cuda.current_stream()
@@ -448,7 +456,7 @@ class TransformerMapperCore:
                     w_out = _scratch(w_out)
                     b_out = _scratch(b_out)
                 if _SIDE_DIAG != "no_dw":
-                    dwh.dW(dy, x, w_out, M=M)
+                    dwh.dW(dy, x, w_out, M=M, accumulate=acc)
             if _SIDE_DIAG != "no_db":
                 st.db.append((dy, b_out))
             if _SIDE_SERIAL:  # diagnostic: the side stream, but joined after every fork (no concurrency)
@@ -460,13 +468,13 @@ class TransformerMapperCore:
                 return
             if not _DB_BATCH:
                 for dy, b_out in st.db:
-                    dwh.db(dy, b_out, M=M)
+                    dwh.db(dy, b_out, M=M, accumulate=acc)
             elif side is None:
-                dwh.db_batch(st.db, M)
+                dwh.db_batch(st.db, M, accumulate=acc)
             else:
                 order(side, torch.cuda.current_stream())
                 with torch.cuda.stream(side):
-                    dwh.db_batch(st.db, M)
+                    dwh.db_batch(st.db, M, accumulate=acc)
             st.db = []
 
         def layer(l):
@@ -487,7 +495,7 @@ class TransformerMapperCore:
             d1 = dr.d1(l)
             ops.layernorm_bwd(ws.h1[l], w.n2_g, ws.mean2[l], ws.rstd2[l], ws.da, ws.g_rm[l], dres=r,
                               dx_drop=ws.g_mm[l] if d1.p > 0 else None, drop=d1, dgamma=gl.n2_g, dbeta=gl.n2_b,
-                              workspace=dwh.ln_ws)
+                              workspace=dwh.ln_ws, param_accumulate=acc)
             dy2 = ws.g_mm[l] if d1.p > 0 else ws.g_rm[l]
             wgrad(dy2, ws.o[l], gl.out_w, gl.out_b)
             ops.gemm(dy2, w.out_wt, ws.do)
@@ -499,7 +507,7 @@ class TransformerMapperCore:
             out = ws.g_r[l - 1] if l > 0 else ws.dres  # d(layer input): the next layer's residual grad / the head's
             ops.layernorm_bwd(ws.x[l], w.n1_g, ws.mean1[l], ws.rstd1[l], ws.da, out, dres=ws.g_rm[l],
                               dx_drop=ws.g_m[l - 1] if (l > 0 and nxt.p > 0) else None, drop=nxt, dgamma=gl.n1_g,
-                              dbeta=gl.n1_b, workspace=dwh.ln_ws)
+                              dbeta=gl.n1_b, workspace=dwh.ln_ws, param_accumulate=acc)
             st.r = out
             flush_db()
             if side is not None and (join_each or l == 0):  # the layer's grads are final when its step ends
@@ -509,10 +517,10 @@ class TransformerMapperCore:
             # x0 = [linear(emb) ; prefix_const]
             dres = st.r
             d_lin = dres.view(B, S * D)[:, : Hl * D]
-            dwh.dW(d_lin, emb_c, g.lin_w, M=B)
-            dwh.db(d_lin, g.lin_b, M=B)
+            dwh.dW(d_lin, emb_c, g.lin_w, M=B, accumulate=acc)
+            dwh.db(d_lin, g.lin_b, M=B, accumulate=acc)
             d_pc = dres.view(B, S * D)[:, Hl * D:]
-            ops.colsum(d_pc, g.prefix_const.view(-1), dwh.cs_ws, accumulate=True, M=B, N=P * D)
+            ops.colsum(d_pc, g.prefix_const.view(-1), dwh.cs_ws, accumulate=acc, M=B, N=P * D)
 
         m = self.m
         steps = [(f"layer{l}", m.transformer.layers[l], (lambda l=l: layer(l))) for l in reversed(range(self.nl))]

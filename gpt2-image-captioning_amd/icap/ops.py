@@ -358,14 +358,16 @@ def layernorm_bwd(x: Tensor, gamma: Tensor, mean: Tensor, rstd: Tensor, dy: Tens
                   dres: Optional[Tensor] = None, dx_drop: Optional[Tensor] = None, drop: Dropout = NO_DROP,
                   dgamma: Optional[Tensor] = None, dbeta: Optional[Tensor] = None,
                   workspace: Optional[Tensor] = None, rows: Optional[int] = None,
-                  dy_rowmap: Optional[Tensor] = None, rows_dev: Optional[Tensor] = None) -> Tensor:
-    """dy_rowmap: int32 [rows]; dy of row r is dy row dy_rowmap[r] (zero when < 0). rows_dev: as layernorm_fwd."""
+                  dy_rowmap: Optional[Tensor] = None, rows_dev: Optional[Tensor] = None,
+                  param_accumulate: bool = True) -> Tensor:
+    """dy_rowmap: int32 [rows]; dy of row r is dy row dy_rowmap[r] (zero when < 0). rows_dev: as layernorm_fwd.
+    param_accumulate: dgamma / dbeta += (True) or = (False: the first micro-batch of a cycle)."""
     rows = _rows(x) if rows is None else rows
     D = gamma.shape[0]
     call("icap_layernorm_bwd", dtype_code(x.dtype), rows, D, x.data_ptr(), _ld(x), gamma.data_ptr(),
          mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), _ld(dy), _p(dres), _ld(dres) if dres is not None else 0,
          dx.data_ptr(), _ld(dx), _p(dx_drop), drop.p, drop.seed, drop.offset, drop.ptr, _p(dgamma), _p(dbeta),
-         _p(workspace), _p(dy_rowmap), _p(rows_dev), _stream())
+         _p(workspace), _p(dy_rowmap), _p(rows_dev), 1 if param_accumulate else 0, _stream())
     return dx
 
 

@@ -80,7 +80,7 @@ def accesses(name, args):
                 ("y_rowmap", ymap, rows * 4), ("rows_dev", rdev, 4)]
     elif name == "icap_layernorm_bwd":
         (dt, rows, D, x, ldx, gm, mean, rstd, dy, lddy, dres, lddres, dx, lddx, dxd, _p, _sd, _o, sp, dg, db, ws,
-         dymap, rdev, _s) = a
+         dymap, rdev, _acc, _s) = a
         es = ES[dt]
         dyrows = 1 if dymap else rows  # row map: compacted slots (see layernorm_fwd)
         out += [("x", x, _rows(rows, ldx, D, es)), ("gamma", gm, D * 4), ("mean", mean, rows * 4),
