@@ -157,31 +157,41 @@ __global__ __launch_bounds__(1024) void caption_pack_kernel(int B, int P, int L,
                                                            int32_t* lab_shift, int32_t* n_valid, int32_t* row_slot,
                                                            int32_t* lab_c) {
   __shared__ int wsum[16];
+  constexpr int PK_LDS = 2048;                   // sequences whose offsets / lengths phase 2 reads from LDS
+  __shared__ int s_off[PK_LDS], s_len[PK_LDS];
   const int S = P + L, n = B * S;
   auto label_at = [&](int b, int t) {  // shifted label of position t of sequence b
     const int tn = t + 1;
     return (tn < S && tn >= P && labels) ? (int)labels[(int64_t)b * L + tn - P] : -100;
   };
-  // phase 1: lengths + offsets
+  // phase 1: lengths + offsets. The last target of a sequence is found by one pass over all its positions whose
+  // loads do not depend on each other (a backwards scan with an early exit made each label load wait for the one
+  // before it: ~50 dependent round trips per caption, the kernel took ~34 us)
   const int bper = (B + 1023) / 1024;
   const int b0 = threadIdx.x * bper < B ? threadIdx.x * bper : B;
   const int b1 = b0 + bper < B ? b0 + bper : B;
   int cnt = 0;
   for (int b = b0; b < b1; ++b) {
     int len = P;
-    for (int t = S - 1; t >= P; --t)
-      if (label_at(b, t) != -100) { len = t + 1; break; }
+#pragma unroll 8
+    for (int t = P; t < S; ++t)
+      if (label_at(b, t) != -100) len = t + 1;
     seq_len[b] = len;
+    if (b < PK_LDS) s_len[b] = len;
     cnt += len;
   }
   int mtot = 0;
   int off = block_excl_scan1024(cnt, wsum, mtot);
   for (int b = b0; b < b1; ++b) {
     seq_off[b] = off;
-    off += seq_len[b];
+    if (b < PK_LDS) s_off[b] = off;
+    off += b < PK_LDS ? s_len[b] : seq_len[b];
   }
   if (threadIdx.x == 0) *m_live = mtot;
-  __syncthreads();  // seq_off / seq_len visible to the whole block
+  __syncthreads();  // seq_off / seq_len (and their LDS copies) visible to the whole block
+  const bool lds = B <= PK_LDS;
+  auto OFF = [&](int b) { return lds ? s_off[b] : seq_off[b]; };
+  auto LEN = [&](int b) { return lds ? s_len[b] : seq_len[b]; };
   // phase 2: per packed row
   const int per = (n + 1023) / 1024;
   const int i0 = threadIdx.x * per < n ? threadIdx.x * per : n;
@@ -192,7 +202,7 @@ __global__ __launch_bounds__(1024) void caption_pack_kernel(int B, int P, int L,
     int lo = 0, hi = B - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (seq_off[mid] <= i0) lo = mid; else hi = mid - 1;
+      if (OFF(mid) <= i0) lo = mid; else hi = mid - 1;
     }
     bb = lo;
   }
@@ -202,8 +212,8 @@ __global__ __launch_bounds__(1024) void caption_pack_kernel(int B, int P, int L,
     for (int i = i0; i < i1; ++i) {
       int lab = -100, km = 0;
       if (i < mtot) {
-        while (i >= seq_off[b] + seq_len[b]) ++b;  // skips empty sequences too
-        const int t = i - seq_off[b];
+        while (i >= OFF(b) + LEN(b)) ++b;  // skips empty sequences too
+        const int t = i - OFF(b);
         km = (t < P || mask == nullptr) ? 1 : (mask[(int64_t)b * L + t - P] != 0 ? 1 : 0);
         lab = label_at(b, t);
       }
