@@ -18,7 +18,8 @@ rc=$?; tail -1 $O/bench.json | cut -c1-400; [ $rc -eq 0 ] || { tail -5 $O/bench.
 cd /tmp; export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/p -o run -- python3 $R/bench.py --steps 8 --warmup 3 --no-decode --no-cpu-baseline --sweep "" > $O/prof_bench.json 2> $O/prof.err
 rc=$?; [ $rc -eq 0 ] || { tail -5 $O/prof.err; exit $rc; }
-cd $R && python tools/kstats.py $O/p/run_results.db "whole 'bench.py --steps 8 --warmup 3 --no-decode --sweep \"\"' run: model build (one-time: the fp32 GEMMs are the LayerNorm folds of the frozen weights, 96 launches), then the packed train step x 12 (3 warm-up + 8 timed + 1 eager roofline pass)" > $O/kstats.txt && head -14 $O/kstats.txt | cut -c1-150
+cd $R && python tools/kstats.py $O/p/run_results.db "the 8 timed train steps of 'bench.py --steps 8 --warmup 3 --no-decode --sweep \"\"' (packed B = 128, graph replay): kernels between the end of the 3rd and the 11th optimizer launch" --window adam_update_kernel 3 8 > $O/kstats.txt && head -16 $O/kstats.txt | cut -c1-150
+python tools/kstats.py $O/p/run_results.db "whole 'bench.py --steps 8 --warmup 3 --no-decode --sweep \"\"' run: model build (one-time: the fp32 GEMMs are the LayerNorm folds of the frozen weights), then the packed train step x 12 (3 warm-up + 8 timed + 1 eager roofline pass)" > $O/kstats_run.txt
 rm -rf $O/p
 if [ -z "$SKIP_DIAG" ]; then
   timeout -k 10 300 python -u tools/gemm_diag.py > $O/gemm_diag.txt 2>&1 || { tail -5 $O/gemm_diag.txt; exit 1; }
