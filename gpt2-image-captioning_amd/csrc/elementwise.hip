@@ -452,6 +452,30 @@ __global__ __launch_bounds__(256) void sqnorm_partial_kernel(int64_t n, const fl
   if (threadIdx.x == 0) partial[blockIdx.x] = a;
 }
 
+// U strips per pass with every load issued before the first accumulate; a thread adds its elements in the same order
+// as the one-strip loop (i0, i0 + S, i0 + 2S, ... for the same grid), so the partials are bitwise the same
+template <int U>
+__global__ __launch_bounds__(256) void sqnorm_partial_u_kernel(int64_t n, const float* __restrict__ x,
+                                                              float* partial) {
+  __shared__ float red[4];
+  float a = 0.f;
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += stride * U) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = i0 + u * stride < n4 ? x4[i0 + u * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * stride < n4) a += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += 256) a += x[i] * x[i];
+  a = block_sum256(a, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = a;
+}
+
 struct AdamState {  // 64-byte device state, see icap.h
   int64_t step;
   float norm, clip, lr, step_size, bc2_sqrt, decay;
@@ -1380,7 +1404,11 @@ extern "C" size_t icap_adamw_workspace_bytes(int64_t n) {
 
 static int sq_partials(int64_t n, const float* x, float* partial, hipStream_t s, int* nparts) {
   const int nb = (int)nblk(n / 4 + 1, 256, SQ_BLOCKS);
-  hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, s, n, x, partial);
+  const char* eu = getenv("ICAP_SQ_U");  // (A/B) strips per pass; the grid, and so the partials, stay the same
+  const int u = eu ? atoi(eu) : 1;
+  if (u == 2) hipLaunchKernelGGL(sqnorm_partial_u_kernel<2>, dim3(nb), dim3(256), 0, s, n, x, partial);
+  else if (u == 4) hipLaunchKernelGGL(sqnorm_partial_u_kernel<4>, dim3(nb), dim3(256), 0, s, n, x, partial);
+  else hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, s, n, x, partial);
   *nparts = nb;
   return check_launch("sqnorm");
 }

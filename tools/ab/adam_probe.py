@@ -1,6 +1,7 @@
 """AdamW update variants on the headline's flat buffer (n = trainable params of the packed B = 128 step, fp32 params /
 grads / moments + the bf16 compute copy): the one-strip kernel against ICAP_ADAM_U strips per thread and
-non-temporal stores (ICAP_ADAM_NT), bitwise-checked against it, each timed as a HIP graph of REPS updates.
+non-temporal stores (ICAP_ADAM_NT), bitwise-checked against it, each timed as a HIP graph of REPS updates;
+then the gradient-norm pass alone with ICAP_SQ_U strips per pass.
 
     python tools/ab/adam_probe.py
 """
@@ -57,6 +58,32 @@ def main():
         gb = n * (4 * 4 + 3 * 4 + 2 + 4) / 1e9  # update: p g m v in, p m v + bf16 out; + the norm pass over g
         print(f"U={u} NT={nt}{'':10s} {us:8.1f} {gb:6.2f} {gb / us * 1e3:6.2f}  {same}", flush=True)
         del gph
+    os.environ.pop("ICAP_ADAM_U"), os.environ.pop("ICAP_ADAM_NT")
+    # the gradient norm pass alone (icap_sqnorm: partials + the fp64 finalize), ICAP_SQ_U strips per pass
+    out = torch.zeros(1, device=dev)
+    ref = None
+    for u in ("1", "2", "4"):
+        os.environ["ICAP_SQ_U"] = u
+        ops.sqnorm(gr, out, ws)
+        torch.cuda.synchronize()
+        val = out.clone()
+        ref = val if ref is None else ref
+        gph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gph):
+            for _ in range(reps):
+                ops.sqnorm(gr, out, ws)
+        gph.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        gph.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        print(f"sqnorm ICAP_SQ_U={u}{'':5s} {us:8.1f} {n * 4 / 1e9:6.2f} {n * 4 / us / 1e3:6.2f}  {torch.equal(val, ref)}",
+              flush=True)
+        del gph
+    os.environ.pop("ICAP_SQ_U")
 
 
 if __name__ == "__main__":
