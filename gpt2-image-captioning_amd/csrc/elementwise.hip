@@ -452,30 +452,6 @@ __global__ __launch_bounds__(256) void sqnorm_partial_kernel(int64_t n, const fl
   if (threadIdx.x == 0) partial[blockIdx.x] = a;
 }
 
-// U strips per pass with every load issued before the first accumulate; a thread adds its elements in the same order
-// as the one-strip loop (i0, i0 + S, i0 + 2S, ... for the same grid), so the partials are bitwise the same
-template <int U>
-__global__ __launch_bounds__(256) void sqnorm_partial_u_kernel(int64_t n, const float* __restrict__ x,
-                                                              float* partial) {
-  __shared__ float red[4];
-  float a = 0.f;
-  const int64_t n4 = n >> 2;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += stride * U) {
-    float4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = i0 + u * stride < n4 ? x4[i0 + u * stride] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (i0 + u * stride < n4) a += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
-  }
-  if (blockIdx.x == 0)
-    for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += 256) a += x[i] * x[i];
-  a = block_sum256(a, red);
-  if (threadIdx.x == 0) partial[blockIdx.x] = a;
-}
-
 struct AdamState {  // 64-byte device state, see icap.h
   int64_t step;
   float norm, clip, lr, step_size, bc2_sqrt, decay;
@@ -557,75 +533,6 @@ __global__ __launch_bounds__(256) void adam_update_kernel(int64_t n, float* __re
     if (out16) {
       const float o[4] = {p.x, p.y, p.z, p.w};
       io<bf16_t>::st4(out16 + 4 * i, o);
-    }
-  }
-  if (blockIdx.x == 0) {
-    for (int64_t i = 4 * n4 + threadIdx.x; i < n; i += 256) {
-      float p = P[i], m = M1[i], v = M2[i];
-      adam_one(p, G[i], m, v, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
-      P[i] = p; M1[i] = m; M2[i] = v;
-      if (out16) out16[i] = f2bf(p);
-    }
-  }
-}
-
-// U float4 strips per thread per pass (strip u of pass i at (i * U + u) * gridDim * 256 + thread: every wave
-// instruction stays one coalesced 1 KiB run), all 4U loads issued before the first update, so a thread keeps U times
-// the bytes in flight of the one-strip form; NT: the parameter / moment / bf16 stores as non-temporal (streamed
-// past the caches: nothing reads them again this step). Same per-element arithmetic as adam_update_kernel.
-typedef float adam_f4_t __attribute__((ext_vector_type(4)));
-typedef uint32_t adam_u2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void nt_store(float4* p, const float4 v) {
-  __builtin_nontemporal_store((adam_f4_t){v.x, v.y, v.z, v.w}, reinterpret_cast<adam_f4_t*>(p));
-}
-template <int U, bool NT>
-__global__ __launch_bounds__(256) void adam_update_u_kernel(int64_t n, float* __restrict__ P,
-                                                           const float* __restrict__ G, float* __restrict__ M1,
-                                                           float* __restrict__ M2, bf16_t* __restrict__ out16,
-                                                           const AdamState* __restrict__ st, float beta1, float beta2,
-                                                           float eps) {
-  const float clip = st->clip, decay = st->decay, step_size = st->step_size, bc2s = st->bc2_sqrt;
-  const float w1 = 1.f - beta1, w2 = 1.f - beta2;
-  const int64_t n4 = n >> 2;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  float4* P4 = reinterpret_cast<float4*>(P);
-  const float4* G4 = reinterpret_cast<const float4*>(G);
-  float4* M14 = reinterpret_cast<float4*>(M1);
-  float4* M24 = reinterpret_cast<float4*>(M2);
-  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n4; i0 += stride * U) {
-    float4 p[U], g[U], m[U], v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + u * stride;
-      if (i < n4) {
-        p[u] = P4[i];
-        g[u] = G4[i];
-        m[u] = M14[i];
-        v[u] = M24[i];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + u * stride;
-      if (i >= n4) continue;
-      adam_one(p[u].x, g[u].x, m[u].x, v[u].x, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
-      adam_one(p[u].y, g[u].y, m[u].y, v[u].y, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
-      adam_one(p[u].z, g[u].z, m[u].z, v[u].z, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
-      adam_one(p[u].w, g[u].w, m[u].w, v[u].w, clip, decay, w1, beta2, w2, step_size, bc2s, eps);
-      if constexpr (NT) {
-        nt_store(P4 + i, p[u]);
-        nt_store(M14 + i, m[u]);
-        nt_store(M24 + i, v[u]);
-      } else {
-        P4[i] = p[u];
-        M14[i] = m[u];
-        M24[i] = v[u];
-      }
-      if (out16) {
-        const uint2 o = make_uint2(f2bf2(p[u].x, p[u].y), f2bf2(p[u].z, p[u].w));  // = io<bf16_t>::st4
-        if constexpr (NT) __builtin_nontemporal_store((adam_u2_t){o.x, o.y}, reinterpret_cast<adam_u2_t*>(out16) + i);
-        else reinterpret_cast<uint2*>(out16)[i] = o;
-      }
     }
   }
   if (blockIdx.x == 0) {
@@ -1404,11 +1311,7 @@ extern "C" size_t icap_adamw_workspace_bytes(int64_t n) {
 
 static int sq_partials(int64_t n, const float* x, float* partial, hipStream_t s, int* nparts) {
   const int nb = (int)nblk(n / 4 + 1, 256, SQ_BLOCKS);
-  const char* eu = getenv("ICAP_SQ_U");  // (A/B) strips per pass; the grid, and so the partials, stay the same
-  const int u = eu ? atoi(eu) : 1;
-  if (u == 2) hipLaunchKernelGGL(sqnorm_partial_u_kernel<2>, dim3(nb), dim3(256), 0, s, n, x, partial);
-  else if (u == 4) hipLaunchKernelGGL(sqnorm_partial_u_kernel<4>, dim3(nb), dim3(256), 0, s, n, x, partial);
-  else hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, s, n, x, partial);
+  hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, s, n, x, partial);
   *nparts = nb;
   return check_launch("sqnorm");
 }
@@ -1444,24 +1347,9 @@ extern "C" int icap_adamw_step(const icap_adamw_args* a, void* workspace, void* 
                      a->num_training_steps);
   rc = check_launch("icap_adamw_step(finalize)");
   if (rc) return rc;
-  // (A/B) ICAP_ADAM_U = float4 strips per thread (1: the one-strip kernel), ICAP_ADAM_NT = non-temporal stores
-  // (read per call: a graph captures the launch it saw)
-  const char* eu = getenv("ICAP_ADAM_U");
-  const char* ent = getenv("ICAP_ADAM_NT");
-  const int au = eu ? atoi(eu) : 1, ant = ent ? atoi(ent) : 0;
-  const int64_t n4 = a->n / 4 + 1;
-#define ICAP_ADAM_U(U, NT)                                                                                          \
-  hipLaunchKernelGGL((adam_update_u_kernel<U, NT>), dim3(nblk((n4 + U - 1) / U, 256, 4096)), dim3(256), 0, s, a->n, \
-                     a->params, a->grads, a->exp_avg, a->exp_avg_sq, (bf16_t*)a->bf16_out,                         \
-                     (const AdamState*)a->state, a->beta1, a->beta2, a->eps)
-  if (au == 2) { if (ant) ICAP_ADAM_U(2, true); else ICAP_ADAM_U(2, false); }
-  else if (au == 4) { if (ant) ICAP_ADAM_U(4, true); else ICAP_ADAM_U(4, false); }
-  else if (ant) ICAP_ADAM_U(1, true);
-  else
-    hipLaunchKernelGGL(adam_update_kernel, dim3(nblk(n4, 256, 4096)), dim3(256), 0, s, a->n, a->params,
-                       a->grads, a->exp_avg, a->exp_avg_sq, (bf16_t*)a->bf16_out, (const AdamState*)a->state, a->beta1,
-                       a->beta2, a->eps);
-#undef ICAP_ADAM_U
+  hipLaunchKernelGGL(adam_update_kernel, dim3(nblk(a->n / 4 + 1, 256, 4096)), dim3(256), 0, s, a->n, a->params,
+                     a->grads, a->exp_avg, a->exp_avg_sq, (bf16_t*)a->bf16_out, (const AdamState*)a->state, a->beta1,
+                     a->beta2, a->eps);
   return check_launch("icap_adamw_step(update)");
 }
 
