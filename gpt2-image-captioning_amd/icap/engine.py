@@ -27,6 +27,9 @@ SHORT_ONLY = os.environ.get("ICAP_SHORT_ONLY", "1") != "0"
 # micro-batch) instead of zeroing the flat gradient buffer and accumulating into it; ICAP_GRAD_OVERWRITE=0 restores
 # the zero_() + accumulate form (A/B)
 GRAD_OVERWRITE = os.environ.get("ICAP_GRAD_OVERWRITE", "1") != "0"
+# the transformer mapper's dW products of a layer unsplit and side by side on four streams at the end of its backward
+# step (mapper.backward_steps group=) instead of split-K + reduce in series inside the step (A/B switch)
+GROUP_DW = os.environ.get("ICAP_GROUP_DW", "0") == "1"
 
 Tensor = torch.Tensor
 
@@ -151,6 +154,14 @@ class CaptionTrainer:
                 and os.environ.get("ICAP_SIDE_DW", "0") == "1"):
             self._side = torch.cuda.Stream(self.dev)
             ops.register_side_stream(self._side)
+        # the mapper's four dW products of a layer unsplit and side by side on three more streams (mapper.
+        # backward_steps group=): ICAP_GROUP_DW
+        self._group = None
+        if (self.dev.type == "cuda" and isinstance(self.mcore, TransformerMapperCore) and self._side is None
+                and GROUP_DW and self.dtype == torch.bfloat16):
+            self._group = [torch.cuda.Stream(self.dev) for _ in range(3)]
+            for sd in self._group:
+                ops.register_side_stream(sd)
 
     def share_state_with(self, other: "CaptionTrainer") -> None:
         """Use `other`'s optimizer step counter and dropout counter (same model, another batch shape)."""
@@ -205,7 +216,7 @@ class CaptionTrainer:
             # the side stream joins at each layer step's end only when the steps are data-parallel buckets
             steps = mc.backward_steps(self.mws, self.emb_c, self.mdr, self.mgrads, self.dwh, side=self._side,
                                       join_each=self.world > 1 or self.force_overlap,
-                                      overwrite=zero and self._overwrite_ok())
+                                      overwrite=zero and self._overwrite_ok(), group=self._group)
             for (_, _, fn), rng in zip(steps, self._ranges_mapper):
                 segs.append((rng, fn))
         else:

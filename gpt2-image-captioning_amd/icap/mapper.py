@@ -72,17 +72,19 @@ class DWHelper:
         return dst
 
     def dW(self, dY: Tensor, X: Tensor, out: Tensor, M: int, N: Optional[int] = None, K: Optional[int] = None,
-           transpose_out: bool = False, accumulate: bool = True) -> None:
-        """accumulate=False overwrites out (the first micro-batch of a cycle: beta 0, no read of the old value)."""
+           transpose_out: bool = False, accumulate: bool = True, split_k: Optional[int] = None) -> None:
+        """accumulate=False overwrites out (the first micro-batch of a cycle: beta 0, no read of the old value).
+        split_k: the K-outer product's split (None: this helper's setting; 1: unsplit, no slabs / reduce pass)."""
         N = dY.shape[1] if N is None else N
         K = X.shape[1] if K is None else K
         beta = 1.0 if accumulate else 0.0
+        sk = self.split_k if split_k is None else split_k
         if self.dtype == torch.bfloat16 and _kout_ok(dY) and _kout_ok(X):
             # bf16: one K-outer GEMM reads dY and X in place (icap_gemm_args.trans_ab), no transposes
             if transpose_out:
-                ops.gemm(X, dY, out, beta=beta, M=K, N=N, K=M, trans_ab=True, split_k=self.split_k)
+                ops.gemm(X, dY, out, beta=beta, M=K, N=N, K=M, trans_ab=True, split_k=sk)
             else:
-                ops.gemm(dY, X, out, beta=beta, M=N, N=K, K=M, trans_ab=True, split_k=self.split_k)
+                ops.gemm(dY, X, out, beta=beta, M=N, N=K, K=M, trans_ab=True, split_k=sk)
             return
         Mp = _rup(M, 64)
         a = self._t(self.tA, dY, M, N, Mp)  # [N][Mp]
@@ -411,7 +413,7 @@ class TransformerMapperCore:
             fn()
 
     def backward_steps(self, ws, emb_c: Tensor, dr, g, dwh: DWHelper, side=None, join_each: bool = True,
-                       overwrite: bool = False):
+                       overwrite: bool = False, group=None):
         """The backward as [(name, module, fn)]: one step per layer (the top layer first), then the input
         projection ("head": linear + prefix_const). Run in order they are backward(); each step finalises the
         grads of its module's parameters, which is what engine.CaptionTrainer's data-parallel all-reduce buckets
@@ -425,7 +427,12 @@ class TransformerMapperCore:
         operands as the serial schedule: bitwise the same result.
         overwrite: every parameter gradient is produced exactly once by these steps, so the first micro-batch of an
         accumulation cycle WRITES them (dW beta 0, column sums and LayerNorm parameter sums stored, not added) and
-        the trainer skips zeroing the flat gradient buffer first; the stored values equal 0 + the sum bitwise."""
+        the trainer skips zeroing the flat gradient buffer first; the stored values equal 0 + the sum bitwise.
+        group: side streams (ops.register_side_stream) for the grouped weight gradients: a layer's four K-outer dW
+        products are queued at the end of its step, unsplit (no slabs, no reduce pass), one on the main stream and
+        the others on these streams, and joined before the next layer's step starts — so they only ever run beside
+        each other (432 tiles at the mapper's shape instead of four split launches + reduces in series), never beside
+        the dX chain. Each product is one kernel on its own operands and output: deterministic."""
         B, M, S, D, Hl, P = ws.B, ws.M, self.S, self.D, self.Hl, self.P
         acc = not overwrite
         scale = 1.0 / math.sqrt(self.hd)
@@ -440,11 +447,16 @@ class TransformerMapperCore:
             ops.keep_event(ev)
 
         st.db = []
+        st.dw = []
 
         def wgrad(dy, x, w_out, b_out):
             """dW += dy^T x now; db += colsum(dy) is queued for the layer's one batched column sum (flush_db: every
             dy is a per-layer buffer, alive until the step ends). With a side stream the dW runs there, behind
             everything queued on the main stream."""
+            if side is None and group:
+                st.dw.append((dy, x, w_out))
+                st.db.append((dy, b_out))
+                return
             if side is None:
                 dwh.dW(dy, x, w_out, M=M, accumulate=acc)
                 st.db.append((dy, b_out))
@@ -461,6 +473,22 @@ class TransformerMapperCore:
                 st.db.append((dy, b_out))
             if _SIDE_SERIAL:  # diagnostic: the side stream, but joined after every fork (no concurrency)
                 order(main, side)
+
+        def flush_dw():
+            """The layer's queued dW products, unsplit and side by side (group streams forked from the main stream
+            first, so none of them waits for another), then joined back into the main stream."""
+            if not st.dw:
+                return
+            main = torch.cuda.current_stream()
+            sides = list(group[: len(st.dw) - 1])
+            for sd in sides:
+                order(sd, main)
+            for i, (dy, x, w_out) in enumerate(st.dw):
+                with torch.cuda.stream(main if i == 0 else sides[i - 1]):
+                    dwh.dW(dy, x, w_out, M=M, accumulate=acc, split_k=1)
+            for sd in sides:
+                order(main, sd)
+            st.dw = []
 
         def flush_db():
             """The layer's bias gradients in one icap_colsum_batch (2 launches instead of 2 per bias)."""
@@ -509,6 +537,7 @@ class TransformerMapperCore:
                               dx_drop=ws.g_m[l - 1] if (l > 0 and nxt.p > 0) else None, drop=nxt, dgamma=gl.n1_g,
                               dbeta=gl.n1_b, workspace=dwh.ln_ws, param_accumulate=acc)
             st.r = out
+            flush_dw()
             flush_db()
             if side is not None and (join_each or l == 0):  # the layer's grads are final when its step ends
                 order(torch.cuda.current_stream(), side)
