@@ -34,6 +34,23 @@ FP8_PEAK_TFLOPS = 5000.0  # dense MX fp8 (block-scaled 16x16x128 f8f6f4: 2x bf16
 HBM_PEAK_GBS = 8000.0
 
 
+_SLEEP_PER_MS = None
+
+
+def prequeue(ms: float) -> None:
+    """Queue a spin kernel (torch.cuda._sleep) of about `ms` milliseconds on the current stream (its rate is
+    calibrated once with HIP events)."""
+    global _SLEEP_PER_MS
+    if _SLEEP_PER_MS is None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.cuda._sleep(1 << 20)
+        e1.record()
+        torch.cuda.synchronize()
+        _SLEEP_PER_MS = (1 << 20) / max(e0.elapsed_time(e1), 1e-3)
+    torch.cuda._sleep(max(1, int(_SLEEP_PER_MS * ms)))
+
+
 class GemmTimer:
     """HIP-event timing of each GEMM launch on the launching stream (icap.ops.GEMM_TIMER hook)."""
 
@@ -485,14 +502,19 @@ def train_rate(trainer, B, steps, warmup, use_graph, world, dev, detail=False):
     torch.cuda.synchronize()
     te0 = time.perf_counter()
     segs = trainer._segments(True, trainer.grad_scale())
-    sev = [torch.cuda.Event(enable_timing=True) for _ in range(len(segs) + 1)]
+    sev = [torch.cuda.Event(enable_timing=True) for _ in range(len(segs) + 2)]
+    # a spin kernel queued first keeps the device behind the host for the whole eager pass, so no host launch gap
+    # enters the per-launch HIP events (the markers themselves remain: profiles/r04_bench_12836_prequeue.json)
+    prequeue(80.0)
     sev[0].record()
     for i, (rng, fn) in enumerate(segs):  # the data-parallel buckets' segments, timed (eager, with GEMM events)
         fn()
         sev[i + 1].record()
     trainer._optimizer()
+    sev[-1].record()
     torch.cuda.synchronize()
-    eager_ms = (time.perf_counter() - te0) * 1e3
+    host_ms = (time.perf_counter() - te0) * 1e3
+    eager_ms = sev[0].elapsed_time(sev[-1])  # device time of the eager step (kernels back to back)
     seg_ms = [round(sev[i].elapsed_time(sev[i + 1]), 3) for i in range(len(segs))]
     seg_bytes = [sum(hi - lo for lo, hi in rng) * 4 for rng, _ in segs]
     ops.GEMM_TIMER = None
@@ -505,7 +527,7 @@ def train_rate(trainer, B, steps, warmup, use_graph, world, dev, detail=False):
             "median_ms": median_ms, "rank_ms": rank_ms, "seg_ms": seg_ms, "seg_bytes": seg_bytes,
             "dom": dom, "n_l": n_l, "fl": fl, "ms": ms, "achieved": achieved,
             "frac": achieved / kernel_peak(dom), "gemm_ms": sum(v[2] for v in agg.values()),
-            "all_fl": sum(v[1] for v in agg.values()), "eager_ms": eager_ms,
+            "all_fl": sum(v[1] for v in agg.values()), "eager_ms": eager_ms, "eager_host_ms": host_ms,
             "block": {"launches": bn, "alg_tflop": round(bfl / 1e12, 4), "ms": round(bms, 3),
                       "achieved": round(bfl / (bms * 1e-3) / 1e12, 1) if bms else None,
                       "frac": round(bfl / (bms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, 4) if bms else None}}
@@ -743,6 +765,7 @@ def main():
                          "alg_gflop_per_launch": round(fl / n_l / 1e9, 3),
                          "all_gemm_ms_per_step": round(gemm_ms, 3), "all_gemm_tflop_per_step": round(all_fl / 1e12, 4),
                          "eager_step_ms": round(eager_ms, 3),
+                         "eager_step_host_ms": round(r["eager_host_ms"], 3),
                          "dp_segments": {"ms": r["seg_ms"], "grad_bytes": r["seg_bytes"],
                                          "what": "eager step cut at the data-parallel buckets (forward + GPT-2 "
                                                  "backward, then one per mapper layer top first, then the mapper "
@@ -753,7 +776,11 @@ def main():
                                                  "one eager step: summed algorithmic FLOPs (live rows) / summed "
                                                  "HIP-event time"),
                          "timing": "HIP events around every GEMM launch of one eager step on its launch stream "
-                                   "(the timed region replays a HIP graph, which cannot host per-kernel events)"},
+                                   "(the timed region replays a HIP graph, which cannot host per-kernel events); a "
+                                   "spin kernel queued ahead keeps the device behind the host for that pass, so no "
+                                   "host launch gap enters the events; eager_step_ms is that pass's device time, "
+                                   "eager_step_host_ms its wall time. The event markers between launches still cost "
+                                   "each launch a few us against the graph replay (DESIGN.md section 8(d))"},
         }
         if not args.no_cpu_baseline and world == 1 and args.config == "small":
             res["cpu_baseline"] = cpu_baseline()
