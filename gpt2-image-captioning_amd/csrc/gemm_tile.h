@@ -57,13 +57,18 @@ __device__ __forceinline__ int kout_off(int r, int ch) { return r * 256 + ((ch ^
 typedef short kv4s_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) kv4s_t* kout_lds_ptr;
 // MFMA 16x16x32 operand (lane: column c0 + (lane & 15)) over k-rows r0..r0+31 of a K-outer image, as two
-// ds_read_b64_tr_b16: lane 4q+p of 16-lane group g addresses row r0 + 4g + q (then + 16), columns 4p..4p+3 of
-// the 16-column block; element j of the result = k-row r0 + 4g + j (j < 4), r0 + 16 + 4g + j - 4 (j >= 4)
+// ds_read_b64_tr_b16: lane 4q+p of 16-lane group g addresses row r0 + kb(g) + q (then + 16), columns 4p..4p+3 of
+// the 16-column block, kb(g) = 8 (g & 1) + 4 (g >> 1); element j of the result = k-row r0 + kb(g) + j (j < 4),
+// r0 + 16 + kb(g) + j - 4 (j >= 4). The two 16-lane groups of a 32-lane half (g, g ^ 1) read blocks 8 rows apart
+// in the same columns, which the image's XOR makes conflict-free (cdna_hip_programming.md T10); with adjacent
+// blocks (kb = 4g) every read was 2-way (SQ_LDS_BANK_CONFLICT = 0.47 of the kernel's LDS cycles,
+// profiles/r04_pmc_lds.txt). Any k order works as long as both operands use the same one.
 __device__ __forceinline__ uint4 kout_frag(const char* img, int r0, int c0, int lane) {
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   const int ch = (c0 >> 3) + (pp >> 1), half = (pp & 1) * 8;
-  const char* a0 = img + kout_off(r0 + 4 * g + q, ch) + half;
-  const char* a1 = img + kout_off(r0 + 16 + 4 * g + q, ch) + half;
+  const int kb = 8 * (g & 1) + 4 * (g >> 1);
+  const char* a0 = img + kout_off(r0 + kb + q, ch) + half;
+  const char* a1 = img + kout_off(r0 + 16 + kb + q, ch) + half;
   const kv4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((kout_lds_ptr)(a0));
   const kv4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((kout_lds_ptr)(a1));
   uint4 r;
@@ -84,7 +89,7 @@ __device__ __forceinline__ uint4 kout_frag(const char* img, int r0, int c0, int 
 // KOUT: both operands K-outer (icap_gemm_args.trans_ab): A stored [K][lda] (m contiguous), B [K][ldb] — the dW
 // products dY^T X over token rows, read without transposing either. A stage is then 64 k-rows x 128 m (n)
 // columns, 256-byte LDS rows in the T10 (b) XOR image (cdna_hip_programming.md T10), written by LDS-DMA with the
-// swizzle on the source address; fragments come from ds_read_b64_tr_b16 pairs (k order {4g..4g+3, 16+4g..},
+// swizzle on the source address; fragments come from ds_read_b64_tr_b16 pairs (k order {kb..kb+3, 16+kb..},
 // the same on both operands, so the contraction is unchanged). bf16 inputs, 128 x 128 tiles only.
 // ACT: false for launches with no activation (act == dact == NONE: most of the step's products): the epilogue's
 // activation code is then not compiled into the kernel at all. Measured (profiles/r03_k768_counters.txt): with it
