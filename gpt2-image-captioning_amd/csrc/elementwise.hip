@@ -602,10 +602,13 @@ __device__ __forceinline__ void transpose16_tile(int64_t rows, int64_t cols, con
     t[1] = make_uint2(v.z, v.w);
   }
   __syncthreads();
+  // read phase: a wave takes one 8-row group rq of all 64 columns (lane = column), so its 16-bit LDS reads hit 32
+  // consecutive dwords (no bank conflict; 8 lanes per column at 8-row spacing were 4-way: 0.67 of the kernel's LDS
+  // cycles, profiles/r04_pmc_lds.txt); each lane still stores 16 contiguous bytes of its output row
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int idx = threadIdx.x + 256 * h;
-    const int c = idx >> 3, rq = idx & 7;
+    const int c = idx & 63, rq = idx >> 6;
     if (c0 + c >= cols) continue;
     uint32_t w[4];
 #pragma unroll
