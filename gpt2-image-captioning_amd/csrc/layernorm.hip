@@ -463,7 +463,7 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
                                   void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
                                   uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
                                   void* workspace, const int32_t* dy_rowmap, const int32_t* rows_dev,
-                                  int32_t param_accumulate, void* stream) {
+                                  int32_t param_overwrite, void* stream) {
   ICAP_REQUIRE(x && gamma && mean && rstd && dy && dx, "icap_layernorm_bwd: null pointer");
   const bool wide8 = ln8_ok(dtype, D, x, ldx) && ln8_ok(dtype, D, dy, lddy) && ln8_ok(dtype, D, dx, lddx) &&
                      (dres == nullptr || ln8_ok(dtype, D, dres, lddres)) &&
@@ -508,6 +508,6 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
   int rc = check_launch("icap_layernorm_bwd");
   if (rc != ICAP_OK || !want_params) return rc;
   hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 63) / 64), 2), dim3(1024), 0, s, nb, (int)D, partial,
-                     dgamma, dbeta, param_accumulate ? 1 : 0);
+                     dgamma, dbeta, param_overwrite ? 0 : 1);
   return check_launch("icap_layernorm_bwd(reduce)");
 }

@@ -192,7 +192,7 @@ class ClipCore:
         vm, dt = self.m.vision_model, self.dtype
         # bf16: layer_norm1 (layers >= 1) / layer_norm2 (all but the last) folded into the QKV / fc1 tile GEMMs, the row
         # statistics handed over from the producing GEMMs' epilogues (icap_gemm_args.ln_stats_out / ln_stats_in)
-        self.fold = dt == torch.bfloat16 and self.D % 32 == 0 and os.environ.get("ICAP_TRAIN_LN_FOLD", "1") != "0"
+        self.fold = dt == torch.bfloat16 and ops.ln_fold_ok(self.D) and TRAIN_LN_FOLD
         # [D, C*p*p] (c, ky, kx) order, zero-padded to the 8-multiple row of icap_im2col_patches (p = 14: 592)
         wp = vm.embeddings.patch_embedding.weight.data.reshape(self.D, -1)
         self.Kp = (wp.shape[1] + 7) // 8 * 8

@@ -446,9 +446,9 @@ class GPT2Core:
 
     def _fold_train(self, keep_for_dw: bool) -> bool:
         """Whether the forward folds ln_1 / ln_2 into the tile GEMMs: a frozen bf16 model (the folded weights exist),
-        not the fp8 path (its MX products have no LayerNorm epilogue), D % 32 == 0."""
+        not the fp8 path (its MX products have no LayerNorm epilogue), a width the hand-off supports (ops.ln_fold_ok)."""
         return (TRAIN_LN_FOLD and not keep_for_dw and self.dtype == torch.bfloat16 and not self.fp8
-                and self.D % 32 == 0 and bool(self.layers) and getattr(self.layers[0], "wf_attn_t", None) is not None)
+                and ops.ln_fold_ok(self.D) and bool(self.layers) and getattr(self.layers[0], "wf_attn_t", None) is not None)
 
     def _bmm(self, ws, A: Tensor, qA, W: Tensor, qW, out: Tensor, **kw) -> Tensor:
         """A block GEMM over the token rows: with packed rows only rows < m_live are computed (m_dev)."""

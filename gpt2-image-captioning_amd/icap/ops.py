@@ -248,6 +248,13 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     return out
 
 
+def ln_fold_ok(D: int) -> bool:
+    """The LayerNorm-statistics hand-off's shape rule (csrc/gemm.hip gemm_plan): the producer stores (mean, M2) per
+    32-column group (N % 32 == 0) and the consumer tile GEMM combines them in its prologue, K % 128 == 0 and
+    K <= 1280. A model whose width breaks it (e.g. GPT-2 XL's 1600, or 192) keeps the standalone LayerNorm launches."""
+    return D % 128 == 0 and D <= 1280
+
+
 GEMM_WORKSPACE_BYTES = 192 << 20  # split-K slabs up to splits*M*N fp32 (LM-head dX: 6 x 6400 x 768)
 GEMM_TICKETS = 1 << 16  # int32 per-tile counters of the in-launch split-K combine (2 per 128 x 128 tile)
 FUSED_SPLIT_K = os.environ.get("ICAP_FUSED_SPLIT_K", "1") != "0"  # 0: split-K always through a reduce pass (A/B)
@@ -367,7 +374,7 @@ def layernorm_bwd(x: Tensor, gamma: Tensor, mean: Tensor, rstd: Tensor, dy: Tens
     call("icap_layernorm_bwd", dtype_code(x.dtype), rows, D, x.data_ptr(), _ld(x), gamma.data_ptr(),
          mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), _ld(dy), _p(dres), _ld(dres) if dres is not None else 0,
          dx.data_ptr(), _ld(dx), _p(dx_drop), drop.p, drop.seed, drop.offset, drop.ptr, _p(dgamma), _p(dbeta),
-         _p(workspace), _p(dy_rowmap), _p(rows_dev), 1 if param_accumulate else 0, _stream())
+         _p(workspace), _p(dy_rowmap), _p(rows_dev), 0 if param_accumulate else 1, _stream())
     return dx
 
 

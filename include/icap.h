@@ -186,8 +186,8 @@ int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const void* x, in
                        void* stream);
 /* dx = LN'(x)^T dy [+ dres];  optional dx_drop = dx * dropmask(p,seed,offset)  */
 /* (the residual-dropout backward of the producing layer, fused);             */
-/* optional dgamma/dbeta (fp32 [D]: += when param_accumulate, = otherwise —   */
-/* the first micro-batch of a cycle overwrites instead of zeroing first) via a */
+/* optional dgamma/dbeta (fp32 [D]: += by default, = when param_overwrite != 0 */
+/* — the first micro-batch of a cycle overwrites instead of zeroing first) via a */
 /* caller workspace of icap_layernorm_bwd_workspace_bytes(rows, D) bytes.      */
 /* dy_rowmap (optional int32 [rows]): dy of row r is dy row dy_rowmap[r], or 0 */
 /* when it is < 0 (scatters the LM-head target-row gradient back).             */
@@ -199,7 +199,7 @@ int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const void* x, in
                        void* dx, int64_t lddx, void* dx_drop, float drop_p, uint64_t seed,
                        uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
                        void* workspace, const int32_t* dy_rowmap, const int32_t* rows_dev,
-                       int32_t param_accumulate, void* stream);
+                       int32_t param_overwrite, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Multi-head softmax attention over a fused QKV activation.                  */

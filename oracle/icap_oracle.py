@@ -791,7 +791,9 @@ def train_steps(gpt_sd, gcfg: GPT2Cfg, map_sd, mcfg: MapperCfg, batches, lr0: fl
     """The inner loop of src/train.py:119-166 with grad_accum_steps=1: forward, backward, clip, AdamW, schedule.
     p_drop > 0 runs the reference's train-mode dropout (GPT-2 embd/attn/resid, mapper; nondeterministic).
     clip=(clip_sd, ClipCfg): each batch's 4th element is pixels, embedded by the CLIP tower first (frozen,
-    src/embeddings/clip.py:132-137). Returns (losses, grad_norms, map_sd, gpt_sd) after len(batches) steps."""
+    src/embeddings/clip.py:132-137); clip=(dino_sd, DinoCfg): by the DINOv3 backbone's pooled CLS, L2-normalised
+    (src/embeddings/dino.py:173-179, BASELINE configs[4]).
+    Returns (losses, grad_norms, map_sd, gpt_sd) after len(batches) steps."""
     map_sd = {k: v.clone().requires_grad_(True) for k, v in map_sd.items()}
     gpt_sd = {k: v.clone().requires_grad_(not freeze_gpt) for k, v in gpt_sd.items()}
     st = AdamWState()
@@ -800,7 +802,8 @@ def train_steps(gpt_sd, gcfg: GPT2Cfg, map_sd, mcfg: MapperCfg, batches, lr0: fl
     for ids, mask, labels, emb in batches:
         if clip is not None:
             with torch.no_grad():
-                emb = clip_embed_normalized(clip[0], clip[1], emb)
+                embed = dinov3_embed_normalized if isinstance(clip[1], DinoCfg) else clip_embed_normalized
+                emb = embed(clip[0], clip[1], emb)
         prefix = mapper_forward(map_sd, mcfg, emb, train, p_drop)
         loss, _ = caption_forward(gpt_sd, gcfg, prefix, ids, mask, labels, train, p_drop)
         trainable = dict(map_sd)

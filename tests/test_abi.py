@@ -31,6 +31,91 @@ def test_header_functions_exported_and_bound():
     assert set(_lib.SIGNATURES) == set(names)
 
 
+# C scalar type in icap.h -> the ctypes class a binding must use (ctypes aliases: c_int is c_int32, c_long is
+# c_int64 and c_ulong is c_uint64 / c_size_t on this LP64 platform)
+_SCALARS = {"int": C.c_int, "int32_t": C.c_int32, "int64_t": C.c_int64, "uint64_t": C.c_uint64, "size_t": C.c_size_t,
+            "float": C.c_float}
+_STRUCTS = {"icap_gemm_args": _lib.GemmArgs, "icap_attn_args": _lib.AttnArgs, "icap_adamw_args": _lib.AdamWArgs,
+            "icap_beam_args": _lib.BeamArgs, "icap_transpose_item": _lib.TransposeItem,
+            "icap_colsum_item": _lib.ColsumItem}
+
+
+def header_prototypes():
+    """name -> (return type, [parameter type]) for every prototype of icap.h (comments stripped, whitespace
+    normalised, parameter names dropped)."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    out = {}
+    for ret, name, params in re.findall(r"([A-Za-z_][\w\s\*]*?)\b(icap_\w+)\s*\(([^)]*)\)\s*;", src):
+        ret = " ".join(ret.replace("*", " * ").split())
+        ps = []
+        for prm in params.split(","):
+            prm = " ".join(prm.replace("*", " * ").split())
+            if prm in ("", "void"):
+                continue
+            toks = prm.split()
+            ps.append(" ".join(toks[:-1]) if toks[-1] != "*" else prm)  # drop the parameter name
+        out[name] = (ret, ps)
+    return out
+
+
+def _ctype_ok(ctype: str, py) -> bool:
+    """Does ctypes class `py` bind C type `ctype` (pointers: c_void_p, or POINTER(the struct's class))?"""
+    t = ctype.replace("const ", "").strip()
+    if t.endswith("*"):
+        base = t[:-1].strip()
+        if base == "char":
+            return py in (C.c_char_p, C.c_void_p)
+        if base in _STRUCTS and py is C.POINTER(_STRUCTS[base]):
+            return True
+        return py is C.c_void_p
+    if t == "void":
+        return py is None
+    return py is _SCALARS[t]
+
+
+def test_signatures_match_header_prototypes():
+    """every binding has the header's arity and C types, so a parameter added to
+    icap.h without the binding (or the reverse) fails here instead of shifting the stream handle."""
+    protos = header_prototypes()
+    assert set(protos) == set(_lib.SIGNATURES)
+    for name, (ret, params) in protos.items():
+        res, args = _lib.SIGNATURES[name]
+        assert len(args) == len(params), f"{name}: header has {len(params)} parameters, binding {len(args)}"
+        assert _ctype_ok(ret, res), f"{name}: return {ret} bound as {res}"
+        for i, (ct, py) in enumerate(zip(params, args)):
+            assert _ctype_ok(ct, py), f"{name}: parameter {i} is {ct}, bound as {py}"
+
+
+def test_integration_snippets_match_header():
+    """The ctypes snippets in INTEGRATION.md run as written against the header: every `lib.icap_X.argtypes = [...]`
+    list has the prototype's arity and types, and every `lib.icap_X(...)` call passes that many arguments."""
+    import ast
+
+    protos = header_prototypes()
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    blocks = re.findall(r"```python\n(.*?)```", doc, flags=re.S)
+    n_lists = n_calls = 0
+    for blk in blocks:
+        for node in ast.walk(ast.parse(blk)):
+            if (isinstance(node, ast.Assign) and isinstance(node.targets[0], ast.Attribute)
+                    and node.targets[0].attr == "argtypes"):
+                name = node.targets[0].value.attr
+                types = eval(compile(ast.Expression(node.value), "<doc>", "eval"), {"C": C})
+                params = protos[name][1]
+                assert len(types) == len(params), f"INTEGRATION.md {name}: {len(types)} argtypes, header {len(params)}"
+                for i, (ct, py) in enumerate(zip(params, types)):
+                    assert _ctype_ok(ct, py), f"INTEGRATION.md {name}: parameter {i} is {ct}, doc binds {py}"
+                n_lists += 1
+            if (isinstance(node, ast.Call) and isinstance(node.func, ast.Attribute)
+                    and node.func.attr.startswith("icap_") and isinstance(node.func.value, ast.Name)
+                    and node.func.value.id == "lib"):
+                name = node.func.attr
+                assert len(node.args) == len(protos[name][1]), f"INTEGRATION.md call of {name}: {len(node.args)} args"
+                n_calls += 1
+    assert n_lists >= 3 and n_calls >= 3, (n_lists, n_calls)
+
+
 def test_version_and_workspace_queries():
     lib = _lib.load()
     assert lib.icap_version() >= 1

@@ -1,0 +1,132 @@
+"""Side-stream determinism over whole steps, localised without extra kernels. Diagnostic only.
+
+det_probe4 cloned every main-stream output right after its launch: the copies shifted the timing and the
+nondeterminism vanished. Here nothing is added to either stream. The trainer's mapper workspace is wrapped so that
+the buffers the mapper backward REUSES within a step (ws.da: written by the linear1 dX product and by the in_proj
+dX product of every layer; ws.do: the out_proj dX product) resolve to a fresh buffer per layer and producer; every
+other gradient buffer of the backward is already per layer (ws.g_*). After each full forward + backward
+(ICAP_SIDE_DW=1: each layer's dW products on the side stream) every one of those buffers holds exactly what its one
+launch wrote, so comparing them across calls names the first launch, in schedule order, whose output differs.
+"""
+import os
+import sys
+
+sys.path[:0] = ["/root/repo", "/root/repo/gpt2-image-captioning_amd", "/root/repo/tests"]
+import torch  # noqa: E402
+
+from icap import CaptionTrainer  # noqa: E402
+from oracle import icap_oracle as O  # noqa: E402
+from test_model_gpu import build  # noqa: E402
+from test_determinism_gpu import _batch  # noqa: E402
+
+dev = torch.device("cuda", 0)
+B = int(os.environ.get("PROBE_B", "32"))
+CALLS = int(os.environ.get("PROBE_CALLS", "6"))
+model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
+t = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10, dropout=False)
+tag = " ".join(f"{k}={os.environ[k]}" for k in sorted(os.environ) if k.startswith(("ICAP_", "PROBE_")))
+print("variant:", tag or "(defaults)", "side", t._side is not None, flush=True)
+t.load_batch(*_batch(B, dev))
+nl = len(t.mws.g_dz)
+
+
+class Split:
+    """Per-layer stand-ins for the reused buffers: the n-th access of `name` during a step gets buffer n // per."""
+
+    def __init__(self, ws):
+        object.__setattr__(self, "_ws", ws)
+        object.__setattr__(self, "_n", {"da": 0, "do": 0})
+        object.__setattr__(self, "_bufs", {"da": [torch.empty_like(ws.da) for _ in range(2 * nl)],
+                                           "do": [torch.empty_like(ws.do) for _ in range(nl)]})
+
+    def reset(self):
+        self._n["da"] = self._n["do"] = 0
+
+    def __getattr__(self, k):
+        if k in ("da", "do"):
+            i = self._n[k]
+            self._n[k] += 1
+            return self._bufs[k][i // 2]  # da: (out, dy) per producer; do: (out, attention dout) per layer
+        return getattr(self._ws, k)
+
+    def __setattr__(self, k, v):
+        setattr(self._ws, k, v)
+
+
+sp = Split(t.mws)
+t.mws = sp
+
+# experiment switches (probe-side monkeypatches of ops.layernorm_bwd; the library is unchanged)
+from icap import ops  # noqa: E402
+_lnb = ops.layernorm_bwd
+DUP = os.environ.get("PROBE_LN2_DUP") == "1"      # LN2 launched a second time into a spare per-layer buffer
+NOPAR = os.environ.get("PROBE_LN_NOPARAMS") == "1"  # LN backward without dgamma / dbeta (dx only)
+SYNC = os.environ.get("PROBE_SYNC_LN2") == "1"    # device-wide synchronize before every LN2 (no concurrency there)
+dups = [torch.empty_like(sp._ws.g_rm[0]) for _ in range(nl)]
+ln_count = [0]
+
+
+def lnb(x, gamma, mean, rstd, dy, dx, **kw):
+    ln_count[0] += 1
+    # the mapper's LN2 backward writes ws.g_rm[l] (the GPT-2 backward's LayerNorms go through here too)
+    li = [k for k, g in enumerate(sp._ws.g_rm) if g is dx]
+    ln2 = bool(li)
+    if NOPAR:
+        kw = dict(kw, dgamma=None, dbeta=None)
+    if ln2 and SYNC:
+        torch.cuda.synchronize()
+    r = _lnb(x, gamma, mean, rstd, dy, dx, **kw)
+    if ln2 and DUP:
+        kd = dict(kw, dgamma=None, dbeta=None, dx_drop=None)
+        _lnb(x, gamma, mean, rstd, dy, dups[nl - 1 - li[0]], **kd)
+    return r
+
+
+ops.layernorm_bwd = lnb
+
+
+def snapshot():
+    w = sp._ws
+    out = []
+    for l in reversed(range(nl)):  # schedule order of the backward (top layer first)
+        j = nl - 1 - l
+        out += [(f"g_dz[{l}] (linear2 dX)", w.g_dz[l]), (f"da[{l}] (linear1 dX)", sp._bufs["da"][2 * j]),
+                (f"g_rm[{l}] (LN2 bwd)", w.g_rm[l]), (f"do[{l}] (out_proj dX)", sp._bufs["do"][j]),
+                (f"g_dqkv[{l}] (attention bwd)", w.g_dqkv[l]), (f"da'[{l}] (in_proj dX)", sp._bufs["da"][2 * j + 1]),
+                (f"{'g_r[%d]' % (l - 1) if l else 'dres'} (LN1 bwd)", w.g_r[l - 1] if l else w.dres)]
+    if DUP:
+        out += [(f"dup LN2[{nl - 1 - j}]", dups[j]) for j in range(nl)]
+    out.append(("flat_grad", t.flat.flat_grad))
+    return [(n, x.detach().clone()) for n, x in out]
+
+
+def dup_vs_orig():
+    """within one call: the duplicate LN2 launch against the original output (same inputs, same stream)"""
+    if not DUP:
+        return ""
+    w = sp._ws
+    nd = [int((dups[j] != w.g_rm[nl - 1 - j]).sum()) for j in range(nl)]
+    return f" dup-vs-orig differing elements per layer (top first) {nd}"
+
+
+snaps = []
+for i in range(CALLS):
+    sp.reset()
+    ln_count[0] = 0
+    t._fwd_bwd(True, 1.0)
+    torch.cuda.synchronize()
+    snaps.append(snapshot())
+    print(f"call {i + 1}:{dup_vs_orig()}", flush=True)
+
+bad = 0
+for i in range(1, CALLS):
+    first, nd = None, 0
+    for (n, a), (_, b) in zip(snaps[i - 1], snaps[i]):
+        if not bool(((a == b) | (a.isnan() & b.isnan())).all()):
+            nd += 1
+            if first is None:
+                d = (a.float() - b.float()).abs().nan_to_num()
+                first = (n, int((a != b).sum()), float(d.max()), float(a.float().abs().nan_to_num().max()))
+    bad += nd
+    print(f"call {i + 1} vs {i}: {nd} buffers differ; first {first}", flush=True)
+print("RESULT", "deterministic" if bad == 0 else "NONDETERMINISTIC", tag, flush=True)
