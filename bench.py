@@ -111,7 +111,7 @@ def live_rows(labels, P, squares=False):
     return lr(labels, P, squares=squares)
 
 
-def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16, fp8=False, pack=None):
+def build(B, dev, dropout=True, config="small", dtype=torch.bfloat16, fp8=False, pack=True):
     """config "small": BASELINE configs[1] (GPT-2 small + CLIP ViT-B/32); "medium": configs[3] (GPT-2 medium +
     CLIP ViT-L/14 encoder on the device, mapper at gpt_dim 1024 / CLIP-L embed 768)."""
     from types import SimpleNamespace

@@ -370,14 +370,11 @@ __global__ __launch_bounds__(64) void attn_decode64_kernel(int B, int H, int pos
 }
 
 // bf16 MFMA kernels (attention_mfma.hip); the fp32 parity mode and shapes they do not cover use the
-// LDS/VALU kernels of this file. ICAP_ATTN_VALU=1 forces the VALU kernels (A/B testing).
+// LDS/VALU kernels of this file. (diagnostic build) ICAP_ATTN_VALU=1 forces the VALU kernels.
 bool mfma_attention_ok(const icap_attn_args* a, bool bwd);
 int mfma_attention_launch(const icap_attn_args* a, bool bwd, uint32_t thr, float inv_keep, hipStream_t s);
 static bool force_valu() {
-  static const bool f = [] {
-    const char* e = getenv("ICAP_ATTN_VALU");
-    return e && e[0] == '1';
-  }();
+  static const bool f = diag_env("ICAP_ATTN_VALU", 0) == 1;
   return f;
 }
 

@@ -6,6 +6,19 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+
+// Diagnostic build only (make stamps: -DICAP_STAMPS): A/B overrides of the kernel choice read from the process
+// environment (tools/ab). The product library reads no environment variable: in it every choice is a function of
+// the call's arguments and diag_env returns its default at compile time.
+#ifdef ICAP_STAMPS
+#include <cstdlib>
+static inline int diag_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+#else
+static constexpr int diag_env(const char*, int dflt) { return dflt; }
+#endif
 #include <stdint.h>
 #include <string>
 

@@ -240,6 +240,105 @@ __global__ __launch_bounds__(1024) void caption_pack_kernel(int B, int P, int L,
   if (threadIdx.x == 0 && n_valid) *n_valid = tot;
 }
 
+// The same outputs from several blocks, for B <= PK2_MAX (round 5: the one-block form above took ~32 us per step, a
+// chain of dependent label loads and block scans on one CU). Every block runs phase 1 over ALL captions — one wave
+// per caption, lanes over its 50 label positions, one ballot: live length, target count, target bit mask — and the
+// two exclusive scans (offsets, target slots) in its own LDS, so no block waits for another; then each wave writes
+// the rows of one caption of the block's share (lanes over positions; the slot of a target row is the caption's
+// slot offset + the targets before it in the ballot), and the blocks stride over the dead rows [m_live, B S).
+// Identical outputs to caption_pack_kernel (tests/test_pack_gpu.py compares both forms element by element).
+constexpr int PK2_MAX = 2048;
+constexpr int PK2_WAVES = 16;
+__global__ __launch_bounds__(1024) void caption_pack2_kernel(int B, int P, int L, const int64_t* __restrict__ mask,
+                                                            const int64_t* __restrict__ labels, int32_t* seq_off,
+                                                            int32_t* seq_len, int32_t* m_live, int32_t* key_mask,
+                                                            int32_t* lab_shift, int32_t* n_valid, int32_t* row_slot,
+                                                            int32_t* lab_c) {
+  __shared__ int wsum[16];
+  __shared__ int s_len[PK2_MAX], s_off[PK2_MAX], s_tgt[PK2_MAX];
+  const int S = P + L, n = B * S;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // position t's shifted label: labels[b, t + 1 - P] for P <= t + 1 < S (t = P - 1 + j, label j of the caption)
+  auto label_at = [&](int b, int t) {
+    const int tn = t + 1;
+    return (tn < S && tn >= P && labels) ? (int)labels[(int64_t)b * L + tn - P] : -100;
+  };
+  // phase 1 (every block, all captions): live length P + (last target j >= 1), target count over j (t = P - 1 + j >= 0)
+  for (int b = w; b < B; b += PK2_WAVES) {
+    int jlast = 0, tg = 0;
+    for (int j0 = 0; j0 < L; j0 += 64) {
+      const int j = j0 + lane;
+      const bool ok = j < L && P - 1 + j >= 0 && labels != nullptr && labels[(int64_t)b * L + j] != -100;
+      const uint64_t bal = __ballot(ok);
+      tg += __popcll(bal);
+      if (bal) jlast = j0 + 63 - __clzll(bal);
+    }
+    if (lane == 0) {
+      s_len[b] = P + (jlast >= 1 ? jlast : 0);
+      s_tgt[b] = tg;
+    }
+  }
+  __syncthreads();
+  // the two exclusive scans over the captions: thread k owns captions [k c, k c + c)
+  const int per = (B + 1023) / 1024;
+  const int b0 = threadIdx.x * per < B ? threadIdx.x * per : B;
+  const int b1 = b0 + per < B ? b0 + per : B;
+  int cl = 0, ct = 0;
+  for (int b = b0; b < b1; ++b) {
+    cl += s_len[b];
+    ct += s_tgt[b];
+  }
+  int mtot = 0, ttot = 0;
+  int off = block_excl_scan1024(cl, wsum, mtot);
+  int slot = block_excl_scan1024(ct, wsum, ttot);
+  __syncthreads();  // every thread has read s_len / s_tgt for its sums
+  for (int b = b0; b < b1; ++b) {
+    const int l = s_len[b], tg = s_tgt[b];
+    s_off[b] = off;
+    s_tgt[b] = slot;  // now the caption's first target slot
+    if (blockIdx.x == 0) {
+      seq_off[b] = off;
+      seq_len[b] = l;
+    }
+    off += l;
+    slot += tg;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *m_live = mtot;
+    if (n_valid) *n_valid = ttot;
+  }
+  __syncthreads();
+  // phase 2: one wave per caption of this block's share
+  for (int b = blockIdx.x * PK2_WAVES + w; b < B; b += gridDim.x * PK2_WAVES) {
+    const int o = s_off[b], len = s_len[b];
+    int sl = s_tgt[b];
+    for (int t0 = 0; t0 < len; t0 += 64) {
+      const int t = t0 + lane;
+      int lab = -100, km = 0;
+      if (t < len) {
+        km = (t < P || mask == nullptr) ? 1 : (mask[(int64_t)b * L + t - P] != 0 ? 1 : 0);
+        lab = label_at(b, t);
+        key_mask[o + t] = km;
+        lab_shift[o + t] = lab;
+      }
+      const bool tgt = lab != -100;
+      const uint64_t bal = __ballot(tgt);
+      if (row_slot && t < len) {
+        const int mine = sl + __popcll(bal & ((1ull << lane) - 1ull));
+        row_slot[o + t] = tgt ? mine : -1;
+        if (tgt && lab_c) lab_c[mine] = lab;
+      }
+      sl += __popcll(bal);
+    }
+  }
+  // the dead rows past the packed ones
+  for (int i = mtot + blockIdx.x * 1024 + (int)threadIdx.x; i < n; i += gridDim.x * 1024) {
+    key_mask[i] = 0;
+    lab_shift[i] = -100;
+    if (row_slot) row_slot[i] = -1;
+  }
+}
+
 template <typename T>
 __global__ void rows_unpack_kernel(int B, int P, int D, const T* __restrict__ src, const int32_t* __restrict__ seq_off,
                                    const int32_t* __restrict__ seq_len, T* __restrict__ dst, int64_t dbs) {
@@ -1258,8 +1357,14 @@ extern "C" int icap_caption_pack(int32_t B, int32_t P, int32_t L, const int64_t*
   ICAP_REQUIRE((int64_t)B * (P + L) < (1ll << 30), "icap_caption_pack: too many rows");
   ICAP_REQUIRE(seq_off && seq_len && m_live && key_mask && labels_shift, "icap_caption_pack: null pointer");
   ICAP_REQUIRE((row_slot == nullptr) == (labels_compact == nullptr), "icap_caption_pack: row_slot and labels_compact go together");
-  hipLaunchKernelGGL(caption_pack_kernel, dim3(1), dim3(1024), 0, S_(stream), B, P, L, mask, labels, seq_off, seq_len,
-                     m_live, key_mask, labels_shift, n_valid, row_slot, labels_compact);
+  if (B <= PK2_MAX) {
+    const int nb = (B + PK2_WAVES - 1) / PK2_WAVES;
+    hipLaunchKernelGGL(caption_pack2_kernel, dim3(nb), dim3(1024), 0, S_(stream), B, P, L, mask, labels, seq_off,
+                       seq_len, m_live, key_mask, labels_shift, n_valid, row_slot, labels_compact);
+  } else {
+    hipLaunchKernelGGL(caption_pack_kernel, dim3(1), dim3(1024), 0, S_(stream), B, P, L, mask, labels, seq_off,
+                       seq_len, m_live, key_mask, labels_shift, n_valid, row_slot, labels_compact);
+  }
   return check_launch("icap_caption_pack");
 }
 

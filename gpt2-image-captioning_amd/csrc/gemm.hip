@@ -380,10 +380,6 @@ using namespace icap;
 // bound by the per-block prologue/epilogue, which co-resident blocks hide -> single LDS buffer, 3-4 blocks/CU (4
 // when the epilogue moves a second M x N tensor: dact_src read / aux store); long K favours the double-buffered
 // main loop at 2 blocks/CU.
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
 static int gemm_variant(const icap_gemm_args& p, int64_t nk_per_block) {
   if (nk_per_block > 16) return 0;
   const bool heavy = p.dact != ICAP_ACT_NONE || p.aux;
@@ -392,7 +388,7 @@ static int gemm_variant(const icap_gemm_args& p, int64_t nk_per_block) {
   // activation only, and with neither. Round 4: dact / aux launches at 3 blocks / CU too — the 4-block form (128
   // VGPRs) spills with those epilogues (profiles/r04_gemm_tiles_ab.txt: GPT-2 c_fc gelu + aux 42.2 vs 46.2 us,
   // mlp c_proj dgelu 43.4 vs 43.5)
-  static const int vh = env_int("ICAP_VAR_HEAVY", 4), va = env_int("ICAP_VAR_ACT", 4), vl = env_int("ICAP_VAR_LIGHT", 4);
+  static const int vh = diag_env("ICAP_VAR_HEAVY", 4), va = diag_env("ICAP_VAR_ACT", 4), vl = diag_env("ICAP_VAR_LIGHT", 4);
   return heavy ? vh : act ? va : vl;
 }
 
@@ -413,11 +409,11 @@ namespace icap {
 int gemm256_launch(const icap_gemm_args& p, uint32_t thr, float inv_keep, hipStream_t s);
 }
 
-// ICAP_GEMM256: 0 = never, 2 = wherever eligible, default = the shape rule below (A/B measurements only)
+// (diagnostic build) ICAP_GEMM256: 0 = never, 2 = wherever eligible, default = the shape rule below
 static int g256_mode() {
   static const int m = [] {
-    const char* e = getenv("ICAP_GEMM256");
-    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
+    const int v = diag_env("ICAP_GEMM256", 1);
+    return v == 0 || v == 2 ? v : 1;
   }();
   return m;
 }
@@ -446,7 +442,7 @@ static bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 1
 // A/B switches for the in-launch split-K: ICAP_FUSED_S = forced split count (read once), ICAP_FUSED_NST = 1 gives
 // its K ranges the variant rule, 4 the 4-stage ring (default: the double-buffered kernel)
 static int fused_s_override() {
-  static const int v = [] { const char* e = getenv("ICAP_FUSED_S"); return e ? atoi(e) : 0; }();
+  static const int v = diag_env("ICAP_FUSED_S", 0);
   return v;
 }
 // K-skew: tile (tm, tn) walks its K range starting at step ((7 tm + tn) * skew) mod nk and wraps, so the tiles of
@@ -457,38 +453,27 @@ static int fused_s_override() {
 // longer, so they keep the natural order. ICAP_KSKEW overrides the skew (0 = off; A/B only); path 1 (tile_only)
 // keeps the natural order (the path-equality tests compare it bitwise with the 256 x 256 kernel).
 static int kskew_for(const icap_gemm_args& p, int64_t nk_split) {
-  static const int v = [] { const char* e = getenv("ICAP_KSKEW"); return e ? atoi(e) : 1; }();
+  static const int v = diag_env("ICAP_KSKEW", 1);
   if (p.path == 1 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
   return v > 0 && v < 256 ? v : 0;
 }
 // ICAP_GEMM_DIAG = 1 / 2 / 3: drop the A / B / both operands' staging loads of the tile kernels (zero-record
 // descriptors) — a timing diagnostic for what the operand traffic costs; the outputs are wrong. Never in a real run.
 // ICAP_FUSED_ACQUIRE=1: the in-launch split-K's last arriver runs an agent-scope acquire after its ticket poll
-static int gemm_acquire() {
-  const char* e = getenv("ICAP_FUSED_ACQUIRE");
-  return e && e[0] == '1' ? 1 : 0;
-}
-static bool kout_fused_on() {  // ICAP_KOUT_FUSED=1: K-outer weight-gradient splits combine in the launch (A/B)
-  const char* e = getenv("ICAP_KOUT_FUSED");
-  return e && e[0] == '1';
-}
-static int gemm_diag() {  // (read per launch: an A/B driver toggles it in one process)
-  const char* e = getenv("ICAP_GEMM_DIAG");
-  return e ? (atoi(e) & 3) : 0;
-}
-static bool spec_act_on() {  // ICAP_SPEC_ACT=0: the runtime-dispatch epilogue everywhere (A/B only)
-  static const bool v = [] { const char* e = getenv("ICAP_SPEC_ACT"); return !(e && e[0] == '0'); }();
-  return v;
-}
-static int fused_min_nk() {  // (A/B only, read per call) ICAP_FUSED_MINK: fewest K stages for the in-launch split
-  const char* e = getenv("ICAP_FUSED_MINK");
-  const int v = e ? atoi(e) : 0;
+static int gemm_acquire() { return diag_env("ICAP_FUSED_ACQUIRE", 0) == 1 ? 1 : 0; }
+// (diagnostic build) ICAP_KOUT_FUSED=1: K-outer weight-gradient splits combine in the launch
+static bool kout_fused_on() { return diag_env("ICAP_KOUT_FUSED", 0) == 1; }
+// (diagnostic build, read per launch: an A/B driver toggles it in one process)
+static int gemm_diag() { return diag_env("ICAP_GEMM_DIAG", 0) & 3; }
+// (diagnostic build) ICAP_SPEC_ACT=0: the runtime-dispatch epilogue everywhere
+static bool spec_act_on() { return diag_env("ICAP_SPEC_ACT", 1) != 0; }
+// (diagnostic build, read per call) ICAP_FUSED_MINK: fewest K stages for the in-launch split
+static int fused_min_nk() {
+  const int v = diag_env("ICAP_FUSED_MINK", 0);
   return v >= 2 ? v : 24;
 }
-static int fused_nst_override() {  // (read per call: tools/gemm_tiles_ab.py toggles it in one process)
-  const char* e = getenv("ICAP_FUSED_NST");
-  return e ? atoi(e) : 0;
-}
+// (diagnostic build, read per call: tools/gemm_tiles_ab.py toggles it in one process)
+static int fused_nst_override() { return diag_env("ICAP_FUSED_NST", 0); }
 
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
@@ -686,10 +671,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
     pl.variant = tiles < 256 ? 12 : 13;
   }
   if (p.trans_ab) pl.variant = nk_split > 16 ? 14 : 15;  // K-outer forms of variants 0 / 4
-  // ICAP_FORCE_TILE = 0 / 4 / 5 / 12 / 13 / 16: that tile variant for unsplit bf16 row-major launches (A/B only; read
-  // per call so one process can interleave the forms)
-  if (const char* fv = getenv("ICAP_FORCE_TILE")) {
-    const int v = atoi(fv);
+  // (diagnostic build) ICAP_FORCE_TILE = 0 / 4 / 5 / 12 / 13 / 16: that tile variant for unsplit bf16 row-major
+  // launches (read per call so one process can interleave the forms)
+  if (const int v = diag_env("ICAP_FORCE_TILE", -1); v >= 0) {
     if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 &&
         (v == 0 || v == 4 || v == 5 || v == 12 || v == 13 || (v == 16 && !lnx))) {
       pl.variant = v;
@@ -697,10 +681,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
       tiles = tiles_m * tiles_n;
     }
   }
-  // (A/B only, read per call) ICAP_LN_VAR = 0 / 4 / 5: that 128 x 128 variant for the LayerNorm hand-off launches
+  // (diagnostic build, read per call) ICAP_LN_VAR = 0 / 4 / 5: that 128 x 128 variant for the LayerNorm hand-off
   if (lnx && (pl.variant == 0 || pl.variant == 4 || pl.variant == 5)) {
-    const char* e = getenv("ICAP_LN_VAR");
-    const int lv = e ? atoi(e) : -1;
+    const int lv = diag_env("ICAP_LN_VAR", -1);
     if (lv == 0 || lv == 4 || lv == 5) pl.variant = lv;
   }
   // the LayerNorm-folded quick_gelu consumer (CLIP c_fc) exists at 3 blocks / CU only (gemm_tile_ln.hip)

@@ -209,10 +209,23 @@ __global__ __launch_bounds__(1024) void ln_param_reduce(int nblk, int D, const f
 // D <= 1536
 constexpr int LN8_DMAX = 6 * 32 * 8;
 
+// Sum over a 32-lane half-wave, in every lane of it, on the VALU's cross-lane paths (round 5): DPP quad_perm for
+// lane ^ 1 and ^ 2, row_half_mirror (i <-> 7 - i: the other quad of each 8), row_ror:8 (lane ^ 8 within a 16-lane
+// row) and v_permlane16_swap for the other row of the half. The __shfl_xor butterfly it replaces lowered to
+// ds_bpermute_b32 (the LDS crossbar, 5 dependent round trips): with the mapper's K-outer weight-gradient GEMMs
+// co-resident on the same CUs (the side-stream schedule, tools/ab/det_probe5.py) that form returned slightly wrong
+// row sums for a few rows per launch — the same launch repeated on the same inputs disagreed with itself
+// (profiles/r05_side_stream_probe5.txt). The operation order is fixed and lane-independent, so every lane of the
+// half holds the same bits. Both halves of a wave must be active or inactive together (the row loops are uniform
+// per half).
 __device__ __forceinline__ float half_sum(float v) {
-#pragma unroll
-  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));   // ^1
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));   // ^2
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));  // 7-i
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));  // ror 8
+  const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                   false, false);
+  return __builtin_bit_cast(float, (unsigned)sw[0]) + __builtin_bit_cast(float, (unsigned)sw[1]);
 }
 
 template <typename T, int LN8_MAXC>
@@ -271,6 +284,13 @@ __global__ __launch_bounds__(256) void ln_fwd8_kernel(int64_t rows, int D, const
       if (rstd_out) rstd_out[r] = rs;
     }
   }
+}
+
+// v + the same register of lane ^ 32 (v_permlane32_swap; the bits equal v + __shfl_xor(v, 32) in every lane)
+__device__ __forceinline__ float lane_pair_sum(float v) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                   false, false);
+  return __builtin_bit_cast(float, (unsigned)sw[0]) + __builtin_bit_cast(float, (unsigned)sw[1]);
 }
 
 // PARAMS: accumulate dgamma / dbeta partials (per block, combined by ln_param_reduce); GPT-2's LNs are frozen
@@ -369,8 +389,8 @@ __global__ __launch_bounds__(256) void ln_bwd8_kernel(int64_t rows, int D, const
     for (int t = 0; t < LN8_MAXC; ++t)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        dg[t][e] += __shfl_xor(dg[t][e], 32, 64);
-        db[t][e] += __shfl_xor(db[t][e], 32, 64);
+        dg[t][e] = lane_pair_sum(dg[t][e]);
+        db[t][e] = lane_pair_sum(db[t][e]);
       }
     if ((threadIdx.x & 63) < 32) {
 #pragma unroll

@@ -154,6 +154,7 @@ SIGNATURES = {
     "icap_im2col_patches": (C.c_int, [i32, i32, i32, i32, i32, vp, vp, vp]),
     "icap_vit_embed": (C.c_int, [i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     "icap_prefix_embed": (C.c_int, [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
+    "icap_patch_embed": (C.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, i64, i32, vp, vp, vp, vp, i64, vp]),
     "icap_rope_patches": (C.c_int, [i32, i32, i32, i32, i32, i32, vp, i64, vp, vp, vp]),
     "icap_l2norm_rows": (C.c_int, [i32, i64, i64, vp, i64, vp, i64, vp]),
     "icap_topp_sample": (C.c_int, [i32, i32, i64, vp, i64, f32, f32, vp, u64, vp, i32, i64, vp, vp]),

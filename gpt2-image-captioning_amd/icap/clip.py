@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
+from . import gpt2 as _gpt2
 from . import ops
 from .gpt2 import fold_layernorm
 from .weights import det_tensor
@@ -192,7 +193,7 @@ class ClipCore:
         vm, dt = self.m.vision_model, self.dtype
         # bf16: layer_norm1 (layers >= 1) / layer_norm2 (all but the last) folded into the QKV / fc1 tile GEMMs, the row
         # statistics handed over from the producing GEMMs' epilogues (icap_gemm_args.ln_stats_out / ln_stats_in)
-        self.fold = dt == torch.bfloat16 and ops.ln_fold_ok(self.D) and TRAIN_LN_FOLD
+        self.fold = dt == torch.bfloat16 and ops.ln_fold_ok(self.D) and _gpt2.TRAIN_LN_FOLD
         # [D, C*p*p] (c, ky, kx) order, zero-padded to the 8-multiple row of icap_im2col_patches (p = 14: 592)
         wp = vm.embeddings.patch_embedding.weight.data.reshape(self.D, -1)
         self.Kp = (wp.shape[1] + 7) // 8 * 8
@@ -228,8 +229,9 @@ class ClipCore:
         M = B * self.S
         e = lambda *shape, dtype=dt: torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
         ws = SimpleNamespace(B=B, M=M)
-        ws.patches = e(B * self.G * self.G, self.Kp)
-        ws.pe = e(B * self.G * self.G, D)
+        if dt != torch.bfloat16:  # (bf16: icap_patch_embed reads the pixels itself — no patch matrix)
+            ws.patches = e(B * self.G * self.G, self.Kp)
+            ws.pe = e(B * self.G * self.G, D)
         ws.x, ws.h1, ws.a, ws.o = e(M, D), e(M, D), e(M, D), e(M, D)
         ws.qkv = e(M, 3 * D)
         ws.f = e(M, c.intermediate_size)
@@ -249,9 +251,14 @@ class ClipCore:
         """Kernel schedule; returns ws.emb (fp32, L2-normalised) — graph-capturable."""
         c, D, B = self.c, self.D, ws.B
         eps = c.layer_norm_eps
-        ops.im2col_patches(pixels, ws.patches, c.patch_size)
-        ops.gemm(ws.patches, self.w_patch, ws.pe)  # Conv2d(stride=patch, bias=False) as a GEMM
-        ops.vit_embed(ws.pe, self.cls, self.pos, ws.h1, B, self.G * self.G, D)
+        if self.dtype == torch.bfloat16:
+            # Conv2d(stride=patch, bias=False) + [CLS || patches] + positions in one launch that gathers the pixel runs
+            # into its LDS stages (round 5: no im2col patch matrix, no separate embedding pass)
+            ops.patch_embed(pixels, self.w_patch, ws.h1, patch=c.patch_size, prefix=self.cls.view(1, D), pos=self.pos)
+        else:  # fp32 parity mode: the exact-fp32 tile GEMM over the im2col matrix
+            ops.im2col_patches(pixels, ws.patches, c.patch_size)
+            ops.gemm(ws.patches, self.w_patch, ws.pe)  # Conv2d(stride=patch, bias=False) as a GEMM
+            ops.vit_embed(ws.pe, self.cls, self.pos, ws.h1, B, self.G * self.G, D)
         ops.layernorm_fwd(ws.h1, self.pre[0], self.pre[1], eps, ws.x, None, None)
         scale = self.hd ** -0.5
         nl = len(self.layers)

@@ -330,8 +330,9 @@ class DinoCore:
         M = B * self.S
         e = lambda *shape, dtype=dt: torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
         ws = SimpleNamespace(B=B, M=M)
-        ws.patches = e(B * self.G * self.G, self.Kp)
-        ws.pe = e(B * self.G * self.G, D)
+        if dt != torch.bfloat16:  # (bf16: icap_patch_embed reads the pixels itself — no patch matrix)
+            ws.patches = e(B * self.G * self.G, self.Kp)
+            ws.pe = e(B * self.G * self.G, D)
         ws.x, ws.h1, ws.a, ws.o = e(M, D), e(M, D), e(M, D), e(M, D)
         ws.qkv = e(M, 3 * D)
         ws.f = e(M, c.intermediate_size)
@@ -346,9 +347,12 @@ class DinoCore:
         """Kernel schedule; fills ws.pool (pooler_output, fp32) and ws.emb (L2-normalised) — graph-capturable."""
         c, D, B, S = self.c, self.D, ws.B, self.S
         eps = c.layer_norm_eps
-        ops.im2col_patches(pixels, ws.patches, c.patch_size)
-        ops.gemm(ws.patches, self.w_patch, ws.pe, bias=self.b_patch)  # Conv2d(stride=patch, bias) as a GEMM
-        ops.prefix_embed(ws.pe, self.prefix, ws.x, B, self.G * self.G, D)  # [CLS || registers || patches]
+        if self.dtype == torch.bfloat16:  # patch Conv2d + [CLS || registers || patches], pixels read by the GEMM
+            ops.patch_embed(pixels, self.w_patch, ws.x, patch=c.patch_size, prefix=self.prefix, bias=self.b_patch)
+        else:
+            ops.im2col_patches(pixels, ws.patches, c.patch_size)
+            ops.gemm(ws.patches, self.w_patch, ws.pe, bias=self.b_patch)  # Conv2d(stride=patch, bias) as a GEMM
+            ops.prefix_embed(ws.pe, self.prefix, ws.x, B, self.G * self.G, D)  # [CLS || registers || patches]
         scale = self.hd ** -0.5
         nl = len(self.layers)
         for i, w in enumerate(self.layers):

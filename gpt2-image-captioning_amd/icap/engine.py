@@ -20,13 +20,14 @@ from . import ops
 from .mapper import DWHelper, MLPMapperCore, TransformerMapperCore
 from .models import _embedding_grads
 
+# Schedule constants (module attributes, not process environment: A/B tools and tests set them explicitly).
 # packed attention launches skip their long-sequence pass when every sequence of the batch is short (set per batch in
-# load_batch); ICAP_SHORT_ONLY=0 always launches both passes (A/B)
-SHORT_ONLY = os.environ.get("ICAP_SHORT_ONLY", "1") != "0"
+# load_batch); False always launches both passes
+SHORT_ONLY = True
 # the first micro-batch of an accumulation cycle writes the trained mapper's gradients (each is produced once per
-# micro-batch) instead of zeroing the flat gradient buffer and accumulating into it; ICAP_GRAD_OVERWRITE=0 restores
-# the zero_() + accumulate form (A/B)
-GRAD_OVERWRITE = os.environ.get("ICAP_GRAD_OVERWRITE", "1") != "0"
+# micro-batch) instead of zeroing the flat gradient buffer and accumulating into it; False restores the zero_() +
+# accumulate form
+GRAD_OVERWRITE = True
 # the transformer mapper's dW products of a layer unsplit and side by side on four streams at the end of its backward
 # step (mapper.backward_steps group=) instead of split-K + reduce in series inside the step (A/B switch)
 GROUP_DW = os.environ.get("ICAP_GROUP_DW", "0") == "1"
@@ -39,7 +40,11 @@ class CaptionTrainer:
                  betas=(0.9, 0.999), eps: float = 1e-8, max_norm: float = 1.0, num_warmup_steps: int = 0,
                  num_training_steps: int = 1, dropout: bool = True, seed: int = 0, clip_model=None,
                  grad_accum_steps: int = 1, process_group=None, compact_head: bool = True,
-                 pack_rows: Optional[bool] = None):
+                 pack_rows: bool = True, dp_overlap: bool = True, dp_bf16: bool = False, force_overlap: bool = False):
+        """pack_rows: packed token rows (GPT2Core.alloc_train); dp_overlap: with N > 1 ranks, all-reduce each backward
+        segment's gradient bucket beside the later segments (False: one whole-buffer all-reduce after the backward);
+        dp_bf16: exchange the gradients as bf16 (half the bytes; rounds the sum over ranks); force_overlap: take the
+        bucketed communication-stream step at world size 1 too (exercises the RCCL calls on one GPU)."""
         self.model = model
         self.dtype = model.compute_dtype
         self.B, self.Lc = batch_size, caption_len
@@ -58,7 +63,7 @@ class CaptionTrainer:
             # GPT-2 / image-tower weights), whatever each process's RNG produced when it built the model
             broadcast_replicas([model] + ([clip_model] if clip_model is not None else []), process_group)
         # the bucketed communication-stream step also at world size 1 (exercises the RCCL calls on one GPU)
-        self.force_overlap = os.environ.get("ICAP_DP_FORCE_OVERLAP", "0") == "1" and self.distributed
+        self.force_overlap = bool(force_overlap) and self.distributed
         self.dev = model.device
         flat = model.flat()
         self.flat = flat
@@ -81,9 +86,7 @@ class CaptionTrainer:
         self.P = P
         self.mws = self.mcore.alloc(B, train=True)
         # packed token rows (GPT2Core.alloc_train): the blocks skip each caption's dead tail (positions after its
-        # last loss target, which the causal mask keeps out of every loss term); default on, ICAP_PACK=0 disables
-        if pack_rows is None:
-            pack_rows = os.environ.get("ICAP_PACK", "1") != "0"
+        # last loss target, which the causal mask keeps out of every loss term)
         self.gws = self.gcore.alloc_train(B, P, Lc, keep_for_dw=self.gpt_trainable, compact_head=compact_head,
                                           pack=pack_rows)
         D = self.gcore.D
@@ -111,10 +114,10 @@ class CaptionTrainer:
         self._ranges_mapper = [flat_ranges(flat, ps) for ps in groups]
         seen = {id(p) for ps in groups for p in ps}
         self._ranges_front = flat_ranges(flat, [p for p in flat.params if id(p) not in seen])
-        self.dp_overlap = os.environ.get("ICAP_DP_OVERLAP", "1") != "0"
+        self.dp_overlap = bool(dp_overlap)
         # opt-in: all-reduce the gradients as bf16 (half the bytes over xGMI; the sum over ranks is rounded to bf16
         # per element, so it is not the fp32 reduction the reference's single-process step corresponds to)
-        self.dp_bf16 = os.environ.get("ICAP_DP_BF16", "0") == "1"
+        self.dp_bf16 = bool(dp_bf16)
         self._g16 = None
         self.seg_graphs = {}  # zero -> [HIP graph per segment] (data-parallel overlapped step)
         self._comm = None

@@ -26,12 +26,12 @@ from .ops import Dropout
 from .weights import det_tensor
 
 # decode steps (M <= 128) of a frozen GPT-2: ln_1 / ln_2 folded into the QKV / c_fc weights (GPT2Core._fold_ln);
-# ICAP_LN_FOLD=0 keeps the LayerNorm-fused GEMMs (A/B measurements)
-LN_FOLD = os.environ.get("ICAP_LN_FOLD", "1") != "0"
-# training / inference forward of a frozen bf16 GPT-2: ln_1 (layers >= 1) and ln_2 folded into the QKV / c_fc tile
-# GEMMs, their row statistics handed over from the producing GEMMs' epilogues (icap_gemm_args.ln_stats_out /
-# ln_stats_in); ICAP_TRAIN_LN_FOLD=0 keeps the standalone LayerNorm launches (A/B)
-TRAIN_LN_FOLD = os.environ.get("ICAP_TRAIN_LN_FOLD", "1") != "0"
+# False keeps the LayerNorm-fused GEMMs (module constant, not process environment: A/B tools and tests set it)
+LN_FOLD = True
+# training / inference forward of a frozen bf16 GPT-2 (and the CLIP tower, clip.ClipCore): ln_1 (layers >= 1) and
+# ln_2 folded into the QKV / c_fc tile GEMMs, their row statistics handed over from the producing GEMMs' epilogues
+# (icap_gemm_args.ln_stats_out / ln_stats_in); False keeps the standalone LayerNorm launches
+TRAIN_LN_FOLD = True
 
 Tensor = torch.Tensor
 

@@ -257,7 +257,8 @@ def ln_fold_ok(D: int) -> bool:
 
 GEMM_WORKSPACE_BYTES = 192 << 20  # split-K slabs up to splits*M*N fp32 (LM-head dX: 6 x 6400 x 768)
 GEMM_TICKETS = 1 << 16  # int32 per-tile counters of the in-launch split-K combine (2 per 128 x 128 tile)
-FUSED_SPLIT_K = os.environ.get("ICAP_FUSED_SPLIT_K", "1") != "0"  # 0: split-K always through a reduce pass (A/B)
+# False: split-K always through a reduce pass (module constant for A/B tools; the two forms are bitwise equal)
+FUSED_SPLIT_K = True
 _gemm_ws = {}
 _gemm_tickets = {}  # workspace data_ptr -> its tickets (zeroed once; every launch leaves them zero)
 
@@ -683,6 +684,31 @@ def broadcast_rows(src: Tensor, dst: Tensor, B: int, dst_bstride: int) -> Tensor
     call("icap_broadcast_rows", dtype_code(dst.dtype), B, R, D, src.data_ptr(), dst.data_ptr(), dst_bstride,
          _stream())
     return dst
+
+
+def patch_embed(pixels: Tensor, w: Tensor, out: Tensor, *, patch: int, prefix: Optional[Tensor],
+                pos: Optional[Tensor] = None, bias: Optional[Tensor] = None) -> Tensor:
+    """Patch Conv2d (stride = kernel = patch) + token assembly in one launch (include/icap.h icap_patch_embed):
+    out[b*S + r] = prefix[r] (+ pos[r]) for r < NP, out[b*S + NP + i] = patch_i . w^T (+ bias) (+ pos[NP + i]).
+    pixels fp32 [B, C, H, H]; w bf16 [N, Kp] in (c, ky, kx) order, zero past C*p*p; out bf16 [B*S, N]."""
+    if pixels.dtype != torch.float32 or not pixels.is_contiguous() or pixels.dim() != 4:
+        raise L.IcapError("patch_embed: pixels must be contiguous fp32 [B,C,H,H]")
+    if w.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
+        raise L.IcapError("patch_embed: w and out must be bf16")
+    B, Cc, H, _ = pixels.shape
+    NP = 0 if prefix is None else prefix.shape[0]
+    N = w.shape[0]
+    S = NP + (H // patch) ** 2
+    if out.shape[0] < B * S or out.shape[1] < N:
+        raise L.IcapError("patch_embed: out is too small")
+    for t in (prefix, pos, bias):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise L.IcapError("patch_embed: prefix / pos / bias must be contiguous fp32")
+    if pos is not None and pos.numel() < S * N:
+        raise L.IcapError("patch_embed: pos must hold S x N values")
+    call("icap_patch_embed", B, Cc, H, patch, NP, N, pixels.data_ptr(), w.data_ptr(), _ld(w), w.shape[1], _p(bias),
+         _p(pos), _p(prefix), out.data_ptr(), _ld(out), _stream())
+    return out
 
 
 def im2col_patches(pixels: Tensor, patches: Tensor, patch: int) -> Tensor:

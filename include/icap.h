@@ -394,6 +394,16 @@ int icap_im2col_patches(int32_t dtype, int32_t B, int32_t C, int32_t HW, int32_t
 /* x[b, 0] = cls + pos[0];  x[b, 1+i] = patch_emb[b*G2 + i] + pos[1+i] */
 int icap_vit_embed(int32_t dtype, int32_t B, int32_t G2, int32_t D, const void* patch_emb,
                    const float* cls, const float* pos, void* x, void* stream);
+/* Patch embedding + token assembly in one launch, for bf16 towers (round 5; replaces icap_im2col_patches + the
+ * patch GEMM + icap_vit_embed / icap_prefix_embed of HF CLIP modeling_clip.py:148-154,209-217, ViT modeling_vit.py,
+ * DINOv3 modeling_dinov3_vit.py:75-92; reached through src/embeddings/clip.py:132, vit.py:120, dino.py:166).
+ * pixels fp32 [B, C, HW, HW]; w bf16 [N][ldw] = the Conv2d weight flattened in (c, ky, kx) order, columns
+ * [C p p, Kp) zero. Rows of out (bf16, ld ldo): out[b S + r] = prefix[r] (+ pos[r]) for r < NP (fp32 prefix [NP, N]:
+ * CLS, registers) and out[b S + NP + i] = patch_i(b) . W^T (+ bias) (+ pos[NP + i]), S = NP + (HW / p)^2, patch i
+ * in row-major (py, px) order — fp32 sums, rounded once. The GEMM reads the pixels itself (no patch matrix). */
+int icap_patch_embed(int32_t B, int32_t C, int32_t HW, int32_t patch, int32_t NP, int32_t N, const float* pixels,
+                     const void* w, int64_t ldw, int32_t Kp, const float* bias, const float* pos, const float* prefix,
+                     void* out, int64_t ldo, void* stream);
 /* DINOv3 token assembly (HF/models/dinov3_vit/modeling_dinov3_vit.py:75-92; BASELINE configs[4], reference
  * src/embeddings/dino.py:166): x[b, t] = prefix[t] (t < NP: CLS, then the register tokens) or
  * patch_emb[b*G2 + t - NP] (t >= NP), plus pos[t] when pos != NULL. prefix fp32 [NP, D], pos fp32 [NP + G2, D]. */

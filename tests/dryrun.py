@@ -167,6 +167,11 @@ def accesses(name, args):
         out += [("pe", pe, B * G2 * D * ES[dt]), ("prefix", pf, NP * D * 4), ("x", x, B * (G2 + NP) * D * ES[dt])]
         if pos:
             out.append(("pos", pos, (G2 + NP) * D * 4))
+    elif name == "icap_patch_embed":
+        B, Cc, HW, p, NP, N, px, w, ldw, Kp, bias, pos, pf, o, ldo, _s = a
+        S = NP + (HW // p) ** 2
+        out += [("pixels", px, B * Cc * HW * HW * 4), ("w", w, _rows(N, ldw, Kp, 2)), ("bias", bias, N * 4),
+                ("pos", pos, S * N * 4), ("prefix", pf, NP * N * 4), ("out", o, _rows(B * S, ldo, N, 2))]
     elif name == "icap_rope_patches":
         dt, B, S, NP, H, hd, q, ld, cs, sn, _s = a
         out += [("qkv", q, _rows(B * S, ld, 2 * H * hd, ES[dt])), ("cos", cs, (S - NP) * hd * 4),

@@ -58,7 +58,9 @@ def test_dino_schedule_in_bounds():
         bad = rec.check()
         names = [c[0] for c in rec.calls]
     assert not bad, bad[:10]
-    assert names.count("icap_rope_patches") == 2 * 3 and names.count("icap_prefix_embed") == 2
+    # fp32: im2col + GEMM + icap_prefix_embed; bf16: one icap_patch_embed (the GEMM gathers the pixels itself)
+    assert names.count("icap_rope_patches") == 2 * 3 and names.count("icap_prefix_embed") == 1
+    assert names.count("icap_patch_embed") == 1 and names.count("icap_im2col_patches") == 1
 
 
 def test_load_dinov3_models_requires_both_files(tmp_path):

@@ -1,12 +1,12 @@
 """The data-parallel path on real RCCL: a world-size-1 `nccl` process group on the one GPU.
 
 CaptionTrainer built under the group broadcasts its replicas through RCCL at construction, and with
-ICAP_DP_FORCE_OVERLAP=1 takes the overlapped data-parallel step even at world size 1: each segment of the step is
+CaptionTrainer(force_overlap=True) takes the overlapped data-parallel step even at world size 1: each segment of the step is
 its own HIP graph, each segment's flat-gradient ranges are all-reduced asynchronously on the communication stream
 behind an event, and the optimizer graph waits for the handles (engine.CaptionTrainer._overlapped_step). A
 one-rank SUM all-reduce is the identity, so after every step the parameters must be BITWISE equal to the plain
 single-graph step of an identical model with no process group (same kernels, same order, same dropout counter).
-The bf16 exchange (ICAP_DP_BF16=1) rounds the sum and is checked against its own bound instead."""
+The bf16 exchange (dp_bf16=True) rounds the sum and is checked against its own bound instead."""
 
 import os
 import socket
@@ -36,8 +36,9 @@ def _batch(B, dev):
     return ids.to(dev), mask.to(dev), labels.to(dev), (emb / emb.norm(dim=-1, keepdim=True)).to(dev)
 
 
-def _run(model, batch, steps):
-    t = CaptionTrainer(model, batch[0].shape[0], 50, lr=1e-3, num_training_steps=steps + 2, dropout=True, seed=11)
+def _run(model, batch, steps, **kw):
+    t = CaptionTrainer(model, batch[0].shape[0], 50, lr=1e-3, num_training_steps=steps + 2, dropout=True, seed=11,
+                       **kw)
     t.load_batch(*batch)
     losses = []
     for _ in range(steps):
@@ -66,10 +67,9 @@ def test_overlapped_rccl_step_bitwise_equals_single_graph(dev, monkeypatch):
     t_ref, l_ref = _run(ref_model, batch, steps)  # no process group: the plain single-graph step
     assert not t_ref.distributed and not t_ref.force_overlap
 
-    monkeypatch.setenv("ICAP_DP_FORCE_OVERLAP", "1")
     with _NcclWorld1(dev):
         model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
-        t, losses = _run(model, batch, steps)
+        t, losses = _run(model, batch, steps, force_overlap=True)
     assert t.distributed and t.force_overlap and t.world == 1
     assert t.seg_graphs, "the overlapped (segment-graph + comm-stream) path did not run"
     assert losses == l_ref, (losses, l_ref)
@@ -84,11 +84,9 @@ def test_overlapped_rccl_step_bf16_exchange(dev, monkeypatch):
     ref_model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
     init = ref_model.flat().flat.clone()
     t_ref, l_ref = _run(ref_model, batch, steps)
-    monkeypatch.setenv("ICAP_DP_FORCE_OVERLAP", "1")
-    monkeypatch.setenv("ICAP_DP_BF16", "1")
     with _NcclWorld1(dev):
         model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
-        t, losses = _run(model, batch, steps)
+        t, losses = _run(model, batch, steps, force_overlap=True, dp_bf16=True)
     assert t.dp_bf16 and t.seg_graphs
     assert abs(losses[0] - l_ref[0]) == 0.0  # the first loss precedes any exchange
     upd, upd_ref = t.flat.flat - init, t_ref.flat.flat - init

@@ -241,6 +241,61 @@ def test_im2col_patches(dev, patch):
     assert torch.all(out[:, K:] == 0)
 
 
+@pytest.mark.parametrize("B,patch,NP,N,pos,bias", [(3, 32, 1, 768, True, False),    # CLIP ViT-B/32
+                                                   (2, 16, 5, 1024, False, True),   # DINOv3: CLS + 4 registers
+                                                   (2, 16, 1, 768, True, True),     # ViT-B/16
+                                                   (2, 14, 1, 1024, True, False),   # CLIP ViT-L/14 (p % 8 != 0)
+                                                   (1, 32, 1, 200, True, True)])   # ragged N (a partial column tile)
+def test_patch_embed_matches_conv(dev, B, patch, NP, N, pos, bias):
+    """icap_patch_embed (round 5: the patch GEMM gathers its pixel runs itself) vs the fp64 Conv2d of the same
+    bf16-rounded pixels and weights (HF modeling_clip.py:148-154,209-217; modeling_dinov3_vit.py:75-92) with the
+    prefix rows, bias and positions added: each output is the fp32 sum rounded once to bf16, so |err| <= |ref| 2^-8
+    (+ the accumulation-order term). And against the im2col + tile GEMM + vit_embed launches it replaces."""
+    C, HW = 3, 224
+    G = HW // patch
+    G2, K = G * G, C * patch * patch
+    Kp = (K + 7) // 8 * 8
+    S = NP + G2
+    px = rnd((B, C, HW, HW), dev, seed=81)
+    w32 = rnd((N, C, patch, patch), dev, scale=0.02, seed=82)
+    wp = torch.nn.functional.pad(w32.reshape(N, K), (0, Kp - K)).to(torch.bfloat16).contiguous()
+    pre = rnd((NP, N), dev, scale=0.5, seed=83)
+    pe = rnd((S, N), dev, scale=0.1, seed=84) if pos else None
+    b = rnd((N,), dev, scale=0.02, seed=85) if bias else None
+    out = torch.full((B * S, N), float("nan"), device=dev, dtype=torch.bfloat16)
+    ops.patch_embed(px, wp, out, patch=patch, prefix=pre, pos=pe, bias=b)
+    torch.cuda.synchronize()
+    px16 = px.to(torch.bfloat16).double().cpu()
+    w16 = wp[:, :K].double().cpu().reshape(N, C, patch, patch)
+    conv = torch.nn.functional.conv2d(px16, w16, stride=patch).flatten(2).transpose(1, 2)  # [B, G2, N]
+    if b is not None:
+        conv = conv + b.double().cpu()
+    ref = torch.cat([pre.double().cpu()[None].expand(B, NP, N), conv], 1)
+    if pe is not None:
+        ref = ref + pe.double().cpu()[None]
+    got = out.double().cpu().reshape(B, S, N)
+    err = (got - ref).abs()
+    assert torch.all(err <= ref.abs() * 2 ** -8 + 1e-4), float((err - ref.abs() * 2 ** -8).max())
+    # the prefix rows: prefix (+ pos) rounded once, exactly
+    assert torch.equal(out.reshape(B, S, N)[:, :NP].cpu(),
+                       (pre + (pe[:NP] if pe is not None else 0)).to(torch.bfloat16).cpu()[None].expand(B, NP, N))
+    # the launches it replaces (im2col + GEMM + token assembly): within two bf16 roundings
+    patches = torch.empty((B * G2, Kp), device=dev, dtype=torch.bfloat16)
+    ops.im2col_patches(px, patches, patch)
+    pe_rows = torch.empty((B * G2, N), device=dev, dtype=torch.bfloat16)
+    ops.gemm(patches, wp, pe_rows, bias=b)
+    old = torch.empty((B * S, N), device=dev, dtype=torch.bfloat16)
+    if pe is not None and NP == 1:
+        ops.vit_embed(pe_rows, pre.reshape(-1), pe, old, B, G2, N)
+    else:
+        ops.prefix_embed(pe_rows, pre, old, B, G2, N, pos=pe)
+    torch.cuda.synchronize()
+    # (the old path rounds the patch product to bf16 before adding the positions: where they cancel, its own error
+    # is |patch| 2^-8, not |result| 2^-8 — so this bound is on the largest magnitude)
+    d = (out.double() - old.double()).abs()
+    assert float(d.max()) <= float(old.double().abs().max()) * 2 ** -7
+
+
 def test_gemm_dropout_statistics(dev):
     M, N, K = 512, 512, 64
     A = torch.ones((M, K), device=dev)

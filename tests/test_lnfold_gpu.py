@@ -214,8 +214,10 @@ def test_clip_fold_vs_layernorm(dev, monkeypatch):
 
     px = torch.randn((64, 3, 224, 224), generator=torch.Generator().manual_seed(9)).to(dev)
     embs = {}
+    import icap.gpt2 as G
+
     for fold in ("1", "0"):
-        monkeypatch.setenv("ICAP_TRAIN_LN_FOLD", fold)
+        monkeypatch.setattr(G, "TRAIN_LN_FOLD", fold == "1")
         tower = CLIPVisionTower.random_init(None, seed=0).to(dev)
         core = tower.core(torch.bfloat16)
         assert core.fold == (fold == "1")

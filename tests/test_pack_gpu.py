@@ -69,7 +69,7 @@ def pack_ref(B, P, L, mask, labels):
     return seq_off, seq_len, m, km, ls, slot, ls[tgt]
 
 
-@pytest.mark.parametrize("B,P,L", [(5, 4, 9), (128, 15, 50), (1100, 3, 6)])
+@pytest.mark.parametrize("B,P,L", [(5, 4, 9), (128, 15, 50), (1100, 3, 6), (40, 0, 70), (2100, 2, 5)])
 def test_caption_pack_layout(dev, B, P, L):
     ids, mask, labels, _ = ragged_batch(B, L, 100, 99, 8, seed=B)
     S = P + L

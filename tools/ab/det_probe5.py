@@ -62,7 +62,10 @@ _lnb = ops.layernorm_bwd
 DUP = os.environ.get("PROBE_LN2_DUP") == "1"      # LN2 launched a second time into a spare per-layer buffer
 NOPAR = os.environ.get("PROBE_LN_NOPARAMS") == "1"  # LN backward without dgamma / dbeta (dx only)
 SYNC = os.environ.get("PROBE_SYNC_LN2") == "1"    # device-wide synchronize before every LN2 (no concurrency there)
+CLONES = os.environ.get("PROBE_INPUT_CLONES") == "1"  # stream-ordered copies of LN2's inputs before and after it
+clones = {}
 dups = [torch.empty_like(sp._ws.g_rm[0]) for _ in range(nl)]
+replay = {}
 ln_count = [0]
 
 
@@ -75,10 +78,17 @@ def lnb(x, gamma, mean, rstd, dy, dx, **kw):
         kw = dict(kw, dgamma=None, dbeta=None)
     if ln2 and SYNC:
         torch.cuda.synchronize()
+    ins = None
+    if ln2 and CLONES:
+        ins = {"x": x, "gamma": gamma, "mean": mean, "rstd": rstd, "dy": dy, "dres": kw.get("dres")}
+        clones[li[0]] = {"pre": {k: v.clone() for k, v in ins.items()}, "ref": ins}
     r = _lnb(x, gamma, mean, rstd, dy, dx, **kw)
+    if ins is not None:
+        clones[li[0]]["post_orig"] = {k: v.clone() for k, v in ins.items()}
     if ln2 and DUP:
         kd = dict(kw, dgamma=None, dbeta=None, dx_drop=None)
         _lnb(x, gamma, mean, rstd, dy, dups[nl - 1 - li[0]], **kd)
+        replay[li[0]] = (x, gamma, mean, rstd, dy, kd)  # for a quiet recomputation after the step
     return r
 
 
@@ -106,7 +116,23 @@ def dup_vs_orig():
         return ""
     w = sp._ws
     nd = [int((dups[j] != w.g_rm[nl - 1 - j]).sum()) for j in range(nl)]
-    return f" dup-vs-orig differing elements per layer (top first) {nd}"
+    msg = f" dup-vs-orig differing elements per layer (top first) {nd}"
+    # which one is right: the same launch again with nothing running beside it
+    for j in range(nl):
+        if not nd[j]:
+            continue
+        l = nl - 1 - j
+        x, gamma, mean, rstd, dy, kd = replay[l]
+        quiet = torch.empty_like(dups[j])
+        _lnb(x, gamma, mean, rstd, dy, quiet, **kd)
+        torch.cuda.synchronize()
+        o, d = w.g_rm[l], dups[j]
+        rows = (o != d).any(1).nonzero().flatten().tolist()
+        per_row = [int((o[r] != d[r]).sum()) for r in rows[:6]]
+        msg += (f"\n  layer {l}: {len(rows)} rows differ {rows[:6]} (elements per row {per_row} of {o.shape[1]}); "
+                f"orig == quiet: {torch.equal(o, quiet)}, dup == quiet: {torch.equal(d, quiet)}; "
+                f"orig rows != quiet: {int((o != quiet).any(1).sum())}, dup rows != quiet: {int((d != quiet).any(1).sum())}")
+    return msg
 
 
 snaps = []
@@ -117,6 +143,18 @@ for i in range(CALLS):
     torch.cuda.synchronize()
     snaps.append(snapshot())
     print(f"call {i + 1}:{dup_vs_orig()}", flush=True)
+    if CLONES:
+        for l in sorted(clones, reverse=True):
+            c = clones[l]
+            ch = [k for k in c["pre"] if not torch.equal(c["pre"][k], c["post_orig"][k]) or
+                  not torch.equal(c["pre"][k], c["ref"][k])]
+            if ch:
+                print(f"  layer {l} LN2 inputs changed (pre / after LN2 / end of step): {ch}", flush=True)
+        if i > 0:
+            ch = [(l, k) for l in clones for k in clones[l]["pre"]
+                  if not torch.equal(clones[l]["pre"][k], prev_clones[l]["pre"][k])]
+            print(f"  LN2 inputs that differ from the previous call (as read): {sorted(ch, reverse=True)[:12]}", flush=True)
+        prev_clones = {l: {"pre": dict(c["pre"])} for l, c in clones.items()}
 
 bad = 0
 for i in range(1, CALLS):
