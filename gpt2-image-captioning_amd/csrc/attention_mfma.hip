@@ -387,12 +387,16 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
   const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
   const bf16_t* dout = reinterpret_cast<const bf16_t*>(p.dout);
   const bf16_t* outp = reinterpret_cast<const bf16_t*>(p.out);
-  for (int r = threadIdx.x; r < Sp; r += blockDim.x) {
-    lse_s[r] = r < S ? p.lse[(int64_t)bh * SS + r] : -INFINITY;
-    delta_s[r] = 0.f;
-    kok_s[r] = (r < S && (p.key_mask == nullptr || p.key_mask[g.kmb + r] != 0)) ? 1 : 0;
+  // per-row lse / key mask: loaded here, stored to LDS after the staging loads below are issued, under the same
+  // barrier (round 5: a barrier and a dependent round trip of their own before). Sp = Sp32 <= Sp16 + 16 <= blockDim
+  // = 4 Sp16, so one row per thread.
+  const int rr = threadIdx.x;
+  float lse_r = -INFINITY;
+  uint8_t kok_r = 0;
+  if (rr < S) {
+    lse_r = p.lse[(int64_t)bh * SS + rr];
+    kok_r = (p.key_mask == nullptr || p.key_mask[g.kmb + rr] != 0) ? 1 : 0;
   }
-  __syncthreads();
   // CPR a power of two (HD 64 / 128): delta[q] = sum_d dO[q][d] O[q][d] fused into the staging loop, the CPR
   // chunk partials of a row summed across its CPR consecutive lanes (block size and the loop bound are multiples
   // of CPR, so a row's lanes are active together); otherwise one thread per query after it. Fixed order either way.
@@ -440,6 +444,11 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
         if (c == 0 && r < S) delta_s[r] = part;
       }
     }
+  }
+  if (rr < Sp) {
+    lse_s[rr] = lse_r;
+    kok_s[rr] = kok_r;
+    if (rr >= S) delta_s[rr] = 0.f;  // (rows < S: written by the fused staging loop or the per-query sums below)
   }
   if constexpr (!FUSED_DELTA) {
     for (int r = threadIdx.x; r < S; r += blockDim.x) {
@@ -600,6 +609,13 @@ __global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint
   bf16_t* Ks = sm;
   bf16_t* Vs = Ks + Sp * LDR;
   const bf16_t* qkv = reinterpret_cast<const bf16_t*>(p.qkv);
+  const int qt = wave;
+  // Q fragments of this query tile straight from HBM/L2 (B operand: rows = queries), issued before the K / V
+  // staging loads so both are one memory round trip (round 5: they were a second dependent trip after the barrier;
+  // gfrag clamps its rows, so the waves past S load valid addresses and exit below)
+  uint4 qf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) qf[ks] = gfrag(qkv, p.ld_qkv, h * HD, g, b, qt * 16, ks * 32, lane);
   for (int idx = threadIdx.x; idx < Sp * CPR; idx += blockDim.x) {
     const int r = idx / CPR, c = idx - r * CPR;
     uint4 k = make_uint4(0, 0, 0, 0), v = k;
@@ -612,13 +628,8 @@ __global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint
     *reinterpret_cast<uint4*>(Vs + r * LDR + 8 * c) = v;
   }
   __syncthreads();
-  const int qt = wave;
   if (qt * 16 >= S) return;  // (packed sequences shorter than the launch's S; no barrier follows)
   const int q = qt * 16 + fr;
-  // Q fragments of this query tile straight from HBM/L2 (B operand: rows = queries)
-  uint4 qf[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) qf[ks] = gfrag(qkv, p.ld_qkv, h * HD, g, b, qt * 16, ks * 32, lane);
   const int npair = Sp >> 5;
   const int kp1 = p.causal ? ((qt * 16 + 15) >> 5) + 1 : npair;
   const int np = kp1 < npair ? kp1 : npair;

@@ -544,7 +544,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
           for (int pos = 1; pos < 4; ++pos) {
             if (pos < splits) {
               const f32x4_t x = pos < split ? v[pos][ii][j] : (pos == split ? own : v[pos - 1][ii][j]);
-              t += x;
+#pragma unroll
+              for (int c = 0; c < 4; ++c) t[c] += x[c];  // per component: no packed-FP32 op
             }
           }
           acc[i0 + ii][j] = t;

@@ -211,13 +211,12 @@ constexpr int LN8_DMAX = 6 * 32 * 8;
 
 // Sum over a 32-lane half-wave, in every lane of it, on the VALU's cross-lane paths (round 5): DPP quad_perm for
 // lane ^ 1 and ^ 2, row_half_mirror (i <-> 7 - i: the other quad of each 8), row_ror:8 (lane ^ 8 within a 16-lane
-// row) and v_permlane16_swap for the other row of the half. The __shfl_xor butterfly it replaces lowered to
-// ds_bpermute_b32 (the LDS crossbar, 5 dependent round trips): with the mapper's K-outer weight-gradient GEMMs
-// co-resident on the same CUs (the side-stream schedule, tools/ab/det_probe5.py) that form returned slightly wrong
-// row sums for a few rows per launch — the same launch repeated on the same inputs disagreed with itself
-// (profiles/r05_side_stream_probe5.txt). The operation order is fixed and lane-independent, so every lane of the
-// half holds the same bits. Both halves of a wave must be active or inactive together (the row loops are uniform
-// per half).
+// row) and v_permlane16_swap for the other row of the half (the __shfl_xor butterfly it replaces lowered to
+// ds_bpermute_b32: 5 LDS round trips). The operation order is fixed and lane-independent, so every lane of the half
+// holds the same bits. Both halves of a wave must be active or inactive together (the row loops are uniform per
+// half). (The side-stream nondeterminism first blamed on the bpermute form was the packed-FP32 instructions of the
+// row arithmetic, not this sum: the readlane, bpermute and DPP forms all failed the same way with them and none
+// does without them — Makefile, DESIGN.md "Concurrency: the packed-FP32 race".)
 __device__ __forceinline__ float half_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));   // ^1
   v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));   // ^2
@@ -327,22 +326,31 @@ __global__ __launch_bounds__(256) void ln_bwd8_kernel(int64_t rows, int D, const
       for (int e = 0; e < 8; ++e) dg[t][e] = db[t][e] = 0.f;
   }
   for (int64_t r = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5); r < rows; r += nr) {
-    const float mean = mean_in[r], rs = rstd_in[r];
-    const int64_t dyr = dy_rowmap ? (int64_t)dy_rowmap[r] : r;
+    // every load of the row is issued unconditionally, from a valid row (a gathered row < 0 reads row 0, a missing
+    // dres re-reads x), and the values are selected afterwards: the data-dependent branches around each load made
+    // hipcc wait for every load before issuing the next (a serial chain of 9 round trips per row)
+    const int64_t dyr0 = dy_rowmap ? (int64_t)dy_rowmap[r] : r;
+    const bool dy_ok = dyr0 >= 0, has_res = dres != nullptr;
+    const T* xp = x + r * ldx;
+    const T* dp = dy + (dy_ok ? dyr0 : 0) * lddy;
+    const T* rp = has_res ? dres + r * lddres : xp;
     float xv[LN8_MAXC][8], dv[LN8_MAXC][8], rv[LN8_MAXC][8];
 #pragma unroll
     for (int t = 0; t < LN8_MAXC; ++t) {
-      const int g = hl + 32 * t;
-      if (g < D8) {
-        io<T>::ld8(x + r * ldx + 8 * g, xv[t]);
-        if (dyr >= 0) io<T>::ld8(dy + dyr * lddy + 8 * g, dv[t]);
-        else
+      const int g = hl + 32 * t, gc = g < D8 ? g : D8 - 1;  // (chunks past D re-read the last one; zeroed below)
+      io<T>::ld8(xp + 8 * gc, xv[t]);
+      io<T>::ld8(dp + 8 * gc, dv[t]);
+      io<T>::ld8(rp + 8 * gc, rv[t]);
+    }
+    const float mean = mean_in[r], rs = rstd_in[r];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) dv[t][e] = 0.f;
-        if (dres) io<T>::ld8(dres + r * lddres + 8 * g, rv[t]);
-        else
+    for (int t = 0; t < LN8_MAXC; ++t) {
+      const bool in = hl + 32 * t < D8;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) rv[t][e] = 0.f;
+      for (int e = 0; e < 8; ++e) {
+        xv[t][e] = in ? xv[t][e] : 0.f;
+        dv[t][e] = (in && dy_ok) ? dv[t][e] : 0.f;
+        rv[t][e] = (in && has_res) ? rv[t][e] : 0.f;
       }
     }
     float s1 = 0.f, s2 = 0.f;

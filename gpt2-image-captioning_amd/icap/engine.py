@@ -10,7 +10,6 @@ trainable weights is written by the AdamW kernel itself.
 
 from __future__ import annotations
 
-import os
 from types import SimpleNamespace
 from typing import List, Optional, Tuple
 
@@ -28,9 +27,6 @@ SHORT_ONLY = True
 # micro-batch) instead of zeroing the flat gradient buffer and accumulating into it; False restores the zero_() +
 # accumulate form
 GRAD_OVERWRITE = True
-# the transformer mapper's dW products of a layer unsplit and side by side on four streams at the end of its backward
-# step (mapper.backward_steps group=) instead of split-K + reduce in series inside the step (A/B switch)
-GROUP_DW = os.environ.get("ICAP_GROUP_DW", "0") == "1"
 
 Tensor = torch.Tensor
 
@@ -40,11 +36,16 @@ class CaptionTrainer:
                  betas=(0.9, 0.999), eps: float = 1e-8, max_norm: float = 1.0, num_warmup_steps: int = 0,
                  num_training_steps: int = 1, dropout: bool = True, seed: int = 0, clip_model=None,
                  grad_accum_steps: int = 1, process_group=None, compact_head: bool = True,
-                 pack_rows: bool = True, dp_overlap: bool = True, dp_bf16: bool = False, force_overlap: bool = False):
+                 pack_rows: bool = True, dp_overlap: bool = True, dp_bf16: bool = False, force_overlap: bool = False,
+                 mapper_dw: str = "serial"):
         """pack_rows: packed token rows (GPT2Core.alloc_train); dp_overlap: with N > 1 ranks, all-reduce each backward
         segment's gradient bucket beside the later segments (False: one whole-buffer all-reduce after the backward);
         dp_bf16: exchange the gradients as bf16 (half the bytes; rounds the sum over ranks); force_overlap: take the
-        bucketed communication-stream step at world size 1 too (exercises the RCCL calls on one GPU)."""
+        bucketed communication-stream step at world size 1 too (exercises the RCCL calls on one GPU).
+        mapper_dw (transformer mapper, GPU): where its weight-gradient products run — "serial" (in the dX chain,
+        split-K), "side" (a second stream beside the dX chain) or "group" (a layer's four products unsplit on four
+        streams at the end of its step). All three give the same gradients; neither alternative measured faster than
+        "serial" (DESIGN.md "Concurrency: the packed-FP32 race"), which stays the default."""
         self.model = model
         self.dtype = model.compute_dtype
         self.B, self.Lc = batch_size, caption_len
@@ -150,18 +151,17 @@ class CaptionTrainer:
         self.gdr = self.gcore.drops(dropout, seed, self.counter, self.gws.M, B, self.gws.S)
         p_map = 0.1 if isinstance(self.mcore, TransformerMapperCore) else 0.0
         self.mdr = self.mcore.drops(dropout, p_map, seed, self.counter, B)
-        # the mapper's weight-gradient products on a side stream beside its dX chain (mapper.backward_steps):
-        # opt-in (ICAP_SIDE_DW=1) — measured nondeterministic under concurrency, so off
+        if mapper_dw not in ("serial", "side", "group"):
+            raise ValueError(f"mapper_dw must be 'serial', 'side' or 'group', not {mapper_dw!r}")
+        multi = self.dev.type == "cuda" and isinstance(self.mcore, TransformerMapperCore)
+        # the mapper's weight-gradient products on a side stream beside its dX chain (mapper.backward_steps side=)
         self._side = None
-        if (self.dev.type == "cuda" and isinstance(self.mcore, TransformerMapperCore)
-                and os.environ.get("ICAP_SIDE_DW", "0") == "1"):
+        if multi and mapper_dw == "side":
             self._side = torch.cuda.Stream(self.dev)
             ops.register_side_stream(self._side)
-        # the mapper's four dW products of a layer unsplit and side by side on three more streams (mapper.
-        # backward_steps group=): ICAP_GROUP_DW
+        # the mapper's four dW products of a layer unsplit and side by side on three more streams (group=)
         self._group = None
-        if (self.dev.type == "cuda" and isinstance(self.mcore, TransformerMapperCore) and self._side is None
-                and GROUP_DW and self.dtype == torch.bfloat16):
+        if multi and mapper_dw == "group" and self.dtype == torch.bfloat16:
             self._group = [torch.cuda.Stream(self.dev) for _ in range(3)]
             for sd in self._group:
                 ops.register_side_stream(sd)
@@ -185,8 +185,10 @@ class CaptionTrainer:
         if self.gws.pack and SHORT_ONLY:
             # every packed sequence of THIS batch <= 32 tokens: the attention launches skip their long-sequence pass
             # (icap_attn_args.short_only — a guarantee, so it is taken from each batch's labels, and the captured
-            # graphs are keyed on it)
-            self.gws.short_only = max_seq_len(labels, self.P) <= 32
+            # graphs are keyed on it). Read from host labels only (the data loaders deliver CPU tensors): for labels
+            # already on the device the flag stays off (both passes launched; same results) rather than forcing a
+            # device-to-host sync per batch
+            self.gws.short_only = labels.device.type == "cpu" and max_seq_len(labels, self.P) <= 32
         self.ids.copy_(ids, non_blocking=True)
         self.mask.copy_(mask, non_blocking=True)
         self.labels.copy_(labels, non_blocking=True)

@@ -9,7 +9,6 @@ explicit forward/backward kernel schedule of `TransformerMapperCore` /
 from __future__ import annotations
 
 import math
-import os
 from types import SimpleNamespace
 from typing import Optional
 
@@ -34,19 +33,6 @@ def _rup(x: int, m: int) -> int:
 def _kout_ok(t: Tensor) -> bool:
     """K-outer GEMM operand requirements: 16-byte aligned base, row stride a multiple of 8 elements."""
     return t.data_ptr() % 16 == 0 and t.stride(0) % 8 == 0 and t.stride(-1) == 1
-
-
-_SIDE_SERIAL = os.environ.get("ICAP_SIDE_SERIAL", "0") == "1"  # diagnostic only (mapper.backward_steps)
-_DB_BATCH = os.environ.get("ICAP_DB_BATCH", "1") != "0"  # A/B: 0 = one icap_colsum per bias (two launches each)
-_SIDE_DIAG = os.environ.get("ICAP_SIDE_DIAG", "")  # diagnostic only: "scratch" / "no_dw" / "no_db"
-_SCRATCH = {}
-
-
-def _scratch(t: Tensor) -> Tensor:
-    k = (tuple(t.shape), t.dtype)
-    if k not in _SCRATCH:
-        _SCRATCH[k] = torch.zeros_like(t)
-    return _SCRATCH[k]
 
 
 class DWHelper:
@@ -464,15 +450,8 @@ class TransformerMapperCore:
             main = torch.cuda.current_stream()
             order(side, main)
             with torch.cuda.stream(side):
-                if _SIDE_DIAG == "scratch":  # diagnostic: the same launches into scratch outputs
-                    w_out = _scratch(w_out)
-                    b_out = _scratch(b_out)
-                if _SIDE_DIAG != "no_dw":
-                    dwh.dW(dy, x, w_out, M=M, accumulate=acc)
-            if _SIDE_DIAG != "no_db":
-                st.db.append((dy, b_out))
-            if _SIDE_SERIAL:  # diagnostic: the side stream, but joined after every fork (no concurrency)
-                order(main, side)
+                dwh.dW(dy, x, w_out, M=M, accumulate=acc)
+            st.db.append((dy, b_out))
 
         def flush_dw():
             """The layer's queued dW products, unsplit and side by side (group streams forked from the main stream
@@ -494,10 +473,7 @@ class TransformerMapperCore:
             """The layer's bias gradients in one icap_colsum_batch (2 launches instead of 2 per bias)."""
             if not st.db:
                 return
-            if not _DB_BATCH:
-                for dy, b_out in st.db:
-                    dwh.db(dy, b_out, M=M, accumulate=acc)
-            elif side is None:
+            if side is None:
                 dwh.db_batch(st.db, M, accumulate=acc)
             else:
                 order(side, torch.cuda.current_stream())

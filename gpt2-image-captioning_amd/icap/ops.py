@@ -325,6 +325,7 @@ def register_side_stream(stream) -> None:
 
 GEMM_TIMER = None  # set to an object with .launch(key, flops, fn) to time every GEMM (and attention) launch
 TIMER_TAG = None  # label the timer records of the launches issued inside timer_tag(...) (bench roofline groups)
+TAG_HOOK = None  # bench.py: callable(tag, entering) run at each timer_tag boundary (marker launches in a graph)
 
 
 @contextlib.contextmanager
@@ -332,10 +333,14 @@ def timer_tag(tag: str):
     """Label every launch GEMM_TIMER records in this block (e.g. "gpt2_block": bench.py's GPT-2-block roofline)."""
     global TIMER_TAG
     old, TIMER_TAG = TIMER_TAG, tag
+    if TAG_HOOK is not None:
+        TAG_HOOK(tag, True)
     try:
         yield
     finally:
         TIMER_TAG = old
+        if TAG_HOOK is not None:
+            TAG_HOOK(tag, False)
 
 
 def _timed(kind: str, desc: str, flops: Optional[float], fn) -> None:

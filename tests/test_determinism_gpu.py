@@ -47,6 +47,10 @@ def _noise(dev, n):
     # a split-K shape with the DEFAULT workspace (one per stream since r03: the noise stream gets its own slabs)
     sa = torch.randn((256, 8192), device=dev).to(torch.bfloat16)
     sc = torch.empty((256, 512), device=dev, dtype=torch.bfloat16)
+    # the 128 x 128 tile family (row-major and K-outer): the co-resident waves that exposed the packed-FP32 race
+    ta, tw = torch.randn((800, 768), device=dev).to(torch.bfloat16), torch.randn((3072, 768), device=dev).to(torch.bfloat16)
+    tc = torch.empty((800, 3072), device=dev, dtype=torch.bfloat16)
+    tf, tdw = torch.randn((800, 3072), device=dev).to(torch.bfloat16), torch.empty((768, 3072), device=dev)
     torch.cuda.synchronize(dev)
 
     def launch():
@@ -54,6 +58,8 @@ def _noise(dev, n):
             for i in range(n):
                 ops.gemm(a, a, c)
                 ops.gemm(sa, sa[:512], sc)
+                ops.gemm(ta, tw, tc)
+                ops.gemm(ta, tf, tdw, M=768, N=3072, K=800, trans_ab=True)
     return launch, s
 
 
@@ -85,3 +91,36 @@ def test_train_step_bitwise_with_concurrent_stream(dev, B):
                             f"(NaN before {int(a[diff].isnan().sum())}, now {int(b[diff].isnan().sum())}), rows "
                             f"{rows[:8]} ({len(rows)}), n_valid {int(t.gws.n_valid.item())}, max finite |d| "
                             f"{float(d[d.isfinite()].max()) if d.isfinite().any() else 0.0:.3g}")
+
+
+def test_layernorm_bwd_exact_beside_tile_gemms(dev):
+    """The round-5 race in isolation (tools/ab/ln_race_probe.py): the mapper-shaped LayerNorm backward (800 x 768
+    bf16, dgamma / dbeta partials, residual gradient) launched 40 times per rep on the main stream while tile and
+    K-outer GEMMs run on a second stream; every output bitwise equal to the quiet launch. With packed-FP32
+    instructions in the library ~5 % of these launches had rows off by up to an ulp."""
+    g = torch.Generator().manual_seed(0)
+    M, D = 800, 768
+    bf = lambda *sh, sc=1.0: (torch.randn(sh, generator=g) * sc).to(dev, torch.bfloat16)  # noqa: E731
+    x, dy, dres = bf(M, D), bf(M, D, sc=1e-4), bf(M, D, sc=1e-4)
+    gamma = (1 + 0.1 * torch.randn(D, generator=g)).to(dev)
+    mean = (0.1 * torch.randn(M, generator=g)).to(dev)
+    rstd = (1 + 0.1 * torch.rand(M, generator=g)).to(dev)
+    ws = torch.empty(ops.layernorm_bwd_workspace(M, D), dtype=torch.uint8, device=dev)
+    dg, db = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+    run = lambda o: ops.layernorm_bwd(x, gamma, mean, rstd, dy, o, dres=dres, dgamma=dg, dbeta=db, workspace=ws)  # noqa: E731
+    launch, s = _noise(dev, 8)
+    ops.register_side_stream(s)
+    launch()
+    torch.cuda.synchronize(dev)
+    ref = torch.empty_like(x)
+    run(ref)
+    torch.cuda.synchronize(dev)
+    outs = [torch.empty_like(x) for _ in range(40)]
+    bad = []
+    for rep in range(5):
+        launch()
+        for o in outs:
+            run(o)
+        torch.cuda.synchronize(dev)
+        bad += [(rep, i, (o != ref).any(1).nonzero().flatten()[:4].tolist()) for i, o in enumerate(outs) if not torch.equal(o, ref)]
+    assert not bad, f"{len(bad)} of 200 launches differ from the quiet one: {bad[:4]}"

@@ -1,4 +1,4 @@
-"""Grouped mapper weight gradients (engine.GROUP_DW, mapper.backward_steps group=): a layer's four K-outer dW
+"""Grouped mapper weight gradients (CaptionTrainer(mapper_dw="group"), mapper.backward_steps group=): a layer's four K-outer dW
 products queued at the end of its backward step, unsplit, one on the main stream and three on registered side
 streams, joined before the next layer. Checked: the gradients equal the serial split-K schedule's to fp32 summation
 order (rel 1e-5 of the largest entry: the same bf16 products, a different K-sum order), the schedule is bitwise
@@ -21,10 +21,9 @@ def _batch(seed, dev, B=6, L=14):
 
 
 def _trainer(dev, monkeypatch, group):
-    import icap.engine as E
-    monkeypatch.setattr(E, "GROUP_DW", group)
     model = build(TINY_G, TINY_M, torch.bfloat16, dev)
-    t = CaptionTrainer(model, 6, 14, lr=1e-3, num_training_steps=8, dropout=True, seed=3)
+    t = CaptionTrainer(model, 6, 14, lr=1e-3, num_training_steps=8, dropout=True, seed=3,
+                       mapper_dw="group" if group else "serial")
     assert (t._group is not None) == group
     return t
 
@@ -61,3 +60,30 @@ def test_grouped_dw_graph_equals_eager(dev, monkeypatch):
         torch.cuda.synchronize()
         out.append(t.flat.flat.clone())
     assert torch.equal(out[0], out[1])
+
+
+def test_side_dw_bitwise_serial(dev):
+    """mapper_dw="side": the weight-gradient products run beside the dX chain on a second stream. Each is the same
+    kernel on the same operands as in the serial schedule, so the flat gradient is bitwise the serial one, on every
+    call (round 5: before the library dropped packed-FP32 instructions, the LayerNorm backward co-resident with these
+    products broke this — DESIGN.md "Concurrency: the packed-FP32 race")."""
+    from test_determinism_gpu import _batch
+
+    from icap import CaptionTrainer as T
+
+    out = {}
+    for mode in ("serial", "side"):
+        model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
+        t = T(model, 32, 50, lr=1e-4, num_training_steps=10, dropout=False, mapper_dw=mode)
+        assert (t._side is not None) == (mode == "side")
+        t.load_batch(*_batch(32, dev))
+        grads = []
+        for _ in range(4 if mode == "side" else 1):
+            t._fwd_bwd(True, 1.0)
+            torch.cuda.synchronize()
+            grads.append(t.flat.flat_grad.clone())
+        out[mode] = grads
+        del t, model
+    ref = out["serial"][0]
+    for i, gr in enumerate(out["side"]):
+        assert torch.equal(gr, ref), f"side call {i}: {int((gr != ref).sum())} gradient entries differ"

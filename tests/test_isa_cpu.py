@@ -1,0 +1,38 @@
+"""CPU-only: properties of the built gfx950 code objects in libicap_hip.so (llvm-objdump on the bundles).
+
+No VOP3P packed-FP32 instruction (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32) in any kernel: with them a kernel
+co-resident with tile-GEMM waves returned slightly wrong rows (DESIGN.md "Concurrency: the packed-FP32 race", tools/ab/ln_race_probe.py); the
+Makefile compiles with -fno-slp-vectorize -fno-vectorize and the sources use no float2 / float4 vector arithmetic."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "..", "gpt2-image-captioning_amd", "icap", "libicap_hip.so")
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+
+def _code_objects(tmp_path):
+    if not os.path.exists(OBJDUMP):
+        pytest.skip("llvm-objdump not available")
+    if not os.path.exists(LIB):
+        pytest.skip("libicap_hip.so not built")
+    lib = tmp_path / "lib.so"
+    shutil.copy(LIB, lib)  # --offloading writes the bundles next to its input
+    subprocess.run([OBJDUMP, "--offloading", str(lib)], check=True, capture_output=True, cwd=tmp_path)
+    objs = sorted(p for p in tmp_path.iterdir() if p.name.endswith("gfx950"))
+    assert objs, "no gfx950 code object in libicap_hip.so"
+    return objs
+
+
+def test_no_packed_fp32(tmp_path):
+    bad = {}
+    for o in _code_objects(tmp_path):
+        dis = subprocess.run([OBJDUMP, "-d", str(o)], check=True, capture_output=True, text=True).stdout
+        n = len(re.findall(r"\bv_pk_(?:add|mul|fma)_f32\b", dis))
+        if n:
+            bad[o.name] = n
+    assert not bad, f"packed-FP32 instructions in {bad}"

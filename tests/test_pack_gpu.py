@@ -273,7 +273,7 @@ def test_trainer_short_only_switches_graphs(dev, monkeypatch):
         assert E.max_seq_len(labels, P) <= 32 and E.max_seq_len(long_[2], P) > 32
         losses = []
         for ids_, mask_, labels_, emb_ in (short, long_, short, long_, short):
-            t.load_batch(ids_.to(dev), mask_.to(dev), labels_.to(dev), emb_.to(dev))
+            t.load_batch(ids_, mask_, labels_, emb_.to(dev))  # host labels: the trainer reads short_only from them
             t.micro_step(use_graph=True)
             losses.append(t.last_loss.item())
         out[flag] = losses

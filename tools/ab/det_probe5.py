@@ -23,7 +23,8 @@ dev = torch.device("cuda", 0)
 B = int(os.environ.get("PROBE_B", "32"))
 CALLS = int(os.environ.get("PROBE_CALLS", "6"))
 model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
-t = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10, dropout=False)
+t = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=10, dropout=False,
+                   mapper_dw="side" if os.environ.get("ICAP_SIDE_DW") == "1" else "serial")
 tag = " ".join(f"{k}={os.environ[k]}" for k in sorted(os.environ) if k.startswith(("ICAP_", "PROBE_")))
 print("variant:", tag or "(defaults)", "side", t._side is not None, flush=True)
 t.load_batch(*_batch(B, dev))
