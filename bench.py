@@ -463,70 +463,65 @@ def kernel_peak(name: str) -> float:
     return FP8_PEAK_TFLOPS if "fp8_t" in name else BF16_PEAK_TFLOPS
 
 
-def _kernel_name(name: str) -> str:
-    """profiler kernel name -> the instantiation name rocprofv3 / icap_gemm_kernel_name report"""
-    name = name.split("(")[0].strip()
-    return name[5:] if name.startswith("void ") else name
-
-
-def replay_roofline(trainer, dom, reps=3):
-    """Kernel durations inside the replayed step graph: the step is captured once more with a
-    marker kernel (torch.cuda._sleep(1), ~1 us) at each boundary of the GPT-2-block region (ops.TAG_HOOK at
-    ops.timer_tag("gpt2_block")), replayed `reps` times under torch.profiler (device timestamps of every kernel of
-    the replay), and read back: the dominant instantiation's launches over the whole step, and the GEMM + attention
-    kernels between the markers (the LayerNorm kernels there excluded, as the eager tagged group does). ROCm graphs
-    refuse timing-event nodes ("External events are disallowed"), hence the profiler."""
-    from torch.profiler import ProfilerActivity, profile
-
+def replay_roofline(trainer, dom, reps=20):
+    """Kernel time inside the replayed step graph, by difference: the step is captured twice
+    more, once with every launch of the dominant instantiation left out and once with every GEMM / attention launch
+    of the GPT-2-block region left out (ops.GEMM_TIMER hook: the launch function is simply not called), and each of
+    the three graphs is replayed `reps` times back to back between HIP events on the capture stream. The full
+    graph's median replay minus a reduced graph's is the time those launches occupy in the step as it is timed
+    (kernel durations plus their share of dispatch gaps; the work on one stream runs in series, so nothing they
+    overlap is lost). Kernel times do not depend on the values the skipped launches would have written. ROCm graphs
+    refuse timing-event nodes ("External events are disallowed"), and the profiler's kernel records of a graph
+    replay were incomplete here, hence the difference."""
     from icap import ops
 
-    def kernels(run):
-        with profile(activities=[ProfilerActivity.CUDA]) as p:
-            run()
-            torch.cuda.synchronize()
-        out = [(e.time_range.start, e.time_range.elapsed_us(), _kernel_name(e.name)) for e in p.events()
-               if e.device_type == torch.autograd.DeviceType.CUDA]
-        return sorted(out)
+    class _Skip:
+        def __init__(self, pred):
+            self.pred, self.n = pred, 0
 
-    torch.cuda.synchronize()
+        def launch(self, key, flops, fn):
+            if self.pred(key, ops.TIMER_TAG):
+                self.n += 1
+            else:
+                fn()
+
+    def capture(timer):
+        torch.cuda.synchronize()
+        ops.GEMM_TIMER = timer
+        try:
+            g = torch.cuda.CUDAGraph()
+            with ops.graph_capture(g):  # forward + backward only: no optimizer step, the parameters stay as they are
+                trainer._fwd_bwd(True, trainer.grad_scale())
+        finally:
+            ops.GEMM_TIMER = None
+        return g
+
+    def median_replay(g):
+        g.replay()
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+        ev[0].record()
+        for k in range(reps):
+            g.replay()
+            ev[k + 1].record()
+        torch.cuda.synchronize()
+        t = sorted(ev[k].elapsed_time(ev[k + 1]) for k in range(reps))
+        return t[reps // 2]
+
     try:
-        mk = kernels(lambda: torch.cuda._sleep(1))
-        if not mk:
-            return {"error": "torch.profiler recorded no device kernels"}
-        marker = mk[-1][2]
-        ops.TAG_HOOK = lambda tag, entering: torch.cuda._sleep(1) if tag == "gpt2_block" else None
-        g = torch.cuda.CUDAGraph()
-        with ops.graph_capture(g):
-            trainer._fwd_bwd(True, trainer.grad_scale())
-            if trainer.world == 1:
-                trainer._optimizer()
+        skip_dom = _Skip(lambda key, tag: key[0] == dom)
+        skip_blk = _Skip(lambda key, tag: tag == "gpt2_block")
+        graphs = {"full": capture(_Skip(lambda key, tag: False)), "no_dom": capture(skip_dom),
+                  "no_block": capture(skip_blk)}
+        ms = {k: median_replay(g) for k, g in graphs.items()}
+        del graphs
     except Exception as e:  # noqa: BLE001 (reported in the bench line, the eager figure stands)
+        ops.GEMM_TIMER = None
         torch.cuda.synchronize()
         return {"error": f"{type(e).__name__}: {e}"[:200]}
-    finally:
-        ops.TAG_HOOK = None
-    g.replay()
-    torch.cuda.synchronize()
-
-    def run():
-        for _ in range(reps):
-            g.replay()
-
-    ks = kernels(run)
-    del g
-    d_n = sum(1 for _, _, n in ks if n == dom)
-    d_us = sum(us for _, us, n in ks if n == dom)
-    b_n, b_us, inside, n_mark = 0, 0.0, False, 0
-    for _, us, n in ks:
-        if n == marker:
-            inside, n_mark = not inside, n_mark + 1
-        elif inside and "ln_" not in n and "layernorm" not in n:
-            b_n, b_us = b_n + 1, b_us + us
-    if d_n == 0:
-        return {"error": f"no {dom} kernel among the {len(ks)} profiled kernels of the replay"}
-    return {"dom_launches": d_n / reps, "dom_ms": d_us / reps * 1e-3, "block_kernels": b_n / reps,
-            "block_ms": b_us / reps * 1e-3, "markers": n_mark / reps, "kernels_per_step": len(ks) / reps,
-            "reps": reps, "timing": "torch.profiler device timestamps of the replayed step graph"}
+    return {"dom_launches": skip_dom.n, "dom_ms": ms["full"] - ms["no_dom"], "block_launches": skip_blk.n,
+            "block_ms": ms["full"] - ms["no_block"], "replay_ms": ms, "reps": reps,
+            "timing": "median graph replay, full minus the graph without those launches"}
 
 
 def train_rate(trainer, B, steps, warmup, use_graph, world, dev, detail=False):
@@ -598,7 +593,7 @@ def train_rate(trainer, B, steps, warmup, use_graph, world, dev, detail=False):
         # the graph-replay durations (the step as it is timed) are the reported ones
         ms = rep["dom_ms"]
         achieved = fl / (ms * 1e-3) / 1e12
-        if rep["block_ms"] > 0 and rep["markers"] == 4:  # (fwd + bwd regions, each entered and left once)
+        if rep["block_ms"] > 0 and rep["block_launches"] == bn:
             bms = rep["block_ms"]
     return {"el": el, "loss": loss, "images_per_s": world * B * steps / el, "ms_per_step": el / steps * 1e3,
             "eager_roofline": eager, "replay_roofline": rep,
@@ -853,12 +848,11 @@ def main():
                                             what="the 12 GPT-2 blocks' GEMMs (fwd + dX) and attention (fwd + bwd) of "
                                                  "one step: summed algorithmic FLOPs (live rows) / summed in-replay "
                                                  "kernel time (timing)"),
-                         "timing": ("graph replay: the step graph captured once more with a ~1 us marker kernel at "
-                                    "the GPT-2-block region's boundaries, replayed 3x under torch.profiler; device "
-                                    "durations of the dominant instantiation's launches (whole step) and of the GEMM + "
-                                    "attention kernels between the markers (replay_roofline). The eager pass (HIP "
-                                    "events around every launch, eager_roofline) picks the dominant kernel and prices "
-                                    "the per-shape table"
+                         "timing": ("graph replay by difference: median replay of the step graph minus that of the "
+                                    "same graph captured without the dominant instantiation's launches (and, for "
+                                    "gpt2_block, without the block region's GEMM + attention launches), HIP events "
+                                    "between replays (replay_roofline). The eager pass (HIP events around every "
+                                    "launch, eager_roofline) picks the dominant kernel and prices the per-shape table"
                                     if r["replay_roofline"] and "dom_ms" in r["replay_roofline"] else
                                     "HIP events around every GEMM launch of one eager step on its launch stream (the "
                                     "replay pass was unavailable: replay_roofline)"),

@@ -407,7 +407,28 @@ static int device_cus() {
 
 namespace icap {
 int gemm256_launch(const icap_gemm_args& p, uint32_t thr, float inv_keep, hipStream_t s);
+int gemm8p_launch(const icap_gemm_args& p, int bn, int actk, uint32_t thr, float inv_keep, hipStream_t s);
 }
+
+// The 256-row 8-phase kernel (gemm8p.hip): bf16 row-major operands, one K range (no split), the epilogue forms it
+// instantiates (none / gelu_new fwd or bwd / any, the LayerNorm producer without an activation, the consumer without
+// one or with gelu_new). Returns its epilogue kind (ACT_* | ACT_LNS / ACT_LNF), or -1 when the launch is not one
+// of them. (diagnostic build) ICAP_GEMM8P = 0 never, 128 / 256 forced where eligible, default the shape rule.
+static int g8p_actk(const icap_gemm_args& p) {
+  if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || (p.ln_wsum && !p.ln_stats_in) || p.split_k > 1) return -1;
+  if (p.M < 256 || p.K < 64 || p.path == 1 || p.path == 3) return -1;
+  if (p.M * p.lda >= (1ll << 30) || p.N * p.ldb >= (1ll << 30)) return -1;  // 32-bit DMA byte offsets per tile
+  const int fa = p.dact == ICAP_ACT_NONE ? p.act : -1, ba = p.act == ICAP_ACT_NONE ? p.dact : -1;
+  int a;
+  if (p.act == ICAP_ACT_NONE && p.dact == ICAP_ACT_NONE) a = ACT_OFF;
+  else if (fa == ICAP_ACT_GELU_NEW) a = ACT_FWD + ICAP_ACT_GELU_NEW;
+  else if (ba == ICAP_ACT_GELU_NEW) a = ACT_BWD + ICAP_ACT_GELU_NEW;
+  else a = ACT_ANY;
+  if (p.ln_stats_out) return a == ACT_OFF ? ACT_LNS : -1;
+  if (p.ln_stats_in) return (a == ACT_OFF || a == ACT_FWD + ICAP_ACT_GELU_NEW) ? ACT_LNF + a : -1;
+  return a;
+}
+static int g8p_mode() { return diag_env("ICAP_GEMM8P", 1); }
 
 // (diagnostic build) ICAP_GEMM256: 0 = never, 2 = wherever eligible, default = the shape rule below
 static int g256_mode() {
@@ -424,7 +445,7 @@ static int g256_mode() {
 // head 8320 x 50304 x 768: 758 vs 835 us), not on the train step's 2-round K = 768 products (8320 x 3072 x 768:
 // 84 vs 80 us) (profiles/r02_gemm256_bench.txt). path 3 forces it where eligible.
 static bool g256_pick(const icap_gemm_args& p) {
-  if (p.path == 1) return false;
+  if (p.path == 1 || p.path == 4 || p.path == 5) return false;
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.beta != 0.f || p.m_dev || p.split_k > 1) return false;
   if (p.ln_stats_out || p.ln_stats_in) return false;
   if (p.M < 256 || p.N < 256 || p.K < 64) return false;
@@ -478,7 +499,7 @@ static int fused_nst_override() { return diag_env("ICAP_FUSED_NST", 0); }
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
-  ICAP_REQUIRE(p.path == 0 || p.path == 1 || p.path == 3, "icap_gemm: path must be 0, 1 or 3");
+  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 5), "icap_gemm: path must be 0, 1, 3, 4 or 5");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16 || p.in_dtype == ICAP_FP8_MX,
                "icap_gemm: bad in_dtype");
@@ -563,6 +584,29 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   if (g256_pick(p)) {
     pl.g256 = true;
     return ICAP_OK;
+  }
+  // the 256-row 8-phase kernel (gemm8p.hip) where its tiles fill the chip in one round
+  if (const int a8 = g8p_actk(p); a8 >= 0) {
+    const int mode = p.path == 4 ? 128 : p.path == 5 ? 256 : g8p_mode();
+    int bn = 0;
+    if (mode == 128 || mode == 256) {
+      bn = mode;
+    } else if (mode == 1) {
+      // one round of 256 x 256 tiles at least 80 % full, K <= 1536: there it beat every 128-row form (CLIP-B/32's
+      // 6400 x 2304 x 768 QKV: 30.6 vs 38.6 us; x 1536: 47.6 vs 68.5); 256 x 128 tiles and other shapes did not
+      // (the 3584-row products: within 3 %; N = 768: 30-60 % slower) — profiles/r05_g8p_ab.txt
+      const int64_t m_pl = (p.m_dev && p.m_hint > 0 && p.m_hint < p.M) ? p.m_hint : p.M;
+      const int64_t t256 = ((m_pl + 255) / 256) * ((p.N + 255) / 256);
+      const int64_t cus = device_cus();
+      if (p.K <= 1536 && t256 * 10 >= cus * 8 && t256 <= cus) bn = 256;
+    }
+    if (bn) {
+      pl.g8p = bn;
+      pl.actk = a8;
+      pl.thr = p.drop_p > 0.f ? drop_threshold(p.drop_p) : 0u;
+      pl.inv_keep = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
+      return ICAP_OK;
+    }
   }
   // split-K over K stages for launches that cannot fill the chip (decode-time M = batch, small projections):
   // fp32 partial slabs in the caller's workspace + one deterministic reduce/epilogue pass — or, with tickets, the
@@ -672,7 +716,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   }
   if (p.trans_ab) pl.variant = nk_split > 16 ? 14 : 15;  // K-outer forms of variants 0 / 4
   // (diagnostic build) ICAP_FORCE_TILE = 0 / 4 / 5 / 12 / 13 / 16: that tile variant for unsplit bf16 row-major
-  // launches (read per call so one process can interleave the forms)
+  // launches (read per call so one process can interleave the forms). (Round 5 also tried 256 x 128 tiles of 8
+  // waves on this template, double-buffered and single-buffered: no faster on any of the step's shapes,
+  // profiles/r05_tile_graph_ab.txt; removed.)
   if (const int v = diag_env("ICAP_FORCE_TILE", -1); v >= 0) {
     if (p.in_dtype == ICAP_BF16 && !p.trans_ab && splits == 1 &&
         (v == 0 || v == 4 || v == 5 || v == 12 || v == 13 || (v == 16 && !lnx))) {
@@ -750,6 +796,10 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
     snprintf(buf, sizeof buf, "icap::gemm256_kernel<%s>", tc);
     return buf;
   }
+  if (pl.g8p) {
+    snprintf(buf, sizeof buf, "icap::gemm8p_kernel<%s, %d, %d>", tc, pl.g8p, pl.actk);
+    return buf;
+  }
   char inner[128];
   if (pl.skinny) {
     snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2, %d>", pl.nt, pl.sku);
@@ -766,7 +816,7 @@ extern "C" int icap_gemm_plan_info(const icap_gemm_args* a, int32_t* splits, int
   GemmPlan pl;
   const int rc = gemm_plan(*a, pl);
   if (rc != ICAP_OK) return rc;
-  *splits = pl.skinny || pl.g256 ? 1 : pl.splits;
+  *splits = pl.skinny || pl.g256 || pl.g8p ? 1 : pl.splits;
   *fused = pl.fused ? 1 : 0;
   return ICAP_OK;
 }
@@ -822,6 +872,7 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
     return check_launch("icap_gemm(skinny)");
   }
   if (pl.g256) return gemm256_launch(p, thr, inv_keep, s);
+  if (pl.g8p) return gemm8p_launch(p, pl.g8p, pl.actk, thr, inv_keep, s);
   const int sp = pl.splits;
   const int nks = pl.nk_split | (kskew_for(p, pl.nk_split) << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));

@@ -8,6 +8,7 @@ namespace icap {
 struct GemmPlan {
   bool skinny = false;
   bool g256 = false;     // the 256 x 256 8-phase kernel (gemm256.hip)
+  int g8p = 0;           // the 256-row 8-phase kernel (gemm8p.hip): its tile width BN (128 / 256), 0 = not taken
   int nt = 1;            // skinny: 16-column slabs per block
   int sku = 3;           // skinny: k-steps in flight per wave
   int variant = 0;       // tile kernel (see ICAP_GEMM_LAUNCH)

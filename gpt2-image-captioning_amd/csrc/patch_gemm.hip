@@ -23,6 +23,7 @@ namespace icap {
 
 struct PatchArgs {
   int B, C, HW, p, G, G2, NP, S, N, K, Kp;
+  float inv_p, inv_pp;    // 1 / p, 1 / p^2 (k -> (c, ky, kx) without integer division: exact for k < 2^20)
   const float* px;        // [B, C, HW, HW] fp32
   const bf16_t* w;        // [N][ldw] bf16, columns k >= K zero
   int64_t ldw;
@@ -36,8 +37,11 @@ struct PatchArgs {
 constexpr int PG_BK = 64;          // K per LDS slice (one 128-byte bf16 row)
 constexpr int PG_STB = 2 * 128 * GROWB;  // bytes per slice: A 128 rows + B 128 rows
 
-template <bool RUN8>
+// RUN: 8 = p % 8 == 0 (an 8-element K chunk is one 32-byte pixel run: two 16-byte loads), 2 = p even (four 8-byte
+// pixel pairs, each inside one pixel row), 1 = per element
+template <int RUN>
 __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(PatchArgs a) {
+  constexpr bool RUN8 = RUN == 8;
   __shared__ __attribute__((aligned(16))) char smem[2 * PG_STB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -53,78 +57,103 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(PatchArgs a) {
   const int64_t m0 = (int64_t)tm * 128;
   const int n0 = tn * 128;
 
-  // this thread's staging chunks: chunk c = j * 256 + tid (j < 4) -> tile row c >> 3, K chunk tid & 7 (8 elements)
+  // this thread's staging chunks: chunk c = j * 256 + tid (j < 4) -> tile row c >> 3, K chunk tid & 7 (8 elements).
+  // Buffer loads, branch-free: rows past M / N and K past K (pixels) / Kp (weights) get an offset beyond the
+  // descriptor's range, which the hardware answers with zeros. The pixel descriptor starts at the tile's first image
+  // (a tile spans <= 128 / G^2 + 2 images), so 32-bit byte offsets suffice for any batch.
   const int kc = tid & 7;
   const int HW2 = a.HW * a.HW, pp = a.p * a.p;
-  int64_t rowbase[4];  // pixel offset of patch (b, py, px) of the A rows this thread stages, or -1 past M
+  const int64_t img = (int64_t)a.C * HW2;  // pixels per image
+  const int64_t b_first = m0 / a.G2;
+  const int64_t px_left = ((int64_t)a.B - b_first) * img * 4;
+  const __amdgpu_buffer_rsrc_t rpx = make_rsrc(a.px + b_first * img, (uint64_t)px_left);
+  uint32_t rowoff[4];  // byte offset (from the tile's first image) of patch (b, py, px) of the A rows staged here
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t m = m0 + j * 32 + (tid >> 3);
     if (m < M) {
       const int b = (int)(m / a.G2), pi = (int)(m - (int64_t)b * a.G2);
       const int py = pi / a.G, pxi = pi - py * a.G;
-      rowbase[j] = (int64_t)b * a.C * HW2 + (int64_t)py * a.p * a.HW + pxi * a.p;
+      rowoff[j] = (uint32_t)(((b - b_first) * img + (int64_t)py * a.p * a.HW + pxi * a.p) * 4);
     } else {
-      rowbase[j] = -1;
+      rowoff[j] = OOB;
     }
   }
-  const bf16_t* wrow[4];
+  const int nrows = a.N - n0 < 128 ? a.N - n0 : 128;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(a.w + (int64_t)n0 * a.ldw, (uint64_t)((nrows - 1) * a.ldw + a.Kp) * 2);
+  uint32_t woff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int n = n0 + j * 32 + (tid >> 3);
-    wrow[j] = n < a.N ? a.w + (int64_t)n * a.ldw : nullptr;
+    const int n = j * 32 + (tid >> 3);
+    woff[j] = n < nrows ? (uint32_t)(n * a.ldw * 2) : OOB;
   }
 
-  uint4 sa[4], sb[4];  // one slice's staged chunks (bf16)
-  auto load_slice = [&](int kt) {
+  // A slice in registers, raw: 4 rows x 8 fp32 pixels and 4 rows x one 16-byte bf16 weight chunk per thread. Two
+  // sets (even / odd slices): the loads of slice k + 2 are issued in iteration k, right after slice k + 1 left its set
+  // for LDS, so each load has two slices of MFMAs to land (round 5: with one set, issued one slice ahead, every
+  // k-step waited out an HBM round trip — 172 us for the CLIP-B/32 embed at B = 128, profiles/r05_kstats_*.txt).
+  struct Raw {
+    float v[4][8];
+    uint4 b[4];
+  };
+  auto load_raw = [&](int kt, Raw& r) __attribute__((always_inline)) {
     const int k0 = kt * PG_BK + kc * 8;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sb[j] = (wrow[j] && k0 < a.Kp) ? *reinterpret_cast<const uint4*>(wrow[j] + k0)
-                                                                : make_uint4(0u, 0u, 0u, 0u);
+    for (int j = 0; j < 4; ++j) r.b[j] = bload(rw, k0 < a.Kp ? woff[j] + (uint32_t)k0 * 2 : OOB);
     if constexpr (RUN8) {  // p % 8 == 0, HW % 8 == 0, K % 8 == 0: the 8 elements are one 32-byte pixel run
       const bool kin = k0 < a.K;
       const int cc = k0 / pp, rem = k0 - cc * pp, ky = rem / a.p, kx = rem - ky * a.p;
-      const int64_t koff = (int64_t)cc * HW2 + (int64_t)ky * a.HW + kx;
-      float4 lo[4], hi[4];
+      const uint32_t koff = (uint32_t)(((int64_t)cc * HW2 + (int64_t)ky * a.HW + kx) * 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (kin && rowbase[j] >= 0) {
-          const float4* src = reinterpret_cast<const float4*>(a.px + rowbase[j] + koff);
-          lo[j] = src[0];
-          hi[j] = src[1];
-        } else {
-          lo[j] = hi[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        const uint32_t o = (kin && rowoff[j] != OOB) ? rowoff[j] + koff : OOB;
+        const uint4 lo = bload(rpx, o), hi = bload(rpx, o == OOB ? OOB : o + 16);
+        r.v[j][0] = __uint_as_float(lo.x), r.v[j][1] = __uint_as_float(lo.y);
+        r.v[j][2] = __uint_as_float(lo.z), r.v[j][3] = __uint_as_float(lo.w);
+        r.v[j][4] = __uint_as_float(hi.x), r.v[j][5] = __uint_as_float(hi.y);
+        r.v[j][6] = __uint_as_float(hi.z), r.v[j][7] = __uint_as_float(hi.w);
+      }
+    } else if constexpr (RUN == 2) {  // even p (ViT-L/14): 4 pixel pairs, (kx, kx + 1) with kx even in one row
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const int k = k0 + e;
+        const bool kin = k < a.K;
+        const int cc = (int)(((float)k + 0.5f) * a.inv_pp), rem = k - cc * pp;
+        const int ky = (int)(((float)rem + 0.5f) * a.inv_p), kx = rem - ky * a.p;
+        const uint32_t koff = (uint32_t)(((int64_t)cc * HW2 + (int64_t)ky * a.HW + kx) * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint2 w = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                        rpx, (kin && rowoff[j] != OOB) ? rowoff[j] + koff : OOB, 0, 0));
+          r.v[j][e] = __uint_as_float(w.x);
+          r.v[j][e + 1] = __uint_as_float(w.y);
         }
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        sa[j] = make_uint4(f2bf2(lo[j].x, lo[j].y), f2bf2(lo[j].z, lo[j].w), f2bf2(hi[j].x, hi[j].y),
-                           f2bf2(hi[j].z, hi[j].w));
-    } else {  // general patch size (ViT-L/14): element by element, k >= K zero
-      float v[4][8];
+    } else {  // general patch size: element by element, k >= K zero
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int k = k0 + e;
         const bool kin = k < a.K;
-        const int cc = kin ? k / pp : 0, rem = k - cc * pp, ky = rem / a.p, kx = rem - ky * a.p;
-        const int64_t koff = (int64_t)cc * HW2 + (int64_t)ky * a.HW + kx;
+        const int cc = kin ? (int)(((float)k + 0.5f) * a.inv_pp) : 0, rem = k - cc * pp;
+        const int ky = (int)(((float)rem + 0.5f) * a.inv_p), kx = rem - ky * a.p;
+        const uint32_t koff = (uint32_t)(((int64_t)cc * HW2 + (int64_t)ky * a.HW + kx) * 4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j][e] = (kin && rowbase[j] >= 0) ? a.px[rowbase[j] + koff] : 0.f;
+        for (int j = 0; j < 4; ++j)
+          r.v[j][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                    rpx, (kin && rowoff[j] != OOB) ? rowoff[j] + koff : OOB, 0, 0));
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        sa[j] = make_uint4(f2bf2(v[j][0], v[j][1]), f2bf2(v[j][2], v[j][3]), f2bf2(v[j][4], v[j][5]),
-                           f2bf2(v[j][6], v[j][7]));
     }
   };
-  auto store_slice = [&](int s) {
+  auto store_raw = [&](const Raw& r, int s) __attribute__((always_inline)) {  // convert to bf16, into LDS buffer s
     char* As = smem + s * PG_STB;
     char* Bs = As + 128 * GROWB;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = j * 32 + (tid >> 3);
-      *reinterpret_cast<uint4*>(As + lds_off(row, kc)) = sa[j];
-      *reinterpret_cast<uint4*>(Bs + lds_off(row, kc)) = sb[j];
+      *reinterpret_cast<uint4*>(As + lds_off(row, kc)) =
+          make_uint4(f2bf2(r.v[j][0], r.v[j][1]), f2bf2(r.v[j][2], r.v[j][3]), f2bf2(r.v[j][4], r.v[j][5]),
+                     f2bf2(r.v[j][6], r.v[j][7]));
+      *reinterpret_cast<uint4*>(Bs + lds_off(row, kc)) = r.b[j];
     }
   };
 
@@ -134,13 +163,7 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(PatchArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (a.Kp + PG_BK - 1) / PG_BK;
-  load_slice(0);
-  store_slice(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_slice(kt + 1);  // in flight during this slice's MFMAs (T14 issue-early)
+  auto compute = [&](int cur) __attribute__((always_inline)) {
     const char* As = smem + cur * PG_STB;
     const char* Bs = As + 128 * GROWB;
     uint4 af[2][4], bfr[2][4];
@@ -158,8 +181,29 @@ __global__ __launch_bounds__(256, 2) void patch_gemm_kernel(PatchArgs a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mfma_chunk<bf16_t>(acc[i][j], af[ks][i], bfr[ks][j]);
-    if (kt + 1 < nk) store_slice(cur ^ 1);  // the other buffer was last read in iteration kt - 1 (write late)
+  };
+
+  // K slices, rounded up to an even count: every iteration then issues, stores and loads unconditionally (slices past
+  // Kp load zeros through the range check). A conditional load made hipcc's wait counting assume the newest loads
+  // could be the ones a store needs, and wait for all of them (vmcnt(0)) in every iteration.
+  const int nk = ((a.Kp + PG_BK - 1) / PG_BK + 1) & ~1;
+  Raw r0, r1;  // slices 0, 2, 4, ... in r0; 1, 3, 5, ... in r1
+  load_raw(0, r0);
+  load_raw(1, r1);
+  store_raw(r0, 0);
+  load_raw(2, r0);
+  __syncthreads();
+  // iteration kt: MFMAs on LDS buffer kt & 1; slice kt + 1 (in its register set since iteration kt - 2) into the
+  // other buffer, which every wave finished reading before the previous barrier; slice kt + 3 loaded into that set
+  auto iter = [&](int kt, Raw& nxt) __attribute__((always_inline)) {
+    compute(kt & 1);
+    store_raw(nxt, (kt & 1) ^ 1);
+    load_raw(kt + 3, nxt);
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    iter(kt, r1);
+    iter(kt + 1, r0);
   }
 
   // prefix rows (CLS / registers): the blocks of the first row panel write them for their columns
@@ -254,8 +298,10 @@ extern "C" int icap_patch_embed(int32_t B, int32_t C, int32_t HW, int32_t patch,
   const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
   ICAP_REQUIRE(tiles < (1ll << 30), "icap_patch_embed: too many tiles");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool run8 = patch % 8 == 0 && HW % 8 == 0;
-  if (run8) hipLaunchKernelGGL(patch_gemm_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(patch_gemm_kernel<false>, dim3((unsigned)tiles), dim3(256), 0, s, a);
+  a.inv_p = 1.f / (float)patch, a.inv_pp = 1.f / (float)(patch * patch);
+  ICAP_REQUIRE(K < (1 << 20), "icap_patch_embed: C p p must stay below 2^20");
+  if (patch % 8 == 0 && HW % 8 == 0) hipLaunchKernelGGL(patch_gemm_kernel<8>, dim3((unsigned)tiles), dim3(256), 0, s, a);
+  else if (patch % 2 == 0) hipLaunchKernelGGL(patch_gemm_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(patch_gemm_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, s, a);
   return check_launch("icap_patch_embed");
 }

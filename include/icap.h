@@ -111,7 +111,10 @@ typedef struct {
   /* kernel, measured slower and removed: rejected); 3 = the 256 x 256 8-phase kernel wherever its           */
   /* preconditions hold (bf16 A/B, no trans_ab / ln / beta /                                                   */
   /*     m_dev / split-K, M and N >= 256) —                                                                      */
-  /* for A/B measurements and for tests that compare the two paths (identical MFMA chains: bitwise equal).     */
+  /* for A/B measurements and for tests that compare the two paths (identical MFMA chains: bitwise equal);    */
+  /* 4 / 5 = the 256-row 8-phase kernel with 128- / 256-column tiles wherever its preconditions hold (bf16    */
+  /*     A/B, no trans_ab / ln_gamma / split-K, M >= 256, K >= 64; m_dev and the LayerNorm hand-off allowed:   */
+  /*     csrc/gemm8p.hip) — same use.                                                                          */
   int32_t path;
   /* in_dtype == ICAP_FP8_MX: the E8M0 block scales of A (M rows) and B (N rows), K % 128 == 0, lda / ldb      */
   /* multiples of 16, 16-byte aligned. For a 128-element K stage s and 64-row group g, 256 bytes at offset      */
