@@ -416,7 +416,7 @@ int gemm8p_launch(const icap_gemm_args& p, int bn, int actk, uint32_t thr, float
 // of them. (diagnostic build) ICAP_GEMM8P = 0 never, 128 / 256 forced where eligible, default the shape rule.
 static int g8p_actk(const icap_gemm_args& p) {
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || (p.ln_wsum && !p.ln_stats_in) || p.split_k > 1) return -1;
-  if (p.M < 256 || p.K < 64 || p.path == 1 || p.path == 3) return -1;
+  if (p.M < 256 || p.K < 64 || p.path == 1 || p.path == 3 || p.path == 6) return -1;
   if (p.M * p.lda >= (1ll << 30) || p.N * p.ldb >= (1ll << 30)) return -1;  // 32-bit DMA byte offsets per tile
   const int fa = p.dact == ICAP_ACT_NONE ? p.act : -1, ba = p.act == ICAP_ACT_NONE ? p.dact : -1;
   int a;
@@ -429,6 +429,26 @@ static int g8p_actk(const icap_gemm_args& p) {
   return a;
 }
 static int g8p_mode() { return diag_env("ICAP_GEMM8P", 1); }
+
+// Variant 22 (gemm_tile_r256.hip: 256 x 128 tiles, 8 waves, 3-stage ring, one block per CU): its epilogue kind for
+// an unsplit bf16 row-major launch, or -1 (the forms it instantiates: none, gelu_new fwd / bwd, quick_gelu fwd, any;
+// the LayerNorm producer without an activation, the consumer without one or with gelu_new / quick_gelu).
+static int r256_actk(const icap_gemm_args& p) {
+  if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || (p.ln_wsum && !p.ln_stats_in)) return -1;
+  const int fa = p.dact == ICAP_ACT_NONE ? p.act : -1, ba = p.act == ICAP_ACT_NONE ? p.dact : -1;
+  int a;
+  if (p.act == ICAP_ACT_NONE && p.dact == ICAP_ACT_NONE) a = ACT_OFF;
+  else if (fa == ICAP_ACT_GELU_NEW) a = ACT_FWD + ICAP_ACT_GELU_NEW;
+  else if (ba == ICAP_ACT_GELU_NEW) a = ACT_BWD + ICAP_ACT_GELU_NEW;
+  else if (fa == ICAP_ACT_QUICK_GELU) a = ACT_FWD + ICAP_ACT_QUICK_GELU;
+  else a = ACT_ANY;
+  if (p.c_dtype != ICAP_BF16) return (p.ln_stats_out || p.ln_stats_in) ? -1 : (a == ACT_OFF ? ACT_OFF : ACT_ANY);
+  if (p.ln_stats_out) return a == ACT_OFF ? ACT_LNS : -1;
+  if (p.ln_stats_in) return (a == ACT_OFF || a == ACT_FWD + ICAP_ACT_GELU_NEW || a == ACT_FWD + ICAP_ACT_QUICK_GELU) ? ACT_LNF + a : -1;
+  return a;
+}
+// (diagnostic build) ICAP_R256 = 1: take variant 22 for every eligible unsplit launch of path 0
+static int r256_mode() { return diag_env("ICAP_R256", 0); }
 
 // (diagnostic build) ICAP_GEMM256: 0 = never, 2 = wherever eligible, default = the shape rule below
 static int g256_mode() {
@@ -445,7 +465,7 @@ static int g256_mode() {
 // head 8320 x 50304 x 768: 758 vs 835 us), not on the train step's 2-round K = 768 products (8320 x 3072 x 768:
 // 84 vs 80 us) (profiles/r02_gemm256_bench.txt). path 3 forces it where eligible.
 static bool g256_pick(const icap_gemm_args& p) {
-  if (p.path == 1 || p.path == 4 || p.path == 5) return false;
+  if (p.path == 1 || p.path == 4 || p.path == 5 || p.path == 6) return false;
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.beta != 0.f || p.m_dev || p.split_k > 1) return false;
   if (p.ln_stats_out || p.ln_stats_in) return false;
   if (p.M < 256 || p.N < 256 || p.K < 64) return false;
@@ -475,7 +495,7 @@ static int fused_s_override() {
 // keeps the natural order (the path-equality tests compare it bitwise with the 256 x 256 kernel).
 static int kskew_for(const icap_gemm_args& p, int64_t nk_split) {
   static const int v = diag_env("ICAP_KSKEW", 1);
-  if (p.path == 1 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
+  if (p.path == 1 || p.path == 6 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
   return v > 0 && v < 256 ? v : 0;
 }
 // ICAP_GEMM_DIAG = 1 / 2 / 3: drop the A / B / both operands' staging loads of the tile kernels (zero-record
@@ -499,7 +519,7 @@ static int fused_nst_override() { return diag_env("ICAP_FUSED_NST", 0); }
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
-  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 5), "icap_gemm: path must be 0, 1, 3, 4 or 5");
+  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 6), "icap_gemm: path must be 0, 1, 3, 4, 5 or 6");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16 || p.in_dtype == ICAP_FP8_MX,
                "icap_gemm: bad in_dtype");
@@ -734,6 +754,19 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   }
   // the LayerNorm-folded quick_gelu consumer (CLIP c_fc) exists at 3 blocks / CU only (gemm_tile_ln.hip)
   if (lnx && pl.variant == 0 && p.act == ICAP_ACT_QUICK_GELU) pl.variant = 4;
+  // variant 22: 256 x 128 tiles on the 3-stage ring (path 6 forces it where eligible)
+  if (splits == 1 && p.M >= 256 && (p.path == 6 || (p.path == 0 && r256_mode() == 1))) {
+    if (const int a22 = r256_actk(p); a22 >= 0) {
+      pl.variant = 22;
+      tiles_n = (p.N + 127) / 128;
+      tiles = ((p.M + 255) / 256) * tiles_n;
+      pl.tiles_n = (int)tiles_n;
+      pl.actk = a22;
+      pl.block = dim3(2 * GNT);
+      pl.grid = dim3((unsigned)tiles);
+      return ICAP_OK;
+    }
+  }
   pl.tiles_n = (int)tiles_n;
   const bool any_act = (splits == 1 || pl.fused) && (p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE);
   pl.actk = any_act ? ACT_ANY : ACT_OFF;
@@ -780,6 +813,7 @@ static const char* variant_kernel(int v) {
     case 13: return "gemm_kernel<%s, %s, 1, 4, 2, 2, 4, 2, false, %d>";
     case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true, %d>";
     case 16: return "gemm_kernel<%s, %s, 4, 1, 2, 2, 4, 4, false, %d>";
+    case 22: return "gemm_kernel<%s, %s, 3, 1, 4, 2, 4, 4, false, %d>";
     default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %d>";
   }
 }
@@ -876,7 +910,8 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const int sp = pl.splits;
   const int nks = pl.nk_split | (kskew_for(p, pl.nk_split) << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
-  if (pl.actk >= ACT_LNS) launch_tile_ln(pl, p, nks, s);                           // gemm_tile_ln.hip
+  if (pl.variant == 22) launch_tile_r256(pl, p, nks, s);                             // gemm_tile_r256.hip
+  else if (pl.actk >= ACT_LNS) launch_tile_ln(pl, p, nks, s);                      // gemm_tile_ln.hip
   else if (pl.actk >= ACT_FWD) launch_tile_act(pl, p, nks, s);                     // gemm_tile_act.hip
   else if (pl.variant == 14 || pl.variant == 15) launch_tile_kout(pl, p, nks, s);    // gemm_tile_kout.hip
   else if (p.in_dtype == ICAP_BF16) launch_tile_bf16(pl, p, nks, s);                 // gemm_tile_bf16.hip

@@ -256,7 +256,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       }
     }
   };
-  static_assert(LNX != 2 || NST != 4, "the ring has no LayerNorm-fold prologue");
 
   f32x4_t acc[TM][TN];
 #pragma unroll
@@ -348,19 +347,22 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     }
   };
 
-  if constexpr (NST == 4) {
-    // Deep ring for launches with about one tile per CU and long K (the packed step's N = 768 products): 4 LDS
-    // stages (128 KiB, one block per CU), stages kt+1..kt+2 in flight while stage kt is read and stage kt+3 is
-    // issued, so three DMA round trips overlap each stage's MFMAs (the double-buffered loop leaves one: at one block
-    // per CU it waited ~0.6 of every k-step on the DMA). The fragment reads are inline asm (hipcc would otherwise
-    // drain the DMA queue, vmcnt(0), in front of every LDS read), retired by counted lgkmcnt waits tied to their
-    // registers; the DMA waits are counted vmcnt (never 0 in the steady state) and the barriers raw s_barrier
-    // (cdna_hip_programming.md "Pipelining across barriers", T3+T4).
+  if constexpr (NST >= 3) {
+    // Deep ring for launches with about one tile per CU (the packed step's N = 768 products, round 3: 128 x 128
+    // tiles, 4 LDS stages = 128 KiB) and for the 256 x 128 tiles of 8 waves (round 5: 3 stages of 48 KiB = 144 KiB):
+    // one block per CU, NST - 2 stages in flight while stage kt is read and stage kt + NST - 1 is issued. The round-5
+    // form exists because a CU's LDS-DMA intake, not the MFMA, bounds the main loop (≈ 70 GB/s per CU from the XCD's
+    // L2: MI355X_MICROARCH.md "Indexed rows: gather into LDS"): a 256 x 128 tile fetches 48 KiB per 64-deep k-step
+    // for the MFMA work two 128 x 128 tiles fetch 64 KiB for, and it needs >= 72 KiB in flight to reach that rate.
+    // The fragment reads are inline asm (hipcc would otherwise drain the DMA queue, vmcnt(0), in front of every LDS
+    // read), retired by counted lgkmcnt waits tied to their registers; the DMA waits are counted vmcnt (never 0 in
+    // the steady state) and the barriers raw s_barrier (cdna_hip_programming.md "Pipelining across barriers", T3+T4).
     //   RAW: stage kt is read after this wave's vmcnt wait for it and a barrier every wave passed after its own.
-    //   WAR: stage kt+3 is written into the slot read in iteration kt-1, whose reads every wave retired (lgkmcnt)
-    //        before that iteration's MFMAs, i.e. before the barrier of iteration kt.
-    static_assert(!KOUT && !MX && sizeof(TI) == 2 && TM == 4 && TN == 4 && APW + BPW == 8,
-                  "ring: bf16 row-major operands, 128 x 128 tiles of 4 waves");
+    //   WAR: stage kt+NST-1 is written into the slot read in iteration kt-1, whose reads every wave retired
+    //        (lgkmcnt) before that iteration's MFMAs, i.e. before the barrier of iteration kt.
+    static_assert(!KOUT && !MX && sizeof(TI) == 2 && TM == 4 && TN == 4,
+                  "ring: bf16 row-major operands, 64 x 64 per wave");
+    constexpr int D = APW + BPW;  // DMA instructions per wave per stage
     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
     const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>(smem);
     uint32_t la[2], lb[2];  // byte offsets in a stage of this lane's fragment rows (A row / B row + 16 i)
@@ -371,19 +373,25 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       lb[ks] = (uint32_t)(BM * GROWB + (wn * 16 * TN + fr) * GROWB) + sw;
     }
 #pragma unroll
-    for (int s = 0; s < 3; ++s)
+    for (int s = 0; s < NST - 1; ++s)
       if (s < nk) load_stage(kbase + kstep(s), s);
+    ln_prologue();  // (its loads are waited for at their first use, which drains the prologue's DMA once)
 #define ICAP_RING_RD(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
     for (int kt = 0; kt < nk; ++kt) {
       __builtin_amdgcn_sched_barrier(0);
-      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");      // stages kt+1, kt+2 stay in flight
-      else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (NST == 4) {
+        if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");  // kt+1, kt+2 stay in flight
+        else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");  // kt+1 stays in flight
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if (kt + 3 < nk) load_stage(kbase + kstep(kt + 3), (kt + 3) & 3);
+      if (kt + NST - 1 < nk) load_stage(kbase + kstep(kt + NST - 1), (kt + NST - 1) % NST);
       __builtin_amdgcn_sched_barrier(0);
-      const uint32_t sb = sbase + (uint32_t)((kt & 3) * STB);
+      const uint32_t sb = sbase + (uint32_t)((kt % NST) * STB);
       u32x4_t fa0[4], fb0[4], fa1[4], fb1[4];
       {
         const uint32_t a0 = sb + la[0], b0 = sb + lb[0], a1 = sb + la[1], b1 = sb + lb[1];
@@ -396,20 +404,24 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
                    : "+v"(fa0[0]), "+v"(fa0[1]), "+v"(fa0[2]), "+v"(fa0[3]), "+v"(fb0[0]), "+v"(fb0[1]), "+v"(fb0[2]),
                      "+v"(fb0[3]));
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NW > 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           mfma_chunk<TI>(acc[i][j], __builtin_bit_cast(uint4, fa0[i]), __builtin_bit_cast(uint4, fb0[j]));
+      if constexpr (NW > 4) __builtin_amdgcn_s_setprio(0);
       asm volatile("s_waitcnt lgkmcnt(0)"
                    : "+v"(fa1[0]), "+v"(fa1[1]), "+v"(fa1[2]), "+v"(fa1[3]), "+v"(fb1[0]), "+v"(fb1[1]), "+v"(fb1[2]),
                      "+v"(fb1[3]));
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NW > 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           mfma_chunk<TI>(acc[i][j], __builtin_bit_cast(uint4, fa1[i]), __builtin_bit_cast(uint4, fb1[j]));
+      if constexpr (NW > 4) __builtin_amdgcn_s_setprio(0);
     }
 #undef ICAP_RING_RD
     __builtin_amdgcn_sched_barrier(0);

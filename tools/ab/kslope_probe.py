@@ -42,7 +42,7 @@ for M, N in ((3584, 2304), (6400, 2304), (3584, 768)):
         B = (torch.randn((N, K), generator=g) * 0.1).to(dev, torch.bfloat16)
         C = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
         row = []
-        for name in ("auto", "v0", "g8p128", "g8p256", "hipblaslt"):
+        for name in ("auto", "v0", "r256", "g8p256", "hipblaslt"):
             os.environ.pop("ICAP_FORCE_TILE", None)
             if name == "v0":
                 os.environ["ICAP_FORCE_TILE"] = "0"
@@ -50,7 +50,8 @@ for M, N in ((3584, 2304), (6400, 2304), (3584, 768)):
                 fn = lambda: torch.mm(A, B.t(), out=C)  # noqa: E731
             else:
                 g8 = {"g8p128": 128, "g8p256": 256}.get(name, 0)
-                fn = lambda g8=g8, name=name: ops.gemm(A, B, C, split_k=0 if name == "auto" else 1, g8p=g8)  # noqa: E731
+                fn = lambda g8=g8, name=name: ops.gemm(A, B, C, split_k=0 if name == "auto" else 1, g8p=g8,  # noqa: E731
+                                                       r256=name == "r256")
             us = per_launch(fn)
             row.append(f"{name} {us:6.1f} ({2.0 * M * N * K / us / 1e6:4.0f})")
         os.environ.pop("ICAP_FORCE_TILE", None)

@@ -13,7 +13,7 @@ from gemm_tiles_ab import SHAPES  # noqa: E402
 from icap import _lib as L  # noqa: E402
 from icap import ops  # noqa: E402
 
-FORMS = [("auto", None), ("v0", "0"), ("v4", "4"), ("v5", "5"), ("v16", "16"), ("g8p128", "g128"), ("g8p256", "g256")]
+FORMS = [("auto", None), ("v0", "0"), ("v4", "4"), ("v5", "5"), ("v16", "16"), ("g8p256", "g256"), ("r256", "r")]
 dev = torch.device("cuda", 0)
 REPS = 20
 
@@ -69,12 +69,13 @@ for M, live, N, K, epi, what in SHAPES:
     ref = None
     for name, fv in FORMS:
         g8 = int(fv[1:]) if fv and fv.startswith("g") else 0
-        if fv is None or g8:
+        rr = fv == "r"
+        if fv is None or g8 or rr:
             os.environ.pop("ICAP_FORCE_TILE", None)
         else:
             os.environ["ICAP_FORCE_TILE"] = fv
         try:
-            us = per_launch(lambda: ops.gemm(A, B, C, split_k=0 if fv is None else 1, g8p=g8, **kw))
+            us = per_launch(lambda: ops.gemm(A, B, C, split_k=0 if fv is None else 1, g8p=g8, r256=rr, **kw))
             got = C[:rows].clone()
             if ref is None:
                 ref = got

@@ -10,3 +10,5 @@ python -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; pri
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 3 --no-decode --no-cpu-baseline --sweep "" > $O/prof_bench.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
 find $O/prof -name "*.db" | head -2
+timeout -k 10 600 python -u bench.py --config large --fp8 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_large_fp8.json 2> $O/bench_large_fp8.err || { tail -20 $O/bench_large_fp8.err; exit 1; }
+python -c "import json; d=json.load(open('$O/bench_large_fp8.json')); print('large fp8', d['value'], d['ms_per_step'], d['roofline']['frac'])"
