@@ -14,7 +14,8 @@
 //
 // Geometry: 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns rows wr*128 + [0,128) and columns wc*WCN + [0,WCN)
 // (WCN = BN / 4), as 8 x (WCN / 16) MFMA 16x16x32 accumulators. K advances 64 per tile (BK).
-// LDS: two K-tile buffers; a K-tile is four half-tiles of 128-byte rows (64 K):
+// LDS: NBUF K-tile buffers (3 at BN 128: the DMA runs two K-tiles ahead; 2 at BN 256: one ahead, gemm256.hip's
+// schedule); a K-tile is four half-tiles of 128-byte rows (64 K):
 //   h0 A-qm0: A rows {0..63} u {128..191}      (the first 64 rows of each wave-row's 128)
 //   h1 B-qn0: B rows wc*WCN + [0, QN), wc = 0..3  (QN = WCN / 2: the first half of each wave-column)
 //   h2 B-qn1: B rows wc*WCN + [QN, WCN)
@@ -22,8 +23,11 @@
 // chunk index XOR-swizzled by (row & 7) (conflict-free ds_read_b128); the LDS-DMA writes lane-linear 1 KiB pieces
 // and the swizzle lives on the per-lane source address (rule 21).
 // Phases of one K-tile (one output quadrant each) and the DMA / wait schedule are gemm256.hip's (its header has the
-// RAW / WAR argument); only the per-wave DMA counts differ: a B half-tile is BN / 2 rows = BN / 128 pieces per wave,
-// so the counted wait leaves 2 + BN / 128 instructions (the next tile's h0, h1) in flight.
+// RAW / WAR argument), shifted by LA = NBUF - 1 K-tiles: half-tile h0 / h1 of K-tile u is issued at phase p2 / p3 of
+// K-tile u - LA - 1, h2 / h3 at p0 / p1 of K-tile u - LA. Every issue still lands in the buffer of a K-tile whose
+// same half was read two or more phases earlier (buffer (u mod NBUF): for h0 at p2 of K-tile t, u = t + LA + 1 ≡ t),
+// so the WAR argument is unchanged; the RAW wait at p3 of K-tile t retires K-tile t + 1 and leaves everything issued
+// after its last half in flight (counted per wave: an A half-tile is 2 DMA instructions, a B half-tile BN / 128).
 #include "gemm_common.h"
 
 namespace icap {
@@ -41,7 +45,10 @@ struct Geo {
   static constexpr int BPW = BN / 128;           // B DMA pieces per wave per half-tile
   static constexpr int ELD = WCN + 4;            // fp32 row stride of the epilogue staging
   static constexpr int EW = 64 * ELD * 4;        // staging bytes per wave (64 rows)
-  static constexpr int SMEM = (2 * TB > 8 * EW) ? 2 * TB : 8 * EW;
+  // K-tile buffers: three for 128-column tiles (144 KiB: two K-tiles in flight, the >= 72 KiB a CU needs in flight
+  // to reach its LDS-DMA intake rate), two for 256 columns (128 KiB)
+  static constexpr int NBUF = BN == 128 ? 3 : 2;
+  static constexpr int SMEM = (NBUF * TB > 8 * EW) ? NBUF * TB : 8 * EW;
   static constexpr int LPR = WCN / 8;            // epilogue lanes per row (8 columns each)
   static constexpr int RPI = 64 / LPR;           // rows per epilogue wave instruction
 };
@@ -56,7 +63,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int ti
   using G = Geo<BN>;
   constexpr int AK = ACT & 0xFF;  // the epilogue's activation kind
   constexpr int LNX = ACT >> 8;   // 1 = LayerNorm statistics producer, 2 = consumer
-  constexpr int NJ = G::NJ, WCN = G::WCN, QN = G::QN, BPW = G::BPW, TB = G::TB, HTB = G::HTB;
+  constexpr int NJ = G::NJ, WCN = G::WCN, QN = G::QN, BPW = G::BPW, TB = G::TB, HTB = G::HTB, NBUF = G::NBUF;
+  constexpr int LA = NBUF - 1;  // K-tiles the DMA runs ahead: half-tile h of K-tile u is issued in K-tile u - LA
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM + (LNX == 2 ? 8 * BM : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -105,7 +113,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int ti
     const int64_t k0 = (int64_t)u * 64;
     const bool kin = k0 + c * 8 < K;  // K % 8 == 0: a 16-byte chunk is wholly inside or outside
     constexpr int off = H == 0 ? 0 : H == 1 ? HTA : H == 2 ? HTA + HTB : HTA + 2 * HTB;
-    char* dst = smem + (u & 1) * TB + off;
+    char* dst = smem + (u % NBUF) * TB + off;
     const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(k0 * 2));
     if constexpr (H == 0 || H == 3) {
 #pragma unroll
@@ -215,34 +223,49 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int ti
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(R[0][0]), "+v"(R[1][0]));
   };
 #define G8P_FENCE() __builtin_amdgcn_sched_barrier(0)
-#define G8P_VMCNT_PRO() asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + BPW) : "memory")
+  // counted waits: DMA instructions per wave of an A / B half-tile = 2 / BPW, a K-tile = 4 + 2 BPW
+  constexpr int DH = 2 + BPW, DT = 4 + 2 * BPW;
+  // retire K-tile t+1 at the end of K-tile t (or tile 0 in the prologue), leaving the later issues in flight:
+  // tile t+2's first two half-tiles (LA 1), or all of tile t+2 and tile t+3's first two (LA 2), as far as issued
+  auto retire_next = [&](int t) __attribute__((always_inline)) {
+    if constexpr (LA == 1) {
+      if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DH) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (t + 3 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DT + DH) : "memory");
+      else if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
 
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
 
-  // prologue: tile 0 and the first two half-tiles of tile 1 in flight; the LN row table; wait for tile 0
-  issue(I0{}, 0); issue(I1{}, 0); issue(I2{}, 0); issue(I3{}, 0);
-  issue(I0{}, 1); issue(I1{}, 1);
+  // prologue: tiles 0 .. LA-1 whole and the first two half-tiles of tile LA in flight; the LN row table; wait for
+  // tile 0
+#pragma unroll
+  for (int u = 0; u < LA; ++u) {
+    issue(I0{}, u); issue(I1{}, u); issue(I2{}, u); issue(I3{}, u);
+  }
+  issue(I0{}, LA); issue(I1{}, LA);
   G8P_FENCE();
-  ln_prologue();  // (its loads complete before the wait below: they are older than nothing it waits on but
-                  //  hipcc waits for them at their first use, inside the prologue)
+  ln_prologue();  // (its loads are waited for at their first use, inside the prologue; that drains the DMA once)
   G8P_FENCE();
-  if (nk >= 2) G8P_VMCNT_PRO();
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  retire_next(-1);
   __builtin_amdgcn_s_barrier();
   // wave-row 1 runs one barrier behind wave-row 0: on every SIMD one wave's MFMAs overlap the other's reads
   if (wr == 1) __builtin_amdgcn_s_barrier();
   G8P_FENCE();
 
   for (int t = 0; t < nk; ++t) {
-    const uint32_t tb = sbase + (uint32_t)((t & 1) * TB);
-    // p0: (qm0, qn0); DMA tile t+1 h2
+    const uint32_t tb = sbase + (uint32_t)((t % NBUF) * TB);
+    // p0: (qm0, qn0); DMA tile t+LA h2
     read_a(tb);
     read_b(RB0, tb + HTA);
     G8P_FENCE();
-    issue(I2{}, t + 1);
+    issue(I2{}, t + LA);
     G8P_FENCE();
     __builtin_amdgcn_s_barrier();
     wait_a();
@@ -252,10 +275,10 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int ti
     G8P_FENCE();
     __builtin_amdgcn_s_barrier();
     G8P_FENCE();
-    // p1: (qm0, qn1); DMA tile t+1 h3
+    // p1: (qm0, qn1); DMA tile t+LA h3
     read_b(RB1, tb + HTA + HTB);
     G8P_FENCE();
-    issue(I3{}, t + 1);
+    issue(I3{}, t + LA);
     G8P_FENCE();
     __builtin_amdgcn_s_barrier();
     wait_b(RB1);
@@ -264,10 +287,10 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int ti
     G8P_FENCE();
     __builtin_amdgcn_s_barrier();
     G8P_FENCE();
-    // p2: (qm1, qn1); DMA tile t+2 h0
+    // p2: (qm1, qn1); DMA tile t+LA+1 h0
     read_a(tb + HTA + 2 * HTB);
     G8P_FENCE();
-    issue(I0{}, t + 2);
+    issue(I0{}, t + LA + 1);
     G8P_FENCE();
     __builtin_amdgcn_s_barrier();
     wait_a();
@@ -276,11 +299,10 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int ti
     G8P_FENCE();
     __builtin_amdgcn_s_barrier();
     G8P_FENCE();
-    // p3: (qm1, qn0); DMA tile t+2 h1; retire tile t+1 (tile t+2's two half-tiles stay in flight)
-    issue(I1{}, t + 2);
+    // p3: (qm1, qn0); DMA tile t+LA+1 h1; retire tile t+1
+    issue(I1{}, t + LA + 1);
     G8P_FENCE();
-    if (t + 2 < nk) G8P_VMCNT_PRO();
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    retire_next(t);
     __builtin_amdgcn_s_barrier();
     G8P_FENCE();
     quad(4, 0, RB0);
@@ -290,7 +312,6 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(icap_gemm_args p, int ti
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // equal barrier counts: wave-row 0 waits for row 1's last phase
 #undef G8P_FENCE
-#undef G8P_VMCNT_PRO
 
   // ---- epilogue: no DMA outstanding (the last wait was vmcnt(0)); every wave is past the last barrier ----------
   // Each wave stages 64 of its 128 rows at a time through its own LDS slice and re-reads 8 consecutive columns per

@@ -42,7 +42,7 @@ for M, N in ((3584, 2304), (6400, 2304), (3584, 768)):
         B = (torch.randn((N, K), generator=g) * 0.1).to(dev, torch.bfloat16)
         C = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
         row = []
-        for name in ("auto", "v0", "r256", "g8p256", "hipblaslt"):
+        for name in ("auto", "v0", "r256", "g8p128", "hipblaslt"):
             os.environ.pop("ICAP_FORCE_TILE", None)
             if name == "v0":
                 os.environ["ICAP_FORCE_TILE"] = "0"

@@ -13,7 +13,7 @@ from gemm_tiles_ab import SHAPES  # noqa: E402
 from icap import _lib as L  # noqa: E402
 from icap import ops  # noqa: E402
 
-FORMS = [("auto", None), ("v0", "0"), ("v4", "4"), ("v5", "5"), ("v16", "16"), ("g8p256", "g256"), ("r256", "r")]
+FORMS = [("auto", None), ("v0", "0"), ("v4", "4"), ("v5", "5"), ("v16", "16"), ("g8p128", "g128"), ("r256", "r")]
 dev = torch.device("cuda", 0)
 REPS = 20
 
