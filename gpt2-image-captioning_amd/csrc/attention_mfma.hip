@@ -329,8 +329,8 @@ __global__ __launch_bounds__(256) void bwd_kernel(icap_attn_args p, Geo g, uint3
 
 // ---------------------------------------------------------------------------------------------------------
 // Backward v2 (needs the forward output O: delta[q] = rowsum(dO o O) = rowsum(P o dP), dropout included).
-// Q, K, V, dO of the head are staged ROW-major in LDS once (16-byte copies, rows padded to HD+8 halves so the
-// 16-row fragment reads hit 16 distinct 4-bank groups); no scalar transposes. Waves split by role:
+// Q, K, V, dO of the head are staged ROW-major in LDS once (16-byte copies, rows padded to ldr_of(HD) halves: see
+// below); no scalar transposes. Waves split by role:
 //   waves [0, nt)   : one 16-key tile each -> dV^T = dO^T P_drop, dK^T = Q^T dS over all queries,
 //   waves [nt, 2nt) : one 16-query tile each -> dQ^T = K^T dS^T over all keys,
 // where the first products (S = Q K^T, dP = dO V^T, in whichever orientation puts the contraction index of the
@@ -341,6 +341,15 @@ __global__ __launch_bounds__(256) void bwd_kernel(icap_attn_args p, Geo g, uint3
 // 4 consecutive head dims per lane (8-byte stores).
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s_t* lds_v4s_ptr;
+// Row stride (halves) of the row-major Q / K / V / dO images: HD + 16. With the 64 four-byte banks and the lane
+// groups of ds_read_b128 (4 x 16 lanes) and ds_read_b64_tr_b16 (2 x 32) (MI355X_MICROARCH.md "LDS"), a stride of
+// HD + 8 put two rows of every 16-row fragment read (rowfrag) and of every 8-row transposed read (trfrag) on the
+// same banks — 8 / 4 LDS cycles per wave-instruction for 4 / 2 conflict-free; HD + 16 (an odd multiple of 32 bytes
+// past a multiple of 128) spreads them over all 64 banks for hd 64, 96 and 128 (round 5; the r04 PMC pass measured
+// SQ_LDS_BANK_CONFLICT at 0.32-0.39 of these kernels' LDS cycles, profiles/r04_pmc_lds.txt). Measured: no change
+// in time (B = 128, S = 65: forward 22.2 -> 22.1 µs, backward 45.1 -> 44.7; profiles/r05_attn_ldr_ab.txt) — the LDS
+// was not what bounds these launches; kept for the conflict-free reads.
+__host__ __device__ constexpr int ldr_of(int hd) { return hd + 16; }
 
 template <int LDR>
 __device__ __forceinline__ uint4 rowfrag(const bf16_t* base, int r0, int k0, int lane) {
@@ -366,7 +375,7 @@ __device__ __forceinline__ uint4 trfrag(const bf16_t* base, int r0, int c0, int 
 template <int HD>
 __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint32_t thr, float inv_keep) {
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
-  constexpr int LDR = HD + 8;
+  constexpr int LDR = ldr_of(HD);
   constexpr int NKS = HD / 32;  // 32-deep k steps over the head dim
   constexpr int NDT = HD / 16;  // 16-wide head-dim tiles of the outputs
   constexpr int CPR = HD / 8;   // 16-byte chunks per row
@@ -596,7 +605,7 @@ __global__ __launch_bounds__(512) void bwd2_kernel(icap_attn_args p, Geo g, uint
 template <int HD>
 __global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint32_t thr, float inv_keep) {
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
-  constexpr int LDR = HD + 8;
+  constexpr int LDR = ldr_of(HD);
   constexpr int NKS = HD / 32;
   constexpr int NDT = HD / 16;
   constexpr int CPR = HD / 8;
@@ -710,7 +719,7 @@ __global__ __launch_bounds__(512) void fwd2_kernel(icap_attn_args p, Geo g, uint
 template <int HD>
 __global__ __launch_bounds__(HD == 64 ? 1024 : 512) void fwd3_kernel(icap_attn_args p, Geo g, uint32_t thr, float inv_keep) {
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
-  constexpr int LDR = HD + 8;
+  constexpr int LDR = ldr_of(HD);
   constexpr int NKS = HD / 32;
   constexpr int NDT = HD / 16;
   constexpr int CPR = HD / 8;
@@ -845,7 +854,7 @@ size_t mfma_bwd_lds(const amfma::Geo& g) {
   return 2 * (3 * (size_t)g.hd * g.ldT + 2 * (size_t)g.Sp16 * g.ldT + 4 * 16 * (size_t)g.ldT);
 }
 
-size_t mfma_fwd2_lds(const amfma::Geo& g) { return 2 * 2 * (size_t)g.Sp32 * (g.hd + 8); }
+size_t mfma_fwd2_lds(const amfma::Geo& g) { return 2 * 2 * (size_t)g.Sp32 * amfma::ldr_of(g.hd); }
 
 static bool mfma_fwd2_ok(const icap_attn_args* a) {
   if ((a->ld_out & 3) || (a->ld_qkv & 7)) return false;
@@ -855,7 +864,7 @@ static bool mfma_fwd2_ok(const icap_attn_args* a) {
 }
 
 size_t mfma_bwd2_lds(const amfma::Geo& g) {
-  return 2 * (3 * (size_t)g.Sp32 + (size_t)g.Sp16) * (g.hd + 8) + 2 * sizeof(float) * (size_t)g.Sp32 +
+  return 2 * (3 * (size_t)g.Sp32 + (size_t)g.Sp16) * amfma::ldr_of(g.hd) + 2 * sizeof(float) * (size_t)g.Sp32 +
          (size_t)g.Sp32;
 }
 
@@ -870,7 +879,7 @@ static bool mfma_bwd2_ok(const icap_attn_args* a) {
   return waves * 64 <= 512 && mfma_bwd2_lds(g) <= 160 * 1024;
 }
 
-size_t mfma_fwd3_lds(const amfma::Geo& g) { return 2 * 2 * (size_t)g.Sp32 * (g.hd + 8); }
+size_t mfma_fwd3_lds(const amfma::Geo& g) { return 2 * 2 * (size_t)g.Sp32 * amfma::ldr_of(g.hd); }
 
 // long-sequence forward (v3): S past 8 key tiles, K/V of the whole sequence in LDS
 static bool mfma_fwd3_ok(const icap_attn_args* a) {

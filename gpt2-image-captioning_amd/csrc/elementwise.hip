@@ -1115,6 +1115,111 @@ __global__ __launch_bounds__(1024) void greedy_next_kernel(int64_t V, const T* _
   }
 }
 
+// Split form (round 5): a 1024-thread block per row left half the CUs idle at B = 128 and read its 100 KB row at
+// one CU's intake (11 µs per decode step). Here GS blocks of 256 threads per row each take a contiguous column
+// range and leave (max, first index) in the row's x slot (D elements, free until the finish kernel rewrites it),
+// and a second launch takes the partials in range order (the first maximum wins: the same token as the single
+// block, NaN and ties included) and does the latch and the embedding of the next token.
+constexpr int GSPLIT = 8;
+template <typename T>
+__global__ __launch_bounds__(256) void greedy_part_kernel(int64_t V, const T* __restrict__ logits, int64_t ld,
+                                                        int64_t chunk, T* __restrict__ x, int D, int vec) {
+  constexpr int NT = 256, NW = NT / 64;
+  __shared__ float rv[NW];
+  __shared__ int64_t ri[NW];
+  const int b = blockIdx.y, sidx = blockIdx.x;
+  const int64_t c0 = (int64_t)sidx * chunk, c1 = c0 + chunk < V ? c0 + chunk : V;
+  const T* row = logits + (int64_t)b * ld;
+  float best = -INFINITY;
+  int64_t bi = V;
+  auto consider = [&](float v, int64_t j) {
+    if (argmax_better(v, j, best, bi)) { best = v; bi = j; }
+  };
+  int64_t j0 = c0;
+  if constexpr (sizeof(T) == 2) {
+    if (vec == 2) {  // c0 % 8 == 0 (chunk is a multiple of 8): 16-byte loads, first maximum per thread by strict >
+      const int64_t q0b = c0 >> 3, q1 = c1 >> 3;
+      float fb = -INFINITY;
+      int64_t fi = V;
+      bool nan = false;
+      for (int64_t q = q0b + threadIdx.x; q < q1; q += NT) {
+        const uint4 w = *reinterpret_cast<const uint4*>(row + 8 * q);
+        const uint32_t h[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v0 = __uint_as_float(h[e] << 16), v1 = __uint_as_float(h[e] & 0xffff0000u);
+          nan |= (v0 != v0) | (v1 != v1);
+          if (v0 > fb) { fb = v0; fi = 8 * q + 2 * e; }
+          if (v1 > fb) { fb = v1; fi = 8 * q + 2 * e + 1; }
+        }
+      }
+      if (__syncthreads_or(nan)) {
+        for (int64_t q = q0b + threadIdx.x; q < q1; q += NT) {
+          float v[8];
+          io<T>::ld8(row + 8 * q, v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) consider(v[e], 8 * q + e);
+        }
+      } else {
+        best = fb;
+        bi = fi;
+      }
+      j0 = q1 << 3;
+    }
+  }
+  for (int64_t j = j0 + threadIdx.x; j < c1; j += NT) consider(io<T>::ld(row + j), j);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int64_t oi = __shfl_xor(bi, o, 64);
+    if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { rv[w] = best; ri[w] = bi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float bv = rv[0];
+    int64_t bj = ri[0];
+    for (int k = 1; k < NW; ++k)
+      if (argmax_better(rv[k], ri[k], bv, bj)) { bv = rv[k]; bj = ri[k]; }
+    int32_t* slot = reinterpret_cast<int32_t*>(x + (int64_t)b * D) + 2 * sidx;
+    slot[0] = __float_as_int(bv);
+    slot[1] = (int32_t)(bj < V ? bj : V);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void greedy_finish_kernel(int64_t V, int nsplit, int64_t eos,
+                                                          const int64_t* __restrict__ forced, int32_t* finished,
+                                                          int64_t* tokens, int64_t ld_tokens, int step,
+                                                          const T* __restrict__ wte, const T* __restrict__ wpe,
+                                                          int pos, int D, T* __restrict__ x) {
+  __shared__ int64_t nxt;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) {
+    const int32_t* slot = reinterpret_cast<const int32_t*>(x + (int64_t)b * D);
+    float bv = -INFINITY;
+    int64_t bj = V;
+    for (int k = 0; k < nsplit; ++k) {
+      const float v = __int_as_float(slot[2 * k]);
+      const int64_t j = slot[2 * k + 1];
+      if (argmax_better(v, j, bv, bj)) { bv = v; bj = j; }
+    }
+    if (bj >= V) bj = 0;
+    if (forced) bj = forced[b];
+    int fin = finished[b];
+    if (fin) bj = eos;
+    if (bj == eos) fin = 1;
+    finished[b] = fin;
+    tokens[(int64_t)b * ld_tokens + step] = bj;
+    nxt = bj;
+  }
+  __syncthreads();
+  const int64_t id = nxt;
+  for (int d = threadIdx.x; d < D; d += blockDim.x)
+    io<T>::st(x + (int64_t)b * D + d, io<T>::ld(wte + id * D + d) + io<T>::ld(wpe + (int64_t)pos * D + d));
+}
+
 template <typename T>
 __global__ void add_position_kernel(int B, int npos, int D, const T* __restrict__ src, int64_t sbs, int64_t sts,
                                     const T* __restrict__ wpe, int pos0, T* __restrict__ x) {
@@ -1741,6 +1846,18 @@ extern "C" int icap_greedy_next(int32_t dtype, int32_t B, int64_t V, const void*
   const int es = dtype == ICAP_BF16 ? 2 : 4;
   const uintptr_t lp = reinterpret_cast<uintptr_t>(logits);
   const int vec = (es == 2 && ld % 8 == 0 && lp % 16 == 0) ? 2 : (ld % 4 == 0 && lp % (4 * es) == 0) ? 1 : 0;
+  // split form when the next-token embedding row can hold the partials (8 bytes per split)
+  const int64_t chunk = ((V + GSPLIT - 1) / GSPLIT + 7) / 8 * 8;
+  if (x && (int64_t)D * es >= 8 * GSPLIT && (reinterpret_cast<uintptr_t>(x) & 7) == 0 && (D * es) % 8 == 0 &&
+      V >= 8 * GSPLIT) {
+    const int nsplit = (int)((V + chunk - 1) / chunk);
+    DISPATCH_T(dtype, hipLaunchKernelGGL(greedy_part_kernel<T>, dim3((unsigned)nsplit, (unsigned)B), dim3(256), 0,
+                                         S_(stream), V, CTP(logits), ld, chunk, TP(x), D, vec));
+    DISPATCH_T(dtype, hipLaunchKernelGGL(greedy_finish_kernel<T>, dim3((unsigned)B), dim3(256), 0, S_(stream), V,
+                                         nsplit, eos, forced, finished, tokens, ld_tokens, step, CTP(wte), CTP(wpe),
+                                         pos, D, TP(x)));
+    return check_launch("icap_greedy_next(split)");
+  }
   DISPATCH_T(dtype, hipLaunchKernelGGL(greedy_next_kernel<T>, dim3((unsigned)B), dim3(1024), 0, S_(stream), V,
                                        CTP(logits), ld, eos, forced, finished, tokens, ld_tokens, step, CTP(wte), CTP(wpe),
                                        pos, D, TP(x), vec));

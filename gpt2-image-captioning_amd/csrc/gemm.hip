@@ -716,6 +716,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   pl.splits = (int)splits;
   pl.nk_split = (int)nk_split;
   pl.variant = gemm_variant(p, nk_split);
+  // one row tile over many column tiles (the greedy decode's LM head, 128 x 50304 x 768): the double-buffered loop
+  // (20.8 vs 22.8 µs, profiles/r05_lmhead_probe.txt)
+  if (tiles_m == 1 && tiles_n > 256 && splits == 1 && pl.variant == 4) pl.variant = 0;
   // in-launch split-K: the double-buffered main loop at 2 blocks per CU for every split's K range (measured on the
   // packed 3584 x 768 x 3072 / x 2304 products: 36.6 / 30.4 vs 40.1 / 32.4 µs with the single-stage form the
   // per-split K of 16 stages would pick; profiles/r03_fused_ab.txt); ICAP_FUSED_NST=1 restores the variant rule
