@@ -447,6 +447,16 @@ static int r256_actk(const icap_gemm_args& p) {
   if (p.ln_stats_in) return (a == ACT_OFF || a == ACT_FWD + ICAP_ACT_GELU_NEW || a == ACT_FWD + ICAP_ACT_QUICK_GELU) ? ACT_LNF + a : -1;
   return a;
 }
+// epilogue kind of variant 24 (192 x 64 tiles), -1 where it has no form: bf16 row-major operands, no LayerNorm fold /
+// consumer; the statistics producer and activation-free launches get their own kinds, the rest the dispatching one
+static int w192_actk(const icap_gemm_args& p) {
+  if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.ln_wsum || p.ln_stats_in) return -1;
+  const bool plain = p.act == ICAP_ACT_NONE && p.dact == ICAP_ACT_NONE;
+  if (p.ln_stats_out) return (plain && p.c_dtype == ICAP_BF16) ? ACT_LNS : -1;
+  return plain ? ACT_OFF : ACT_ANY;
+}
+// (diagnostic build) ICAP_W192 = 1: take variant 24 for every eligible launch of path 0; 2: never automatically
+static int w192_mode() { return diag_env("ICAP_W192", 0); }
 // (diagnostic build) ICAP_R256 = 1: take variant 22 for every eligible unsplit launch of path 0
 static int r256_mode() { return diag_env("ICAP_R256", 0); }
 
@@ -495,7 +505,7 @@ static int fused_s_override() {
 // keeps the natural order (the path-equality tests compare it bitwise with the 256 x 256 kernel).
 static int kskew_for(const icap_gemm_args& p, int64_t nk_split) {
   static const int v = diag_env("ICAP_KSKEW", 1);
-  if (p.path == 1 || p.path == 6 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
+  if (p.path == 1 || p.path == 6 || p.path == 7 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
   return v > 0 && v < 256 ? v : 0;
 }
 // ICAP_GEMM_DIAG = 1 / 2 / 3: drop the A / B / both operands' staging loads of the tile kernels (zero-record
@@ -519,7 +529,7 @@ static int fused_nst_override() { return diag_env("ICAP_FUSED_NST", 0); }
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
-  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 6), "icap_gemm: path must be 0, 1, 3, 4, 5 or 6");
+  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 7), "icap_gemm: path must be 0, 1 or 3 ... 7");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16 || p.in_dtype == ICAP_FP8_MX,
                "icap_gemm: bad in_dtype");
@@ -770,6 +780,34 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
       return ICAP_OK;
     }
   }
+  // variant 24: 192 x 64 tiles, unsplit (path 7 forces it where eligible). The automatic plan takes it for the
+  // products with N <= 1024 that run unsplit on 128 x 64 tiles (K <= 16 stages: 3584 / 3200 / 6400 x 768 x 768 —
+  // one round of 228 / 204 tiles instead of 1.3-2.6 rounds) or on 128 x 128 tiles filling one to two rounds
+  // (CLIP's 6400 x 768 x 3072), measured 0.7-1.6 and 5 us faster per launch (profiles/r05_w192_ab.txt); the
+  // long-K products that split K inside the launch stay there (33.9 vs 43.9 us on the mapper's 3200 x 768 x 3072).
+  // A LayerNorm statistics producer takes the kernel its plain product takes (equal C, tests/test_lnfold_gpu.py;
+  // 17.0 vs 17.1 us for GPT-2's attn c_proj)
+  bool w24 = p.path == 7 || (p.path == 0 && w192_mode() == 1);
+  if (p.path == 0 && w192_mode() != 2 && !p.ln_stats_in && p.N <= 1024 && splits == 1 && !pl.fused && p.in_dtype == ICAP_BF16 && !p.trans_ab) {
+    const int64_t t192 = ((m_plan + 191) / 192) * ((p.N + 63) / 64);
+    if (narrow) w24 = true;
+    else if (nk_split > 16 && !p.m_dev && tiles_plan >= cus && tiles_plan <= 2 * cus && t192 <= 2 * cus) w24 = true;
+  }
+  if (p.M >= 192 && w24) {
+    if (const int a24 = w192_actk(p); a24 >= 0) {
+      pl.variant = 24;
+      pl.splits = 1;
+      pl.fused = false;
+      pl.nk_split = (int)nk;
+      tiles_n = (p.N + 63) / 64;
+      tiles = ((p.M + 191) / 192) * tiles_n;
+      pl.tiles_n = (int)tiles_n;
+      pl.actk = a24;
+      pl.block = dim3(GNT);
+      pl.grid = dim3((unsigned)tiles);
+      return ICAP_OK;
+    }
+  }
   pl.tiles_n = (int)tiles_n;
   const bool any_act = (splits == 1 || pl.fused) && (p.act != ICAP_ACT_NONE || p.dact != ICAP_ACT_NONE);
   pl.actk = any_act ? ACT_ANY : ACT_OFF;
@@ -817,6 +855,7 @@ static const char* variant_kernel(int v) {
     case 14: return "gemm_kernel<%s, %s, 2, 2, 2, 2, 4, 4, true, %d>";
     case 16: return "gemm_kernel<%s, %s, 4, 1, 2, 2, 4, 4, false, %d>";
     case 22: return "gemm_kernel<%s, %s, 3, 1, 4, 2, 4, 4, false, %d>";
+    case 24: return "gemm_kernel<%s, %s, 2, 2, 4, 1, 3, 4, false, %d>";
     default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %d>";
   }
 }
@@ -914,6 +953,7 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const int nks = pl.nk_split | (kskew_for(p, pl.nk_split) << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
   if (pl.variant == 22) launch_tile_r256(pl, p, nks, s);                             // gemm_tile_r256.hip
+  else if (pl.variant == 24) launch_tile_w192(pl, p, nks, s);                        // gemm_tile_w192.hip
   else if (pl.actk >= ACT_LNS) launch_tile_ln(pl, p, nks, s);                      // gemm_tile_ln.hip
   else if (pl.actk >= ACT_FWD) launch_tile_act(pl, p, nks, s);                     // gemm_tile_act.hip
   else if (pl.variant == 14 || pl.variant == 15) launch_tile_kout(pl, p, nks, s);    // gemm_tile_kout.hip

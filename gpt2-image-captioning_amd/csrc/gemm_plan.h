@@ -28,6 +28,7 @@ void launch_tile_mx(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStr
 void launch_tile_f32(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);   // fp32 parity (0 / 4 / 5)
 void launch_tile_ln(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);    // LN statistics hand-off
 void launch_tile_r256(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);  // 256 x 128 ring (22)
+void launch_tile_w192(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);  // 192 x 64 (24)
 
 }  // namespace icap
 

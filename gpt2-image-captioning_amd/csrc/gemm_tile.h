@@ -110,7 +110,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   constexpr int NW = WM * WN;
   constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
   constexpr int STB = (BM + BN) * GROWB;    // bytes per stage
-  constexpr int EPR = NST >= 2 ? 32 : 16;   // rows per LDS-staged epilogue pass
+  // rows per LDS-staged epilogue pass (16 where a wave's 16 TM rows are no multiple of 32: the 192-row tiles)
+  constexpr int EPR = (NST >= 2 && (16 * TM) % 32 == 0) ? 32 : 16;
   constexpr int ELD = 16 * TN + 4;          // fp32 row stride of the epilogue staging tile
   static_assert(NW * EPR * ELD * 4 <= NST * STB, "epilogue staging must fit the stage buffers");
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "each wave stages whole 8-row DMA pieces");
@@ -530,7 +531,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(pbase, (uint64_t)PB * splits);
     // the other splits' partials, GI accumulator rows at a time (all loads of a group in flight together; one row
     // at 3-4 blocks per CU, whose register budget is 170 / 128)
-    constexpr int GI = MINB >= 3 ? 1 : 2;
+    constexpr int GI = (MINB >= 3 || TM % 2 != 0) ? 1 : 2;
 #pragma unroll
     for (int i0 = 0; i0 < TM; i0 += GI) {
       f32x4_t v[3][GI][TN];

@@ -115,7 +115,9 @@ typedef struct {
   /* 4 / 5 = the 256-row 8-phase kernel with 128- / 256-column tiles wherever its preconditions hold (bf16    */
   /*     A/B, no trans_ab / ln_gamma / split-K, M >= 256, K >= 64; m_dev and the LayerNorm hand-off allowed:   */
   /*     csrc/gemm8p.hip) — same use; 6 = the 256 x 128 tile kernel on the 3-stage ring (csrc/gemm_tile.h       */
-  /*     variant 22) for unsplit bf16 row-major launches, M >= 256 — same use.                                 */
+  /*     variant 22) for unsplit bf16 row-major launches, M >= 256 — same use; 7 = 192 x 64 tiles (variant 24:  */
+  /*     4 waves stacked in M) for bf16 row-major launches without a LayerNorm fold / consumer, M >= 192,       */
+  /*     unsplit — same use.                                                                                   */
   int32_t path;
   /* in_dtype == ICAP_FP8_MX: the E8M0 block scales of A (M rows) and B (N rows), K % 128 == 0, lda / ldb      */
   /* multiples of 16, 16-byte aligned. For a 128-element K stage s and 64-row group g, 256 bytes at offset      */
