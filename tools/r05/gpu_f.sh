@@ -1,15 +1,10 @@
 #!/bin/bash
-# r05 call F: the LN2 duplicate launch, row pattern and a quiet recomputation; patch embed / pack / CLIP tests
+# round-5 closing measurements: the bench line, its kernel trace (graph-replay window), HBM traffic by PMC
 set -o pipefail
-mkdir -p gpurun_out/r05f
-env ICAP_SIDE_DW=1 PROBE_LN2_DUP=1 PROBE_CALLS=8 timeout -k 10 300 python -u tools/ab/det_probe5.py > gpurun_out/r05f/det_dup_rows.txt 2>&1; rc=$?
-grep -v amdgpu.ids gpurun_out/r05f/det_dup_rows.txt | head -60
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_pack_gpu.py tests/test_kernels_gpu.py -k "pack or patch or im2col" > gpurun_out/r05f/tests.txt 2>&1
-rc=$?
-tail -5 gpurun_out/r05f/tests.txt
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_parity_gpu.py -k "clip or vit or dino" tests/test_bench_shape_gpu.py > gpurun_out/r05f/tests2.txt 2>&1
-rc=$?
-tail -5 gpurun_out/r05f/tests2.txt
-exit $rc
+O=gpurun_out/r05f; mkdir -p $O
+timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print(d['value'], d['ms_per_step'], r['frac'], r['gpt2_block'], d['greedy_captions_per_s'])"
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 -u bench.py --steps 10 --warmup 3 --no-decode --no-cpu-baseline --sweep "" > $O/prof_bench.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 1; }
+find $O/prof -name "*.db"
+bash tools/pmc_traffic.sh r05f/pmc || exit 1
