@@ -361,8 +361,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     //   RAW: stage kt is read after this wave's vmcnt wait for it and a barrier every wave passed after its own.
     //   WAR: stage kt+NST-1 is written into the slot read in iteration kt-1, whose reads every wave retired
     //        (lgkmcnt) before that iteration's MFMAs, i.e. before the barrier of iteration kt.
-    static_assert(!KOUT && !MX && sizeof(TI) == 2 && TM == 4 && TN == 4,
-                  "ring: bf16 row-major operands, 64 x 64 per wave");
+    static_assert(!KOUT && !MX && sizeof(TI) == 2 && (TM == 4 || TM == 3) && TN == 4,
+                  "ring: bf16 row-major operands, 64 x 64 or 48 x 64 per wave");
     constexpr int D = APW + BPW;  // DMA instructions per wave per stage
     typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
     const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>(smem);
@@ -396,29 +396,40 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       u32x4_t fa0[4], fb0[4], fa1[4], fb1[4];
       {
         const uint32_t a0 = sb + la[0], b0 = sb + lb[0], a1 = sb + la[1], b1 = sb + lb[1];
-        ICAP_RING_RD(fa0[0], a0, 0); ICAP_RING_RD(fa0[1], a0, 2048); ICAP_RING_RD(fa0[2], a0, 4096); ICAP_RING_RD(fa0[3], a0, 6144);
+        ICAP_RING_RD(fa0[0], a0, 0); ICAP_RING_RD(fa0[1], a0, 2048); ICAP_RING_RD(fa0[2], a0, 4096);
+        if constexpr (TM == 4) ICAP_RING_RD(fa0[3], a0, 6144);
         ICAP_RING_RD(fb0[0], b0, 0); ICAP_RING_RD(fb0[1], b0, 2048); ICAP_RING_RD(fb0[2], b0, 4096); ICAP_RING_RD(fb0[3], b0, 6144);
-        ICAP_RING_RD(fa1[0], a1, 0); ICAP_RING_RD(fa1[1], a1, 2048); ICAP_RING_RD(fa1[2], a1, 4096); ICAP_RING_RD(fa1[3], a1, 6144);
+        ICAP_RING_RD(fa1[0], a1, 0); ICAP_RING_RD(fa1[1], a1, 2048); ICAP_RING_RD(fa1[2], a1, 4096);
+        if constexpr (TM == 4) ICAP_RING_RD(fa1[3], a1, 6144);
         ICAP_RING_RD(fb1[0], b1, 0); ICAP_RING_RD(fb1[1], b1, 2048); ICAP_RING_RD(fb1[2], b1, 4096); ICAP_RING_RD(fb1[3], b1, 6144);
       }
-      asm volatile("s_waitcnt lgkmcnt(8)"
-                   : "+v"(fa0[0]), "+v"(fa0[1]), "+v"(fa0[2]), "+v"(fa0[3]), "+v"(fb0[0]), "+v"(fb0[1]), "+v"(fb0[2]),
-                     "+v"(fb0[3]));
+      // the first half's TM + 4 reads retired, the second half's TM + 4 still in flight
+      if constexpr (TM == 4)
+        asm volatile("s_waitcnt lgkmcnt(8)"
+                     : "+v"(fa0[0]), "+v"(fa0[1]), "+v"(fa0[2]), "+v"(fa0[3]), "+v"(fb0[0]), "+v"(fb0[1]), "+v"(fb0[2]),
+                       "+v"(fb0[3]));
+      else
+        asm volatile("s_waitcnt lgkmcnt(7)"
+                     : "+v"(fa0[0]), "+v"(fa0[1]), "+v"(fa0[2]), "+v"(fb0[0]), "+v"(fb0[1]), "+v"(fb0[2]), "+v"(fb0[3]));
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (NW > 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           mfma_chunk<TI>(acc[i][j], __builtin_bit_cast(uint4, fa0[i]), __builtin_bit_cast(uint4, fb0[j]));
       if constexpr (NW > 4) __builtin_amdgcn_s_setprio(0);
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(fa1[0]), "+v"(fa1[1]), "+v"(fa1[2]), "+v"(fa1[3]), "+v"(fb1[0]), "+v"(fb1[1]), "+v"(fb1[2]),
-                     "+v"(fb1[3]));
+      if constexpr (TM == 4)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(fa1[0]), "+v"(fa1[1]), "+v"(fa1[2]), "+v"(fa1[3]), "+v"(fb1[0]), "+v"(fb1[1]), "+v"(fb1[2]),
+                       "+v"(fb1[3]));
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(fa1[0]), "+v"(fa1[1]), "+v"(fa1[2]), "+v"(fb1[0]), "+v"(fb1[1]), "+v"(fb1[2]), "+v"(fb1[3]));
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (NW > 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           mfma_chunk<TI>(acc[i][j], __builtin_bit_cast(uint4, fa1[i]), __builtin_bit_cast(uint4, fb1[j]));

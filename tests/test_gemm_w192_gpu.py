@@ -1,5 +1,6 @@
 """The 192 x 64 tile kernel (variant 24: gemm_kernel<.., 2, 2, 4, 1, 3, 4, ..>, 4 waves stacked in M, csrc/
-gemm_tile_w192.hip) against the 128-row tile kernels and fp64.
+gemm_tile_w192.hip; past 16 k-stages the 4-stage LDS-DMA ring, variant 25: gemm_kernel<.., 4, 1, 4, 1, 3, 4, ..>)
+against the 128-row tile kernels and fp64.
 
 Both run the same MFMA 16x16x32 chain per output element (64-deep k-steps in order, their two 32-deep halves in
 order; the tile path with tile_only=True keeps the natural k order) and the shared epilogue, so the outputs are
@@ -27,8 +28,10 @@ SHAPES = [
 ]
 
 
-def _name(tc, act):
-    return f"icap::gemm_kernel<unsigned short, {tc}, 2, 2, 4, 1, 3, 4, false, {act}>"
+def _name(tc, act, K=0):
+    """variant 24 (double-buffered, 2 blocks / CU) up to 16 k-stages of 64, the 4-stage ring (variant 25) past that"""
+    form = "4, 1" if (K + 63) // 64 > 16 else "2, 2"
+    return f"icap::gemm_kernel<unsigned short, {tc}, {form}, 4, 1, 3, 4, false, {act}>"
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
@@ -38,7 +41,7 @@ def test_w192_plain_matches_tile_and_fp64(dev, M, N, K):
     C = torch.full((M, N), 7.0, device=dev, dtype=torch.bfloat16)
     Ct = torch.empty_like(C)
     names = _run(lambda: ops.gemm(A, B, C, split_k=1, w192=True))
-    assert names == [_name("unsigned short", 0)], names
+    assert names == [_name("unsigned short", 0, K)], names
     ops.gemm(A, B, Ct, split_k=1, tile_only=True)
     torch.cuda.synchronize()
     _assert_same("C", C, Ct)

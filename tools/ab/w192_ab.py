@@ -1,8 +1,9 @@
 """Variant 24 (192 x 64 tiles, ops.gemm(w192=True)) against the automatic plan and hipBLASLt (torch.mm, plain
 products only) on the step's N = 768 products, each captured as 20 back-to-back launches in a HIP graph and replayed
-5 times (best per-launch us). w192 = path 7 (natural k order); w192s = the automatic plan with ICAP_W192=1, i.e.
-variant 24 with the K-skew the plan gives the 128-row tiles — needs the diagnostic build
-(ICAP_LIB=.../libicap_hip_stamps.so), where that switch is read at capture time."""
+5 times (best per-launch us). Forms (diagnostic build, ICAP_LIB=.../libicap_hip_stamps.so, whose switches are read
+at capture time): auto = the automatic plan; p7 = path 7 (natural k order: variant 24 up to 16 k-stages, the
+4-stage ring variant 25 past that); p7r3 / p7n2 = path 7 with the 3-stage ring / the double-buffered loop for long
+K (ICAP_W192R = 3 / 2); w192s = the automatic plan forced to the 192-row tiles with its K-skew (ICAP_W192 = 1)."""
 import os
 import sys
 
@@ -51,7 +52,9 @@ def per_launch(body):
 
 
 g = torch.Generator(device="cpu").manual_seed(0)
-print(f"{'shape':48s} {'auto':>8s} {'w192':>8s} {'w192s':>8s} {'hipBLASLt':>10s}   (us per launch, graph replay; auto kernel)")
+FORMS = [("auto", {}, {}), ("p7", {}, dict(w192=True)), ("p7r3", {"ICAP_W192R": "3"}, dict(w192=True)),
+         ("p7n2", {"ICAP_W192R": "2"}, dict(w192=True)), ("w192s", {"ICAP_W192": "1"}, {})]
+print(f"{'shape':48s} " + " ".join(f"{f[0]:>8s}" for f in FORMS) + f" {'hipBLASLt':>10s}   (us per launch, graph replay)")
 for M, live, N, K, epi, what in SHAPES:
     rows = live or M
     A = (torch.rand((M, K), generator=g) * 2 - 1).to(dev, torch.bfloat16)
@@ -66,21 +69,21 @@ for M, live, N, K, epi, what in SHAPES:
             kw["ln_stats_out"] = torch.empty((M, N // 32, 2), device=dev)
     if live is not None:
         kw.update(m_dev=torch.tensor([live], dtype=torch.int32, device=dev), m_hint=live)
-    auto_name = names_of(lambda: ops.gemm(A, B, C, **kw))
-    ta = per_launch(lambda: ops.gemm(A, B, C, **kw))
-    ref = C[:rows].float().clone()
-    tw = per_launch(lambda: ops.gemm(A, B, C, w192=True, **kw))
-    ok = torch.allclose(C[:rows].float(), ref, rtol=2e-2, atol=2e-2)
-    os.environ["ICAP_W192"] = "1"
-    try:
-        ts = per_launch(lambda: ops.gemm(A, B, C, **kw))
-        sname = names_of(lambda: ops.gemm(A, B, C, **kw))
-    finally:
-        os.environ.pop("ICAP_W192", None)
-    ok = ok and torch.allclose(C[:rows].float(), ref, rtol=2e-2, atol=2e-2) and "4, 1, 3, 4" in sname
+    cells, ref, names = [], None, []
+    for name, env, extra in FORMS:
+        os.environ.update(env)
+        try:
+            t = per_launch(lambda: ops.gemm(A, B, C, **kw, **extra))
+            names.append(names_of(lambda: ops.gemm(A, B, C, **kw, **extra)).replace("gemm_kernel<bf16, bf16, ", "<"))
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+        got = C[:rows].float().clone()
+        ref = got if ref is None else ref
+        ok = torch.allclose(got, ref, rtol=2e-2, atol=2e-2)
+        cells.append(f"{t:7.1f}{' ' if ok else '!'}")
     lib = ""
     if epi == "plain":
         a = A[:rows]
         lib = f"{per_launch(lambda: torch.mm(a, B.t(), out=C[:rows])):10.1f}"
-    print(f"{what + f' {rows}x{N}x{K}':48s} {ta:8.1f} {tw:8.1f} {ts:7.1f}{' ' if ok else '!'} {lib:>10s}   {auto_name}",
-          flush=True)
+    print(f"{what + f' {rows}x{N}x{K}':48s} " + " ".join(cells) + f" {lib:>10s}   " + " | ".join(names), flush=True)
