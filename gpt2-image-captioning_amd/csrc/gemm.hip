@@ -795,14 +795,13 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   }
   if (p.M >= 192 && w24) {
     if (const int a24 = w192_actk(p); a24 >= 0) {
-      // K > 16 stages over one round of tiles: the 4-stage ring at one block per CU (ICAP_W192R in the diagnostic
-      // build: 2 = never, 3 = the 3-stage ring). Measured (profiles/r05_w192_ab.txt): GPT-2 c_attn dX 3584 x 768 x
+      // K > 16 stages over one round of tiles: the 4-stage ring at one block per CU (ICAP_W192R = 2 in the
+      // diagnostic build: never). Measured (profiles/r05_w192_ab.txt): GPT-2 c_attn dX 3584 x 768 x
       // 2304 28.1 µs on the ring, 33.0 double-buffered (29.4 with the automatic in-launch split-K); past one round
       // the double-buffered loop at 2 blocks per CU wins by far (CLIP fc2, 408 tiles: 48.2 vs 64.8 µs)
       const int wr = diag_env("ICAP_W192R", 4);
       const int64_t t192 = ((m_plan + 191) / 192) * ((p.N + 63) / 64);
-      pl.variant = nk > 16 && wr != 2 && t192 <= cus ? (wr == 3 ? 26 : wr == 5 ? 27 : 25) : 24;
-      if (wr == 6) pl.variant = 28;  // (diagnostic: the register-staged form for every length of K)
+      pl.variant = nk > 16 && wr != 2 && t192 <= cus ? 25 : 24;
       pl.splits = 1;
       pl.fused = false;
       pl.nk_split = (int)nk;
@@ -864,9 +863,6 @@ static const char* variant_kernel(int v) {
     case 22: return "gemm_kernel<%s, %s, 3, 1, 4, 2, 4, 4, false, %d>";
     case 24: return "gemm_kernel<%s, %s, 2, 2, 4, 1, 3, 4, false, %d>";
     case 25: return "gemm_kernel<%s, %s, 4, 1, 4, 1, 3, 4, false, %d>";
-    case 26: return "gemm_kernel<%s, %s, 3, 1, 4, 1, 3, 4, false, %d>";
-    case 27: return "gemm_kernel<%s, %s, 5, 1, 4, 1, 3, 4, false, %d>";
-    case 28: return "gemm_kernel<%s, %s, 6, 2, 4, 1, 3, 4, false, %d>";
     default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %d>";
   }
 }
@@ -964,7 +960,7 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const int nks = pl.nk_split | (kskew_for(p, pl.nk_split) << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
   if (pl.variant == 22) launch_tile_r256(pl, p, nks, s);                             // gemm_tile_r256.hip
-  else if (pl.variant >= 24 && pl.variant <= 28) launch_tile_w192(pl, p, nks, s);   // gemm_tile_w192.hip
+  else if (pl.variant == 24 || pl.variant == 25) launch_tile_w192(pl, p, nks, s);   // gemm_tile_w192.hip
   else if (pl.actk >= ACT_LNS) launch_tile_ln(pl, p, nks, s);                      // gemm_tile_ln.hip
   else if (pl.actk >= ACT_FWD) launch_tile_act(pl, p, nks, s);                     // gemm_tile_act.hip
   else if (pl.variant == 14 || pl.variant == 15) launch_tile_kout(pl, p, nks, s);    // gemm_tile_kout.hip

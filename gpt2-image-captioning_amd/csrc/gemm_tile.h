@@ -109,21 +109,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   static_assert(!MX || (!KOUT && TM == 4 && TN == 4 && WM == 2 && WN == 2), "MX fp8: 128 x 128 tiles of 4 waves");
   constexpr int NW = WM * WN;
   constexpr int BM = 16 * WM * TM, BN = 16 * WN * TN;
-  // NST 5: the 4-slot ring with the next stage's fragments read during this stage's MFMAs (PLR, below)
-  constexpr bool PLR = NST == 5;
-  // NST 6: two LDS slots filled through registers (global loads -> VGPRs -> ds_write), the next stage's loads in
-  // flight under this stage's MFMAs (RS, below)
-  constexpr bool RS = NST == 6;
-  constexpr int NS = PLR ? 4 : RS ? 2 : NST;  // LDS stage slots
   constexpr int STB = (BM + BN) * GROWB;    // bytes per stage
   // rows per LDS-staged epilogue pass (16 where a wave's 16 TM rows are no multiple of 32: the 192-row tiles)
   constexpr int EPR = (NST >= 2 && (16 * TM) % 32 == 0) ? 32 : 16;
   constexpr int ELD = 16 * TN + 4;          // fp32 row stride of the epilogue staging tile
-  static_assert(NW * EPR * ELD * 4 <= NS * STB, "epilogue staging must fit the stage buffers");
+  static_assert(NW * EPR * ELD * 4 <= NST * STB, "epilogue staging must fit the stage buffers");
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "each wave stages whole 8-row DMA pieces");
   constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW);  // DMA instructions per wave per stage
   // (+ the consumer's LayerNorm row table, LNX == 2: its own 8 BM bytes past the stage buffers)
-  __shared__ __attribute__((aligned(16))) char smem[NS * STB + (LNX == 2 ? 8 * BM : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[NST * STB + (LNX == 2 ? 8 * BM : 0)];
   constexpr int ES = sizeof(TI);
   constexpr int EPC = 16 / ES;         // elements per 16-byte chunk
   constexpr int BKE = GROWB / ES;      // K elements per stage
@@ -223,7 +217,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   // over the loaded pairs, no E[x^2] - mean^2 cancellation); rstd = 1 / sqrt(M2 / K + eps). Computed in the prologue,
   // right after the first stage's DMA is issued (its loads overlap that DMA instead of adding a dependent round
   // trip to the epilogue), into an LDS table of its own that the epilogue rows read after the main loop's barriers.
-  float* lnr = reinterpret_cast<float*>(smem + NS * STB);
+  float* lnr = reinterpret_cast<float*>(smem + NST * STB);
   auto ln_prologue = [&]() __attribute__((always_inline)) {
     if constexpr (LNX == 2) {
       static_assert(NW * 64 == 2 * BM, "two threads per LN table row");
@@ -354,51 +348,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     }
   };
 
-  if constexpr (RS) {
-    // Register-staged double buffer (round 5, an A/B against the LDS-DMA forms): hipBLASLt stages its tiles through
-    // registers (profiles/r05_blaslt_kernels.txt). Iteration kt reads stage kt's fragments from its slot, writes stage
-    // kt+1 (loaded into registers during iteration kt-1) into the other slot, issues the loads of stage kt+2, runs the
-    // MFMAs and passes one barrier. The LDS image is the DMA's (lane l of piece i: row 8 i + l / 8, physical chunk l % 8
-    // holding source chunk (l % 8) ^ row % 8), so the fragment reads and the arithmetic are the other forms'.
-    //   RAW: stage kt+1 is written before the barrier that ends iteration kt and read after it.
-    //   WAR: the slot written in iteration kt was read in iteration kt-1, before that iteration's barrier.
-    static_assert(!KOUT && !MX && LNX != 2, "register-staged form: row-major bf16 / f32 operands, no LN consumer");
-    constexpr int D = APW + BPW;
-    uint4 R[D];
-    auto gload = [&](int64_t k0) __attribute__((always_inline)) {
-      const uint32_t kb = (uint32_t)(k0 * ES);
-      const bool kin = k0 + lchunk < K;
-#pragma unroll
-      for (int i = 0; i < APW; ++i) R[i] = bload(ra_rsrc, kin ? a_off[i] + kb : OOB);
-#pragma unroll
-      for (int i = 0; i < BPW; ++i) R[APW + i] = bload(rb_rsrc, kin ? b_off[i] + kb : OOB);
-    };
-    auto lwrite = [&](int slot) __attribute__((always_inline)) {
-      char* As = smem + slot * STB;
-      char* Bs = As + BM * GROWB;
-#pragma unroll
-      for (int i = 0; i < APW; ++i) *reinterpret_cast<uint4*>(As + (wave * APW + i) * 8 * GROWB + lane * 16) = R[i];
-#pragma unroll
-      for (int i = 0; i < BPW; ++i) *reinterpret_cast<uint4*>(Bs + (wave * BPW + i) * 8 * GROWB + lane * 16) = R[APW + i];
-    };
-    gload(kbase + kstep(0));
-    lwrite(0);
-    if (nk > 1) gload(kbase + kstep(1));
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      frag_t af[KS][TM], bfr[KS][TN];
-      read_frags(smem + (kt & 1) * STB, af, bfr);
-      if (kt + 1 < nk) {
-        lwrite((kt + 1) & 1);
-        if (kt + 2 < nk) gload(kbase + kstep(kt + 2));
-      }
-      mfmas(af, bfr);
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's slot writes landed (no vmcnt: kt+2 in flight)
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else if constexpr (NST >= 3) {
+  if constexpr (NST >= 3) {
     // Deep ring for launches with about one tile per CU (the packed step's N = 768 products, round 3: 128 x 128
     // tiles, 4 LDS stages = 128 KiB) and for the 256 x 128 tiles of 8 waves (round 5: 3 stages of 48 KiB = 144 KiB):
     // one block per CU, NST - 2 stages in flight while stage kt is read and stage kt + NST - 1 is issued. The round-5
@@ -424,76 +374,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
       lb[ks] = (uint32_t)(BM * GROWB + (wn * 16 * TN + fr) * GROWB) + sw;
     }
 #pragma unroll
-    for (int s = 0; s < NS - 1; ++s)
+    for (int s = 0; s < NST - 1; ++s)
       if (s < nk) load_stage(kbase + kstep(s), s);
     ln_prologue();  // (its loads are waited for at their first use, which drains the prologue's DMA once)
 #define ICAP_RING_RD(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:" #off : "=v"(dst) : "v"(addr))
-    if constexpr (PLR) {
-      // Fragment prefetch across stages (round 5): iteration kt retires stage kt+1's DMA and passes the barrier
-      // first, then issues the DMA of stage kt+3 and the LDS reads of stage kt+1's fragments, and runs stage kt's
-      // MFMAs (fragments read in iteration kt-1) while those reads are in flight — the ring above waits for the first
-      // half of its own stage's reads after every barrier.
-      //   RAW: stage kt+1 is read after this wave's vmcnt wait for it and a barrier every wave passed after its own.
-      //   WAR: stage kt+3 goes into the slot of stage kt-1, whose reads were issued in iteration kt-2 and retired
-      //        (lgkmcnt(0)) before that iteration ended, i.e. before the barrier of iteration kt-1.
-      static_assert(LNX != 2, "fragment-prefetch ring: no LayerNorm consumer form");
-      u32x4_t F[2][2][8];  // [parity][k half][A rows 0..TM-1, B rows at 4..7]
-      auto rd = [&](auto pc, int slot, u32x4_t (&F)[2][2][8]) __attribute__((always_inline)) {
-        constexpr int q = decltype(pc)::value;
-        const uint32_t sb = sbase + (uint32_t)(slot * STB);
-        const uint32_t a0 = sb + la[0], b0 = sb + lb[0], a1 = sb + la[1], b1 = sb + lb[1];
-        ICAP_RING_RD(F[q][0][0], a0, 0); ICAP_RING_RD(F[q][0][1], a0, 2048); ICAP_RING_RD(F[q][0][2], a0, 4096);
-        if constexpr (TM == 4) ICAP_RING_RD(F[q][0][3], a0, 6144);
-        ICAP_RING_RD(F[q][0][4], b0, 0); ICAP_RING_RD(F[q][0][5], b0, 2048); ICAP_RING_RD(F[q][0][6], b0, 4096); ICAP_RING_RD(F[q][0][7], b0, 6144);
-        ICAP_RING_RD(F[q][1][0], a1, 0); ICAP_RING_RD(F[q][1][1], a1, 2048); ICAP_RING_RD(F[q][1][2], a1, 4096);
-        if constexpr (TM == 4) ICAP_RING_RD(F[q][1][3], a1, 6144);
-        ICAP_RING_RD(F[q][1][4], b1, 0); ICAP_RING_RD(F[q][1][5], b1, 2048); ICAP_RING_RD(F[q][1][6], b1, 4096); ICAP_RING_RD(F[q][1][7], b1, 6144);
-      };
-      auto rd_wait = [&](auto pc, u32x4_t (&F)[2][2][8]) __attribute__((always_inline)) {  // lgkmcnt(0), tied to the registers it retires
-        constexpr int q = decltype(pc)::value;
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(F[q][0][0]), "+v"(F[q][0][1]), "+v"(F[q][0][2]), "+v"(F[q][0][3]), "+v"(F[q][0][4]),
-                       "+v"(F[q][0][5]), "+v"(F[q][0][6]), "+v"(F[q][0][7]));
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(F[q][1][0]), "+v"(F[q][1][1]), "+v"(F[q][1][2]), "+v"(F[q][1][3]), "+v"(F[q][1][4]),
-                       "+v"(F[q][1][5]), "+v"(F[q][1][6]), "+v"(F[q][1][7]));
-      };
-      if constexpr (TM == 3) {  // (the unused A slot is tied by the waits: give it a value)
-        F[0][0][3] = F[0][1][3] = F[1][0][3] = F[1][1][3] = (u32x4_t){0u, 0u, 0u, 0u};
-      }
-      // prologue: stage 0 landed (stages 1, 2 stay in flight), its fragments read
-      if (nk > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");
-      else if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      rd(std::integral_constant<int, 0>{}, 0, F);
-      rd_wait(std::integral_constant<int, 0>{}, F);
-      auto step = [&](auto pc, int kt, u32x4_t (&F)[2][2][8]) __attribute__((always_inline)) {
-        constexpr int q = decltype(pc)::value, qn = q ^ 1;
-        __builtin_amdgcn_sched_barrier(0);
-        if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");  // stage kt+1 in, kt+2 in flight
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if (kt + 3 < nk) load_stage(kbase + kstep(kt + 3), (kt + 3) & 3);
-        if (kt + 1 < nk) rd(std::integral_constant<int, qn>{}, (kt + 1) & 3, F);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              mfma_chunk<TI>(acc[i][j], __builtin_bit_cast(uint4, F[q][ks][i]), __builtin_bit_cast(uint4, F[q][ks][4 + j]));
-        __builtin_amdgcn_sched_barrier(0);
-        rd_wait(std::integral_constant<int, qn>{}, F);
-      };
-      for (int kt = 0; kt < nk; kt += 2) {
-        step(std::integral_constant<int, 0>{}, kt, F);
-        if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1, F);
-      }
-    } else
     for (int kt = 0; kt < nk; ++kt) {
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (NST == 4) {

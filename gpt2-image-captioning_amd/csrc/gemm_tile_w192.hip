@@ -8,21 +8,15 @@ namespace icap {
 // = 228 tiles, one round over 256 CUs, where 128 x 64 tiles make 336 (1.3 rounds) and 128 x 128 make 168 (two thirds
 // of the CUs). hipBLASLt runs those shapes on one round of 128 x 96 tiles (profiles/r05_blaslt_kernels.txt); 96
 // columns per tile do not split into the 32-column groups of the LayerNorm statistics epilogue, 64 do.
-// Variants 25 / 26: the same tiles on the LDS-DMA ring (gemm_tile.h NST 4 / 3: three / two stages in flight, one
-// block per CU) for long K; 27: the 4-slot ring with the next stage's fragments read under this stage's MFMAs;
-// 28: register-staged double buffer (global loads -> VGPRs -> ds_write, as hipBLASLt stages).
+// Variant 25: the same tiles on the LDS-DMA ring (gemm_tile.h NST 4: three stages in flight, one
+// block per CU) for long K. (Round 5 also measured a fragment prefetch across the ring's stages and a register-staged
+// double buffer on these tiles — bitwise equal, neither faster: profiles/r05_w192_ab.txt; removed.)
 void launch_tile_w192(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s) {
   ICAP_TILE_PRELUDE;
 #define ICAP_GKW(TC, KIND)                                                                                                 \
   do {                                                                                                                     \
     if (pl.variant == 25)                                                                                                  \
       hipLaunchKernelGGL((gemm_kernel<bf16_t, TC, 4, 1, 4, 1, 3, 4, false, KIND>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
-    else if (pl.variant == 28)                                                                                             \
-      hipLaunchKernelGGL((gemm_kernel<bf16_t, TC, 6, 2, 4, 1, 3, 4, false, KIND>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
-    else if (pl.variant == 27)                                                                                             \
-      hipLaunchKernelGGL((gemm_kernel<bf16_t, TC, 5, 1, 4, 1, 3, 4, false, KIND>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
-    else if (pl.variant == 26)                                                                                             \
-      hipLaunchKernelGGL((gemm_kernel<bf16_t, TC, 3, 1, 4, 1, 3, 4, false, KIND>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
     else                                                                                                                   \
       hipLaunchKernelGGL((gemm_kernel<bf16_t, TC, 2, 2, 4, 1, 3, 4, false, KIND>), grid, block, 0, s, p, tn, sp, nks, thr, inv_keep); \
   } while (0)
