@@ -455,7 +455,7 @@ static int w192_actk(const icap_gemm_args& p) {
   if (p.ln_stats_out) return (plain && p.c_dtype == ICAP_BF16) ? ACT_LNS : -1;
   return plain ? ACT_OFF : ACT_ANY;
 }
-// (diagnostic build) ICAP_W192 = 1: take variant 24 for every eligible launch of path 0; 2: never automatically
+// (diagnostic build) ICAP_W192 = 1: take variant 24 / 25 for every eligible launch of path 0; 2: never automatically
 static int w192_mode() { return diag_env("ICAP_W192", 0); }
 // (diagnostic build) ICAP_R256 = 1: take variant 22 for every eligible unsplit launch of path 0
 static int r256_mode() { return diag_env("ICAP_R256", 0); }
@@ -788,10 +788,15 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // A LayerNorm statistics producer takes the kernel its plain product takes (equal C, tests/test_lnfold_gpu.py;
   // 17.0 vs 17.1 us for GPT-2's attn c_proj)
   bool w24 = p.path == 7 || (p.path == 0 && w192_mode() == 1);
-  if (p.path == 0 && w192_mode() != 2 && !p.ln_stats_in && p.N <= 1024 && splits == 1 && !pl.fused && p.in_dtype == ICAP_BF16 && !p.trans_ab) {
+  if (p.path == 0 && w192_mode() != 2 && !p.ln_stats_in && p.N <= 1024 && p.in_dtype == ICAP_BF16 && !p.trans_ab) {
     const int64_t t192 = ((m_plan + 191) / 192) * ((p.N + 63) / 64);
-    if (narrow) w24 = true;
-    else if (nk_split > 16 && !p.m_dev && tiles_plan >= cus && tiles_plan <= 2 * cus && t192 <= 2 * cus) w24 = true;
+    if (splits == 1 && !pl.fused) {
+      if (narrow) w24 = true;
+      else if (nk_split > 16 && !p.m_dev && tiles_plan >= cus && tiles_plan <= 2 * cus && t192 <= 2 * cus) w24 = true;
+    }
+    // (Not for the launches that split K inside the launch: GPT-2's c_attn dX 3584 x 768 x 2304 runs 27.7-28.5 µs
+    // unsplit on the 192 x 64 ring against 29.4-30.1 split in isolation, but the step with that rule measured 0.5 %
+    // slower — 12833 / 12811 vs 12876 / 12895 images/s, profiles/r05_w192_ab.txt — so the split stays.)
   }
   if (p.M >= 192 && w24) {
     if (const int a24 = w192_actk(p); a24 >= 0) {

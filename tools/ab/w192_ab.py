@@ -3,8 +3,8 @@ products only) on the step's N = 768 products, each captured as 20 back-to-back 
 5 times (best per-launch us). Forms (diagnostic build, ICAP_LIB=.../libicap_hip_stamps.so, whose switches are read
 at capture time): auto = the automatic plan; p7 = path 7 (natural k order: variant 24 up to 16 k-stages, the
 4-stage ring variant 25 past that); p7r3 / p7n2 = path 7 with the 3-stage ring / the double-buffered loop for long
-K (ICAP_W192R = 3 / 2); p7r5 = the fragment-prefetch ring (ICAP_W192R = 5, variant 27); p7rs = register-staged double buffer for
-every K (ICAP_W192R = 6, variant 28); w192s = the automatic plan
+K (ICAP_W192R = 3 / 2; forms removed after round 5's third pass: p7r5 = fragment prefetch, p7rs = register staging);
+p7s2 / p7s3 = path 7 with K split 2 / 3 ways and combined inside the launch (ICAP_W192S); w192s = the automatic plan
 forced to the 192-row tiles with its K-skew (ICAP_W192 = 1). '!' = not allclose to auto; '#' = not bitwise equal to p7."""
 import os
 import sys
@@ -54,10 +54,8 @@ def per_launch(body):
 
 
 g = torch.Generator(device="cpu").manual_seed(0)
-FORMS = [("auto", {}, {}), ("p7", {}, dict(w192=True)), ("p7rs", {"ICAP_W192R": "6"}, dict(w192=True)),
-         ("p7r5", {"ICAP_W192R": "5"}, dict(w192=True)),
-         ("p7r3", {"ICAP_W192R": "3"}, dict(w192=True)),
-         ("p7n2", {"ICAP_W192R": "2"}, dict(w192=True)), ("w192s", {"ICAP_W192": "1"}, {})]
+FORMS = [("auto", {}, {}), ("p7", {}, dict(w192=True)), ("p7s2", {"ICAP_W192S": "2"}, dict(w192=True)),
+         ("p7s3", {"ICAP_W192S": "3"}, dict(w192=True)), ("p7n2", {"ICAP_W192R": "2"}, dict(w192=True))]
 print(f"{'shape':48s} " + " ".join(f"{f[0]:>8s}" for f in FORMS) + f" {'hipBLASLt':>10s}   (us per launch, graph replay)")
 for M, live, N, K, epi, what in SHAPES:
     rows = live or M
@@ -88,7 +86,7 @@ for M, live, N, K, epi, what in SHAPES:
         if name == "p7":
             p7 = got
         mark = " " if ok else "!"
-        if name in ("p7rs", "p7r5", "p7r3", "p7n2") and not torch.equal(got, p7):
+        if name in ("p7n2",) and not torch.equal(got, p7):
             mark = "#"  # not bitwise equal to path 7's default form (same k order: must be equal)
         cells.append(f"{t:7.1f}{mark}")
     lib = ""
