@@ -104,7 +104,9 @@ def extract_directory(image_dir: str, output_path: str, embed: Callable, process
             batch_names, batch_images = batch
             px = processor(images=batch_images).pixel_values
             if device is not None:
-                px = px.to(device, non_blocking=True)
+                # (pageable host memory: a plain copy — non_blocking buys nothing without a pinned source, and one
+                # suite run hung inside such a copy with the loader's workers alive; the packed path pins its buffer)
+                px = px.to(device)
         # the embeddings stay on the device until the end (one copy back, src/embeddings/clip.py:140 copies per
         # batch): no per-batch synchronisation, so the next batch's host work overlaps this batch's kernels
         embs.append(embed(px))
