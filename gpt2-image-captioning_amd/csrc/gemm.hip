@@ -416,7 +416,7 @@ int gemm8p_launch(const icap_gemm_args& p, int bn, int actk, uint32_t thr, float
 // of them. (diagnostic build) ICAP_GEMM8P = 0 never, 128 / 256 forced where eligible, default the shape rule.
 static int g8p_actk(const icap_gemm_args& p) {
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || (p.ln_wsum && !p.ln_stats_in) || p.split_k > 1) return -1;
-  if (p.M < 256 || p.K < 64 || p.path == 1 || p.path == 3 || p.path == 6) return -1;
+  if (p.M < 256 || p.K < 64 || p.path == 1 || p.path == 3 || p.path >= 6) return -1;
   if (p.M * p.lda >= (1ll << 30) || p.N * p.ldb >= (1ll << 30)) return -1;  // 32-bit DMA byte offsets per tile
   const int fa = p.dact == ICAP_ACT_NONE ? p.act : -1, ba = p.act == ICAP_ACT_NONE ? p.dact : -1;
   int a;
@@ -455,6 +455,29 @@ static int w192_actk(const icap_gemm_args& p) {
   if (p.ln_stats_out) return (plain && p.c_dtype == ICAP_BF16) ? ACT_LNS : -1;
   return plain ? ACT_OFF : ACT_ANY;
 }
+// epilogue kind of the split-role ring variants (26: 128 x 256, 27: 96 x 128), -1 where it has no form: bf16 row-major
+// operands, no ln_gamma / decode fold; 27 has no LayerNorm consumer (its 96-row tiles do not pair two threads per row)
+static int roles_actk(const icap_gemm_args& p, int v) {
+  if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || (p.ln_wsum && !p.ln_stats_in)) return -1;
+  const int fa = p.dact == ICAP_ACT_NONE ? p.act : -1, ba = p.act == ICAP_ACT_NONE ? p.dact : -1;
+  int a;
+  if (p.act == ICAP_ACT_NONE && p.dact == ICAP_ACT_NONE) a = ACT_OFF;
+  else if (v == 27) a = ACT_ANY;
+  else if (fa == ICAP_ACT_GELU_NEW) a = ACT_FWD + ICAP_ACT_GELU_NEW;
+  else if (ba == ICAP_ACT_GELU_NEW) a = ACT_BWD + ICAP_ACT_GELU_NEW;
+  else if (fa == ICAP_ACT_QUICK_GELU) a = ACT_FWD + ICAP_ACT_QUICK_GELU;
+  else a = ACT_ANY;
+  if (p.c_dtype != ICAP_BF16) return (p.ln_stats_out || p.ln_stats_in) ? -1 : (a == ACT_OFF ? ACT_OFF : ACT_ANY);
+  if (p.ln_stats_out) return a == ACT_OFF ? ACT_LNS : -1;
+  if (p.ln_stats_in) {
+    if (v == 27) return -1;
+    return (a == ACT_OFF || a == ACT_FWD + ICAP_ACT_GELU_NEW || a == ACT_FWD + ICAP_ACT_QUICK_GELU) ? ACT_LNF + a : -1;
+  }
+  return a;
+}
+// (diagnostic build) ICAP_ROLES = 0: never take variants 26 / 27 automatically
+static int roles_mode() { return diag_env("ICAP_ROLES", 1); }
+
 // (diagnostic build) ICAP_W192 = 1: take variant 24 / 25 for every eligible launch of path 0; 2: never automatically
 static int w192_mode() { return diag_env("ICAP_W192", 0); }
 // (diagnostic build) ICAP_R256 = 1: take variant 22 for every eligible unsplit launch of path 0
@@ -475,7 +498,7 @@ static int g256_mode() {
 // head 8320 x 50304 x 768: 758 vs 835 us), not on the train step's 2-round K = 768 products (8320 x 3072 x 768:
 // 84 vs 80 us) (profiles/r02_gemm256_bench.txt). path 3 forces it where eligible.
 static bool g256_pick(const icap_gemm_args& p) {
-  if (p.path == 1 || p.path == 4 || p.path == 5 || p.path == 6) return false;
+  if (p.path == 1 || (p.path >= 4 && p.path <= 9)) return false;
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.beta != 0.f || p.m_dev || p.split_k > 1) return false;
   if (p.ln_stats_out || p.ln_stats_in) return false;
   if (p.M < 256 || p.N < 256 || p.K < 64) return false;
@@ -505,7 +528,7 @@ static int fused_s_override() {
 // keeps the natural order (the path-equality tests compare it bitwise with the 256 x 256 kernel).
 static int kskew_for(const icap_gemm_args& p, int64_t nk_split) {
   static const int v = diag_env("ICAP_KSKEW", 1);
-  if (p.path == 1 || p.path == 6 || p.path == 7 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
+  if (p.path == 1 || p.path >= 6 || p.in_dtype == ICAP_FP8_MX || nk_split > 64) return 0;
   return v > 0 && v < 256 ? v : 0;
 }
 // ICAP_GEMM_DIAG = 1 / 2 / 3: drop the A / B / both operands' staging loads of the tile kernels (zero-record
@@ -527,9 +550,29 @@ static int fused_min_nk() {
 static int fused_nst_override() { return diag_env("ICAP_FUSED_NST", 0); }
 
 
+// The automatic choice of the split-role variants (0 = neither), one round of tiles at one block per CU (the kernel
+// walks the tiles, but a second round pays a whole prologue / main loop / epilogue with nothing beside it). Measured
+// against the automatic plan of round 5 (profiles/r06_roles_ab.txt, graph replay, packed rows): N <= 1024 on 96 x 128
+// tiles — GPT-2 c_attn dX 3584 x 768 x 2304 30.5 -> 20.3 us, c_fc dX x 3072 33.9 -> 24.4, mlp c_proj fwd (+ LayerNorm
+// statistics) 38.5 -> 28.1, attn c_proj 17.0 -> 14.4 / 12.4 -> 11.0, mapper 3200 x 768 x 3072 33.1 -> 25.3, CLIP fc2
+// 6400 x 768 x 3072 (1.6 rounds, long K) 53.2 -> 48.2; CLIP's 6400 x 768 x 768 (1.6 rounds, short K) 20.4 -> 23.0: not
+// taken. N > 1024 on 128 x 256 tiles where they fill one round: c_attn (LayerNorm consumer) 26.4 -> 24.5, mapper qkv
+// 22.5 -> 19.9; the N = 3072 products (336 tiles: two rounds) 36.9 -> 45.1: not taken. Long K over fewer tiles
+// (the LM-head dX, K = 50304 over 1792 rows) keeps the split-K kernels.
+static int roles_pick(const icap_gemm_args& p, int64_t m_plan, int64_t nk, int64_t cus) {
+  if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.split_k > 1) return 0;
+  if (p.N <= 1024) {
+    const int64_t t = ((m_plan + 95) / 96) * ((p.N + 127) / 128);
+    if (nk > 96 || t * 5 < cus * 3) return 0;
+    return (t <= cus || (nk >= 32 && 2 * t >= 3 * cus && t <= 2 * cus)) ? 27 : 0;
+  }
+  const int64_t t = ((m_plan + 127) / 128) * ((p.N + 255) / 256);
+  return (t <= cus && t * 5 >= cus * 3) ? 26 : 0;
+}
+
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
-  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 7), "icap_gemm: path must be 0, 1 or 3 ... 7");
+  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 9), "icap_gemm: path must be 0, 1 or 3 ... 9");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16 || p.in_dtype == ICAP_FP8_MX,
                "icap_gemm: bad in_dtype");
@@ -767,6 +810,27 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   }
   // the LayerNorm-folded quick_gelu consumer (CLIP c_fc) exists at 3 blocks / CU only (gemm_tile_ln.hip)
   if (lnx && pl.variant == 0 && p.act == ICAP_ACT_QUICK_GELU) pl.variant = 4;
+  // variants 26 / 27: the split-role ring (gemm_tile.h ROLES) on 128 x 256 / 96 x 128 tiles, one K range per tile
+  // (path 8 / 9 force them where eligible; the automatic rule: roles_pick)
+  {
+    const int rv = p.path == 8 ? 26 : p.path == 9 ? 27 : (p.path == 0 && roles_mode() != 0) ? roles_pick(p, m_plan, nk, cus) : 0;
+    const int bm = rv == 26 ? 128 : 96, bn = rv == 26 ? 256 : 128;
+    if (rv && p.M >= bm && p.split_k <= 1) {
+      if (const int ar = roles_actk(p, rv); ar >= 0) {
+        pl.variant = rv;
+        pl.splits = 1;
+        pl.fused = false;
+        pl.nk_split = (int)nk;
+        tiles_n = (p.N + bn - 1) / bn;
+        tiles = ((p.M + bm - 1) / bm) * tiles_n;
+        pl.tiles_n = (int)tiles_n;
+        pl.actk = ar;
+        pl.block = dim3(2 * GNT);
+        pl.grid = dim3((unsigned)(tiles < cus ? tiles : cus));  // the kernel walks the live tiles
+        return ICAP_OK;
+      }
+    }
+  }
   // variant 22: 256 x 128 tiles on the 3-stage ring (path 6 forces it where eligible)
   if (splits == 1 && p.M >= 256 && (p.path == 6 || (p.path == 0 && r256_mode() == 1))) {
     if (const int a22 = r256_actk(p); a22 >= 0) {
@@ -868,6 +932,8 @@ static const char* variant_kernel(int v) {
     case 22: return "gemm_kernel<%s, %s, 3, 1, 4, 2, 4, 4, false, %d>";
     case 24: return "gemm_kernel<%s, %s, 2, 2, 4, 1, 3, 4, false, %d>";
     case 25: return "gemm_kernel<%s, %s, 4, 1, 4, 1, 3, 4, false, %d>";
+    case 26: return "gemm_kernel<%s, %s, 3, 1, 2, 2, 4, 8, false, %d, true>";
+    case 27: return "gemm_kernel<%s, %s, 5, 1, 2, 2, 3, 4, false, %d, true>";
     default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %d>";
   }
 }
@@ -962,9 +1028,14 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   if (pl.g256) return gemm256_launch(p, thr, inv_keep, s);
   if (pl.g8p) return gemm8p_launch(p, pl.g8p, pl.actk, thr, inv_keep, s);
   const int sp = pl.splits;
-  const int nks = pl.nk_split | (kskew_for(p, pl.nk_split) << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
+  // (the split-role variants walk K in its natural order: one round of tiles, no lockstep panel misses to stagger,
+  // and automatic launches then equal forced ones and the tile path bitwise)
+  const int skew = (pl.variant == 26 || pl.variant == 27) ? 0 : kskew_for(p, pl.nk_split);
+  const int nks = pl.nk_split | (skew << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
-  if (pl.variant == 22) launch_tile_r256(pl, p, nks, s);                             // gemm_tile_r256.hip
+  if (pl.variant == 26) launch_tile_roles(pl, p, nks, s);                            // gemm_tile_roles.hip
+  else if (pl.variant == 27) launch_tile_roles96(pl, p, nks, s);                     // gemm_tile_roles96.hip
+  else if (pl.variant == 22) launch_tile_r256(pl, p, nks, s);                        // gemm_tile_r256.hip
   else if (pl.variant == 24 || pl.variant == 25) launch_tile_w192(pl, p, nks, s);   // gemm_tile_w192.hip
   else if (pl.actk >= ACT_LNS) launch_tile_ln(pl, p, nks, s);                      // gemm_tile_ln.hip
   else if (pl.actk >= ACT_FWD) launch_tile_act(pl, p, nks, s);                     // gemm_tile_act.hip

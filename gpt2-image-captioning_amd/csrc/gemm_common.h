@@ -93,6 +93,14 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint3
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(lds), 16, off, 0, 0, 0);
 }
 
+// same with the LDS destination as an integer byte address that the caller made wave-uniform (readfirstlane), so M0
+// is written from an SGPR with no waterfall loop. (Not through a generic pointer built from that integer: a value of
+// 0 — the first byte of LDS — would be cast to the LDS null, 0xffffffff.)
+__device__ __forceinline__ void dma16a(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t off) {
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(uintptr_t)lds, 16, off, 0, 0, 0);
+}
+
 // same with a wave-uniform soffset (row / k offsets in SGPRs, one per-lane VGPR offset)
 __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
   typedef __attribute__((address_space(3))) void* lds_ptr_t;

@@ -29,6 +29,8 @@ void launch_tile_f32(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipSt
 void launch_tile_ln(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);    // LN statistics hand-off
 void launch_tile_r256(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);  // 256 x 128 ring (22)
 void launch_tile_w192(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);  // 192 x 64 (24)
+void launch_tile_roles(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);    // roles 128 x 256 (26)
+void launch_tile_roles96(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);  // roles 96 x 128 (27)
 
 }  // namespace icap
 

@@ -79,6 +79,20 @@ __device__ __forceinline__ uint4 kout_frag(const char* img, int r0, int c0, int 
   return r;
 }
 
+// N fragment reads of 16 rows each (ds_read_b128, 2048 bytes apart) from LDS byte address a + BASE, as inline asm:
+// hipcc would wait vmcnt(0) for any in-flight LDS-DMA before an LDS read it can see (the roles / ring main loops
+// retire these reads with counted lgkmcnt waits instead)
+typedef uint32_t frag_u32x4_t __attribute__((ext_vector_type(4)));
+template <int I, int N, int BASE>
+struct lds_frags {
+  static __device__ __forceinline__ void run(frag_u32x4_t* f, uint32_t a) {
+    if constexpr (I < N) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[I]) : "v"(a), "n"(BASE + I * 2048));
+      lds_frags<I + 1, N, BASE>::run(f, a);
+    }
+  }
+};
+
 // Block geometry: WM x WN waves, each owning a (16 TM) x (16 TN) sub-tile of MFMA 16x16 accumulators, so the
 // block tile is BM = 16 WM TM by BN = 16 WN TN. One pipeline stage holds 128 bytes of K per row (bf16: 64 K,
 // f32: 32 K) for the BM rows of A and the BN rows of B in LDS.
@@ -95,11 +109,19 @@ __device__ __forceinline__ uint4 kout_frag(const char* img, int r0, int c0, int 
 // activation code is then not compiled into the kernel at all. Measured (profiles/r03_k768_counters.txt): with it
 // present, the plain 8320 x 2304 x 768 product ran 53.7 vs 45.0 us — the same memory instructions, +7 % VALU and
 // +22 % SQ_WAIT_ANY (the larger function scheduled its main loop worse), SQ_WAIT_INST_ANY +1 % (not instruction fetch).
-template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, int ACT = ACT_ANY>
-__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
-                                                                  int nk_split, uint32_t drop_thresh, float inv_keep) {
+// ROLES (round 6; variants 26 / 27): the block has twice the waves; waves 0 .. NW-1 read fragments and issue MFMAs
+// only (one per SIMD), waves NW .. 2 NW-1 issue the LDS-DMA of the NST-stage ring and wait for it (one per SIMD), so
+// the DMA's issue cost runs beside the MFMA stream instead of in front of it (the main loop below).
+template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, int ACT = ACT_ANY,
+          bool ROLES = false>
+// The body of one tile (gemm_kernel below runs it once per block, or, for ROLES, once per live tile of a grid-stride
+// loop): bid = the tile's block id in the capacity grid of tiles_m x tiles_n x splits blocks, Mv = the device row count.
+__device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int splits, int nk_split, uint32_t drop_thresh,
+                                          float inv_keep, const int bid, const int tiles_m, const int64_t Mv) {
   static_assert(!KOUT || (sizeof(TI) == 2 && 16 * WM * TM == 128 && 16 * WN * TN == 128),
                 "K-outer operands: bf16, 128 x 128 tiles");
+  static_assert(!ROLES || (!KOUT && sizeof(TI) == 2 && WM == 2 && WN == 2 && NST >= 3 && MINB == 1),
+                "roles: bf16 row-major operands, 2 x 2 MFMA waves, a ring of >= 3 stages, one block per CU");
   // MX block-scaled fp8 (TI = fp8_t): a stage's 128-byte LDS row is one 128-deep K step of
   // v_mfma_scale_f32_16x16x128_f8f6f4 (twice the bf16 flops per staged byte and per fragment byte read); the
   // per-32 E8M0 scales of the wave's 4 fragment rows of A and of B come in one 16-byte load each per stage
@@ -122,20 +144,20 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   constexpr int EPC = 16 / ES;         // elements per 16-byte chunk
   constexpr int BKE = GROWB / ES;      // K elements per stage
 
-  const int tid = threadIdx.x;
+  int tid = threadIdx.x;
+  // (ROLES runs this body in a loop over tiles: an opaque thread index keeps hipcc from hoisting the lane-dependent
+  // offsets of both roles out of the loop, where they would stay live through the whole body and spill)
+  if constexpr (ROLES) asm volatile("" : "+v"(tid));
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave - wm * WN;
 
   const int64_t M = p.M, N = p.N, K = p.K;
-  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < M ? (int64_t)*p.m_dev : M;  // device row count
   // bijective XCD-aware remap over the LIVE blocks: blocks sharing an XCD get consecutive tiles (consecutive
   // tiles share the A row panel). With a device row count the grid is sized for M but only the first
   // nlive = (row tiles of Mv) x tiles_n x splits blocks work: they are the lowest block ids, which the dispatcher
   // hands out first and round-robin over the XCDs, so the live tiles land one per CU before any CU takes a second
   // (the dead blocks exit at once), and the remap over nlive keeps every XCD's share contiguous.
-  const int bid = blockIdx.x;
-  const int tiles_m = (int)(gridDim.x / splits) / tiles_n;
   const int tiles_mv = p.m_dev ? (int)((Mv + BM - 1) / BM) : tiles_m;
   const int nwg = tiles_mv * tiles_n * splits;
   if (bid >= nwg) return;
@@ -348,7 +370,105 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     }
   };
 
-  if constexpr (NST >= 3) {
+  if constexpr (ROLES) {
+    // Split roles over an NST-stage LDS-DMA ring, one barrier per 64-deep k-step (tools/microbench/gemm_lab.hip,
+    // profiles/r06_gemm_lab.txt). Barrier B_k (k = 0 .. nk) is reached by
+    //   a loader wave after its DMA of stage k has landed (counted vmcnt: stages k+1 .. k+NST-2 stay in flight);
+    //   an MFMA wave after every fragment read of stage k-1 has retired (lgkmcnt(0)).
+    // After B_k the loaders issue stage k+NST-1 into the slot stage k-1 used (free: its reads retired before B_k), the
+    // MFMA waves read stage k. The MFMA waves read each 32-deep substep's fragments while the previous substep's MFMAs
+    // issue, so B_{k+1} falls between the two substeps of stage k: [wait F0] [read F1 of k] [MFMAs F0] [wait F1] B_{k+1}
+    // [read F0 of k+1] [MFMAs F1]. Loader waves never read LDS and MFMA waves never issue DMA, so no wave ever waits
+    // for LDS-DMA it did not issue except through a barrier.
+    // Stages past K are issued with out-of-range offsets (nothing is fetched, zeros land in a free slot), so every
+    // loop iteration has the same DMA count and the same vmcnt.
+    constexpr int P = (BM + BN) / (8 * NW);  // 1-KiB DMA pieces per loader wave per stage
+    constexpr int PA = BM / (8 * NW);        // of them A rows (pieces i < PA)
+    static_assert((BM + BN) % (8 * NW) == 0 && BM % (8 * NW) == 0 && (NST - 2) * P < 64, "roles: stage split");
+    const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>(smem);
+    if (wave >= NW) {
+      const int lw = wave - NW;
+      uint32_t voff[P];
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        const int q = i * NW + lw;  // 8-row piece of the [A tile; B tile] stack
+        const int row = (i < PA ? q : q - BM / 8) * 8 + lrow;
+        voff[i] = (uint32_t)((int64_t)row * (i < PA ? p.lda : p.ldb) + lchunk) * ES;
+      }
+      auto issue = [&](int kt, int slot) __attribute__((always_inline)) {
+        const bool live = kt < nk;
+        const int64_t k0 = live ? kbase + kstep(kt) : 0;
+        const uint32_t kb = (uint32_t)(k0 * ES);
+        const bool kin = live && k0 + lchunk < K;
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+          const uint32_t lds = __builtin_amdgcn_readfirstlane(sbase + (uint32_t)(slot * STB + (i * NW + lw) * 1024));
+          dma16a(i < PA ? ra_rsrc : rb_rsrc, lds, kin ? voff[i] + kb : OOB);
+        }
+      };
+#pragma unroll
+      for (int s = 0; s < NST - 1; ++s) issue(s, s);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * P) : "memory");
+      __builtin_amdgcn_s_barrier();  // B_0
+      for (int kt = 0; kt < nk; ++kt) {
+        issue(kt + NST - 1, (kt + NST - 1) % NST);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * P) : "memory");  // stage kt + 1 landed
+        __builtin_amdgcn_s_barrier();                                        // B_{kt+1}
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the past-K stages' zeros, before the epilogue reuses LDS
+    } else {
+    typedef frag_u32x4_t u32x4_t;
+    uint32_t la[2], lb[2];  // this lane's fragment row in a stage (A row / B row), swizzled chunk of substep ks
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint32_t sw = (uint32_t)(((ks * 4 + fg) ^ (fr & 7)) << 4);
+      la[ks] = (uint32_t)((wm * 16 * TM + fr) * GROWB) + sw;
+      lb[ks] = (uint32_t)((wn * 16 * TN + fr) * GROWB) + sw;
+    }
+    u32x4_t fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+    auto rd = [&](u32x4_t (&fa)[TM], u32x4_t (&fb)[TN], uint32_t a, uint32_t b) __attribute__((always_inline)) {
+      lds_frags<0, TM, 0>::run(fa, a);
+      lds_frags<0, TN, BM * GROWB>::run(fb, b);
+    };
+    // retire every outstanding fragment read; the empty asm ties make the MFMAs that use them wait here
+    auto retire = [&](u32x4_t (&fa)[TM], u32x4_t (&fb)[TN]) __attribute__((always_inline)) {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[i]));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[j]));
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mm = [&](const u32x4_t (&fa)[TM], const u32x4_t (&fb)[TN]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          mfma_chunk<TI>(acc[i][j], __builtin_bit_cast(uint4, fa[i]), __builtin_bit_cast(uint4, fb[j]));
+    };
+    ln_prologue();  // (its loads are the MFMA waves' only vector-memory operations)
+    __builtin_amdgcn_s_barrier();  // B_0
+    __builtin_amdgcn_sched_barrier(0);
+    rd(fa0, fb0, sbase + la[0], sbase + lb[0]);
+    for (int kt = 0; kt < nk; ++kt) {
+      const uint32_t sb = sbase + (uint32_t)((kt % NST) * STB);
+      retire(fa0, fb0);
+      rd(fa1, fb1, sb + la[1], sb + lb[1]);
+      mm(fa0, fb0);
+      retire(fa1, fb1);
+      __builtin_amdgcn_s_barrier();  // B_{kt+1}
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) {
+        const uint32_t sn = sbase + (uint32_t)(((kt + 1) % NST) * STB);
+        rd(fa0, fb0, sn + la[0], sn + lb[0]);
+      }
+      mm(fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    }
+    __syncthreads();  // every MFMA wave is done reading the ring and the loaders' DMA has drained
+  } else if constexpr (NST >= 3) {
     // Deep ring for launches with about one tile per CU (the packed step's N = 768 products, round 3: 128 x 128
     // tiles, 4 LDS stages = 128 KiB) and for the 256 x 128 tiles of 8 waves (round 5: 3 stages of 48 KiB = 144 KiB):
     // one block per CU, NST - 2 stages in flight while stage kt is read and stage kt + NST - 1 is issued. The round-5
@@ -490,7 +610,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   // Nobody waits on a block that has not taken its ticket, so there is no residency assumption
   // (cdna_hip_programming.md §5 "In-launch split-K reduction", §6 Guideline 16 R1 with sc1 loads).
   ICAP_STAMP(3, ICAP_NOW());
-  const bool fused = splits > 1 && p.tickets != nullptr;
+  const bool fused = !ROLES && splits > 1 && p.tickets != nullptr;  // (roles: one K range per tile, host rule)
   if (fused) {
     typedef uint32_t u32x4f_t __attribute__((ext_vector_type(4)));
     int* sflag = reinterpret_cast<int*>(smem);
@@ -578,7 +698,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   }
   ICAP_STAMP(0, (uint64_t)split | ((uint64_t)(fused ? splits - 1 : 0) << 8) | ((uint64_t)tile << 32));
   ICAP_STAMP(4, ICAP_NOW());
-  const bool whole = splits == 1 || fused;  // this block applies the full epilogue
+  const bool whole = ROLES || splits == 1 || fused;  // this block applies the full epilogue
 
   uint64_t seed = 0;
   if (whole && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
@@ -587,13 +707,20 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
 
   // ---- LDS-staged epilogue: each wave re-reads its accumulators EW = 8 consecutive columns per lane, so every
   // global access of the epilogue is 16 bytes (bf16) — the store tail is issue-bound (cdna_hip_programming.md T21)
-  float* cs = reinterpret_cast<float*>(smem) + wave * (EPR * ELD);
+  // ROLES: both waves of a SIMD store the tile of its MFMA wave (ew), which stages its accumulators; the rows of
+  // even / odd t go to the MFMA / loader wave (half), so the epilogue's VALU and stores run on twice the waves
+  const int ew = ROLES ? (wave & (NW - 1)) : wave;
+  const int ewm = ew / WN, ewn = ew - ewm * WN;
+  const int half = ROLES ? wave / NW : 0;
+  constexpr int NHALF = ROLES ? 2 : 1;
+  const bool stager = !ROLES || wave < NW;
+  float* cs = reinterpret_cast<float*>(smem) + ew * (EPR * ELD);
   constexpr int EW = 8;
   constexpr int LPR = 16 * TN / EW;  // lanes per staged row (EW columns each)
   constexpr int RPI = 64 / LPR;     // rows per wave instruction
   const int er = lane / LPR;
   const int ec = (lane - er * LPR) * EW;
-  const int64_t col = n0 + wn * 16 * TN + ec;
+  const int64_t col = n0 + ewn * 16 * TN + ec;
   const bool fullw = col + EW <= N;
   float biasw[EW];
 #pragma unroll
@@ -616,12 +743,13 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   bool want_pre = false;  // block-uniform: this launch has a bf16 dact_src / resid operand
   const bf16_t* esrc = nullptr;
   int64_t eld = 0;
-  const int64_t rb = m0 + wm * 16 * TM + er;  // row of (pass h, row t) = rb + h EPR + t RPI
+  const int64_t rb = m0 + ewm * 16 * TM + er;  // row of (pass h, row t) = rb + h EPR + t RPI
   auto prefetch = [&](auto gc) __attribute__((always_inline)) {  // rows of passes [g HPG, g HPG + HPG)
     constexpr int g = decltype(gc)::value;
     if (want_pre && fullw) {
 #pragma unroll
       for (int i = 0; i < NEP; ++i) {
+        if (NHALF > 1 && (i % (EPR / RPI)) % NHALF != half) continue;  // (roles: the other wave's rows)
         const int64_t r0 = rb + (int64_t)(g * NEP + i) * RPI;
         const int64_t row = r0 < Mv ? r0 : Mv - 1;
         pre[i] = *reinterpret_cast<const pre_t*>(esrc + row * eld + col);
@@ -663,14 +791,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
   };
   auto store_row = [&](int h, int t, const pre_t* pq) __attribute__((always_inline)) {
     const int lr = t * RPI + er;  // 0..EPR-1
-    const int64_t row = m0 + wm * 16 * TM + h * EPR + lr;
+    const int64_t row = m0 + ewm * 16 * TM + h * EPR + lr;
     float x[EW];
 #pragma unroll
     for (int q = 0; q < EW / 4; ++q)
       *reinterpret_cast<float4*>(x + 4 * q) = *reinterpret_cast<const float4*>(cs + lr * ELD + ec + 4 * q);
     const bool ok = row < Mv && col < N;
     if constexpr (LNX == 2) {  // rstd (A.B^T - mean wsum); the host passed bias = b + W . beta
-      const int br = wm * 16 * TM + h * EPR + lr;
+      const int br = ewm * 16 * TM + h * EPR + lr;
       const float mean = lnr[2 * br], rs = lnr[2 * br + 1];
 #pragma unroll
       for (int e = 0; e < EW; ++e) x[e] = rs * (x[e] - mean * wsumw[e]);
@@ -716,25 +844,47 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(icap_gemm_args
     static_for<0, NH>([&](auto hc) {
       constexpr int h = decltype(hc)::value;
       if constexpr (h > 0 && h % HPG == 0) prefetch(std::integral_constant<int, h / HPG>{});
-      stage_rows(hc);
+      if (stager) stage_rows(hc);
       __syncthreads();
       static_for<0, EPR / RPI>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        store_row(h, t, (want_pre && fullw) ? &pre[(h % HPG) * (EPR / RPI) + t] : nullptr);
+        if (NHALF == 1 || t % NHALF == half)
+          store_row(h, t, (want_pre && fullw) ? &pre[(h % HPG) * (EPR / RPI) + t] : nullptr);
       });
       __syncthreads();
     });
   } else {
     static_for<0, NH>([&](auto hc) {  // h compile-time: acc[] is indexed by it
       constexpr int h = decltype(hc)::value;
-      stage_rows(hc);
+      if (stager) stage_rows(hc);
       __syncthreads();
 #pragma unroll 2
-      for (int t = 0; t < EPR / RPI; ++t) store_row(h, t, nullptr);
+      for (int t = half; t < EPR / RPI; t += NHALF) store_row(h, t, nullptr);
       __syncthreads();
     });
   }
   ICAP_STAMP(5, ICAP_NOW());
+}
+
+template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, int ACT = ACT_ANY,
+          bool ROLES = false>
+__global__ __launch_bounds__(64 * WM * WN * (ROLES ? 2 : 1), MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
+                                                                  int nk_split, uint32_t drop_thresh, float inv_keep) {
+  const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < p.M ? (int64_t)*p.m_dev : p.M;  // device row count
+  if constexpr (ROLES) {
+    // a grid of at most one block per CU walks the live tiles (host: grid = min(tiles, CUs)): with the capacity grid
+    // of the packed step (65 row tiles for 28 live ones) the dead blocks — 147 KiB of LDS each, so never co-resident
+    // with a live one — were dispatched only as the live ones finished and delayed the launch's end
+    constexpr int BM = 16 * WM * TM;
+    const int tiles_m = (int)((p.M + BM - 1) / BM);
+    const int nlive = (int)((Mv + BM - 1) / BM) * tiles_n;
+    for (int b = blockIdx.x; b < nlive; b += gridDim.x)
+      gemm_body<TI, TC, NST, MINB, WM, WN, TM, TN, KOUT, ACT, ROLES>(p, tiles_n, 1, nk_split, drop_thresh, inv_keep, b,
+                                                                       tiles_m, Mv);
+  } else {
+    gemm_body<TI, TC, NST, MINB, WM, WN, TM, TN, KOUT, ACT, ROLES>(p, tiles_n, splits, nk_split, drop_thresh, inv_keep,
+                                                                     blockIdx.x, (int)(gridDim.x / splits) / tiles_n, Mv);
+  }
 }
 
 }  // namespace icap

@@ -152,7 +152,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
          alg_flops: Optional[float] = None, split_k: int = 0, m_dev: Optional[Tensor] = None,
          trans_ab: bool = False, ln: Optional[tuple] = None, workspace: Optional[Tensor] = None,
          tile_only: bool = False, g256: bool = False, g8p: int = 0, r256: bool = False, w192: bool = False,
-         m_hint: Optional[int] = None,
+         roles: int = 0, m_hint: Optional[int] = None,
          ln_fold: Optional[tuple] = None, ln_stats_out: Optional[Tensor] = None,
          ln_stats_in: Optional[Tensor] = None, ln_rows_out: Optional[tuple] = None,
          diag_stamps: Optional[Tensor] = None) -> Tensor:
@@ -171,7 +171,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     tile_only: the 128-row tile kernels only; g256: the 256 x 256 kernel wherever eligible; g8p = 128 / 256: the
     256-row 8-phase kernel with that tile width wherever eligible; r256: the 256 x 128 ring tile kernel (variant
     22) wherever eligible, unsplit (A/B measurements, path-equality tests); w192: 192 x 64 tiles (variant 24)
-    wherever eligible, unsplit (same use).
+    wherever eligible, unsplit (same use); roles = 256 / 96: the split-role ring kernel on 128 x 256 (variant 26) /
+    96 x 128 (variant 27) tiles wherever eligible, unsplit (same use).
     ln_stats_out: fp32 [M, N/32, 2] — this (producer) launch also writes (mean, M2) of each row's 32-column groups of
     the stored C; ln_stats_in (with ln_fold = (wsum, eps)): the LayerNorm of A folded into the epilogue from the
     producer's statistics (tile kernels, any M); ln_rows_out: (mean, rstd) fp32 [M] of that LayerNorm (for its
@@ -224,8 +225,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
         a.tickets, a.tickets_len = tk.data_ptr(), tk.numel()
     a.m_dev = _p(m_dev)
     a.m_hint = int(m_hint) if (m_hint is not None and m_dev is not None) else 0
-    a.path = 1 if tile_only else (3 if g256 else (4 if g8p == 128 else 5 if g8p == 256 else
-                                                (6 if r256 else (7 if w192 else 0))))
+    a.path = (1 if tile_only else 3 if g256 else 4 if g8p == 128 else 5 if g8p == 256 else 6 if r256 else
+              7 if w192 else 8 if roles == 256 else 9 if roles == 96 else 0)
     if ln is not None:
         a.ln_gamma, a.ln_beta, a.ln_eps = ln[0].data_ptr(), ln[1].data_ptr(), float(ln[2])
     if ln_fold is not None:

@@ -188,10 +188,12 @@ def test_packed_step_with_dropout_runs(dev):
 
 @pytest.mark.parametrize("N,K,epi", [(768, 3072, "resid_drop"), (768, 2304, "plain"), (768, 1160, "f32"),
                                      (640, 3072, "plain")])
-def test_ring_gemm_equals_tile_kernel(dev, N, K, epi, monkeypatch):
-    """The 4-stage ring (icap_gemm variant for long K over ~one tile per CU, chosen through m_hint when split-K is
-    off: split_k = 1) runs the same MFMA chain as the double-buffered tile kernel: bitwise-equal outputs on the live
-    rows; close to fp32 torch."""
+def test_packed_gemm_kernel_equals_tile_kernel(dev, N, K, epi):
+    """The packed step's N <= 1024 products with the expected live-row count (m_hint) take the split-role ring on
+    96 x 128 tiles (round 6, icap_gemm variant 27: one round of tiles, no split of K); it runs the tile kernel's MFMA
+    chain in natural k order, so its live rows equal the 128-row tile path's (tile_only) bitwise and rows past the
+    device count stay untouched; close to fp32 torch. (Round 3's 4-stage ring, variant 16, took these launches
+    before; the unhinted plan sizes its choice for the capacity rows and keeps the split / 128-row kernels.)"""
     from icap import _lib as L
 
     mcap, mlive = 8320, 3584
@@ -204,19 +206,21 @@ def test_ring_gemm_equals_tile_kernel(dev, N, K, epi, monkeypatch):
         kw = dict(bias=torch.randn(N, generator=g).to(dev), resid=torch.randn((mcap, N), generator=g).to(dev, cdt),
                   drop=ops.Dropout(0.1, 7))
     mdev = torch.tensor([mlive], dtype=torch.int32, device=dev)
-    outs, names = [], []
-    for hint in (mlive, None):
+    outs = []
+    for form in ("hint", "tile"):
         C = torch.zeros((mcap, N), device=dev, dtype=cdt)
-        a = ops.gemm(A, B, C, m_dev=mdev, m_hint=hint, split_k=1, **kw)
-        outs.append(a)
-        ga = L.GemmArgs()
-        ga.M, ga.N, ga.K, ga.in_dtype, ga.c_dtype = mcap, N, K, L.BF16, ops.dtype_code(cdt)
-        ga.A, ga.lda, ga.B, ga.ldb, ga.C, ga.ldc = A.data_ptr(), K, B.data_ptr(), K, C.data_ptr(), N
-        ga.m_dev, ga.m_hint = mdev.data_ptr(), hint or 0
-        ga.alpha, ga.split_k = 1.0, 1
-        names.append(L.load().icap_gemm_kernel_name(ga).decode())
+        extra = dict(m_hint=mlive) if form == "hint" else dict(tile_only=True)
+        outs.append(ops.gemm(A, B, C, m_dev=mdev, split_k=1, **extra, **kw))
+    ga = L.GemmArgs()
+    ga.M, ga.N, ga.K, ga.in_dtype, ga.c_dtype = mcap, N, K, L.BF16, ops.dtype_code(cdt)
+    ga.A, ga.lda, ga.B, ga.ldb, ga.C, ga.ldc = A.data_ptr(), K, B.data_ptr(), K, outs[0].data_ptr(), N
+    ga.m_dev, ga.m_hint = mdev.data_ptr(), mlive
+    ga.alpha, ga.split_k = 1.0, 1
+    if epi == "resid_drop":
+        ga.resid, ga.ldr = kw["resid"].data_ptr(), N
+    name = L.load().icap_gemm_kernel_name(ga).decode()
     torch.cuda.synchronize()
-    assert "4, 1, 2, 2, 4, 4" in names[0] and "4, 1, 2, 2" not in names[1], names
+    assert "5, 1, 2, 2, 3, 4" in name and name.endswith(", true>"), name
     assert torch.equal(outs[0][:mlive], outs[1][:mlive])
     assert torch.count_nonzero(outs[0][mlive:]) == 0  # rows past the device count untouched
     if epi != "resid_drop":
