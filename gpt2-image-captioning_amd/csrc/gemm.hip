@@ -416,7 +416,7 @@ int gemm8p_launch(const icap_gemm_args& p, int bn, int actk, uint32_t thr, float
 // of them. (diagnostic build) ICAP_GEMM8P = 0 never, 128 / 256 forced where eligible, default the shape rule.
 static int g8p_actk(const icap_gemm_args& p) {
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || (p.ln_wsum && !p.ln_stats_in) || p.split_k > 1) return -1;
-  if (p.M < 256 || p.K < 64 || p.path == 1 || p.path == 3 || p.path >= 6) return -1;
+  if (p.M < 256 || p.K < 64 || p.path == 1 || p.path == 3 || p.path >= 6) return -1;  // (6 ... 10: other forced forms)
   if (p.M * p.lda >= (1ll << 30) || p.N * p.ldb >= (1ll << 30)) return -1;  // 32-bit DMA byte offsets per tile
   const int fa = p.dact == ICAP_ACT_NONE ? p.act : -1, ba = p.act == ICAP_ACT_NONE ? p.dact : -1;
   int a;
@@ -466,6 +466,8 @@ static int roles_actk(const icap_gemm_args& p, int v) {
   else if (fa == ICAP_ACT_GELU_NEW) a = ACT_FWD + ICAP_ACT_GELU_NEW;
   else if (ba == ICAP_ACT_GELU_NEW) a = ACT_BWD + ICAP_ACT_GELU_NEW;
   else if (fa == ICAP_ACT_QUICK_GELU) a = ACT_FWD + ICAP_ACT_QUICK_GELU;
+  else if (v == 28 && fa == ICAP_ACT_RELU) a = ACT_FWD + ICAP_ACT_RELU;
+  else if (v == 28 && ba == ICAP_ACT_RELU) a = ACT_BWD + ICAP_ACT_RELU;
   else a = ACT_ANY;
   if (p.c_dtype != ICAP_BF16) return (p.ln_stats_out || p.ln_stats_in) ? -1 : (a == ACT_OFF ? ACT_OFF : ACT_ANY);
   if (p.ln_stats_out) return a == ACT_OFF ? ACT_LNS : -1;
@@ -572,7 +574,7 @@ static int roles_pick(const icap_gemm_args& p, int64_t m_plan, int64_t nk, int64
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
-  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 9), "icap_gemm: path must be 0, 1 or 3 ... 9");
+  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 10), "icap_gemm: path must be 0, 1 or 3 ... 10");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16 || p.in_dtype == ICAP_FP8_MX,
                "icap_gemm: bad in_dtype");
@@ -813,8 +815,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // variants 26 / 27: the split-role ring (gemm_tile.h ROLES) on 128 x 256 / 96 x 128 tiles, one K range per tile
   // (path 8 / 9 force them where eligible; the automatic rule: roles_pick)
   {
-    const int rv = p.path == 8 ? 26 : p.path == 9 ? 27 : (p.path == 0 && roles_mode() != 0) ? roles_pick(p, m_plan, nk, cus) : 0;
-    const int bm = rv == 26 ? 128 : 96, bn = rv == 26 ? 256 : 128;
+    const int rv = p.path == 8 ? 26 : p.path == 9 ? 27 : p.path == 10 ? 28
+                   : (p.path == 0 && roles_mode() != 0) ? roles_pick(p, m_plan, nk, cus) : 0;
+    const int bm = rv == 26 ? 128 : rv == 27 ? 96 : 192, bn = rv == 27 ? 128 : 256;
     if (rv && p.M >= bm && p.split_k <= 1) {
       if (const int ar = roles_actk(p, rv); ar >= 0) {
         pl.variant = rv;
@@ -825,7 +828,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
         tiles = ((p.M + bm - 1) / bm) * tiles_n;
         pl.tiles_n = (int)tiles_n;
         pl.actk = ar;
-        pl.block = dim3(2 * GNT);
+        pl.block = dim3(rv == 28 ? 3 * GNT : 2 * GNT);
         pl.grid = dim3((unsigned)(tiles < cus ? tiles : cus));  // the kernel walks the live tiles
         return ICAP_OK;
       }
@@ -934,6 +937,7 @@ static const char* variant_kernel(int v) {
     case 25: return "gemm_kernel<%s, %s, 4, 1, 4, 1, 3, 4, false, %d>";
     case 26: return "gemm_kernel<%s, %s, 3, 1, 2, 2, 4, 8, false, %d, true>";
     case 27: return "gemm_kernel<%s, %s, 5, 1, 2, 2, 3, 4, false, %d, true>";
+    case 28: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 6, 4, false, %d, true>";
     default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %d>";
   }
 }
@@ -1030,11 +1034,12 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const int sp = pl.splits;
   // (the split-role variants walk K in its natural order: one round of tiles, no lockstep panel misses to stagger,
   // and automatic launches then equal forced ones and the tile path bitwise)
-  const int skew = (pl.variant == 26 || pl.variant == 27) ? 0 : kskew_for(p, pl.nk_split);
+  const int skew = (pl.variant >= 26 && pl.variant <= 28) ? 0 : kskew_for(p, pl.nk_split);
   const int nks = pl.nk_split | (skew << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
   if (pl.variant == 26) launch_tile_roles(pl, p, nks, s);                            // gemm_tile_roles.hip
   else if (pl.variant == 27) launch_tile_roles96(pl, p, nks, s);                     // gemm_tile_roles96.hip
+  else if (pl.variant == 28) launch_tile_roles192(pl, p, nks, s);                    // gemm_tile_roles192.hip
   else if (pl.variant == 22) launch_tile_r256(pl, p, nks, s);                        // gemm_tile_r256.hip
   else if (pl.variant == 24 || pl.variant == 25) launch_tile_w192(pl, p, nks, s);   // gemm_tile_w192.hip
   else if (pl.actk >= ACT_LNS) launch_tile_ln(pl, p, nks, s);                      // gemm_tile_ln.hip

@@ -109,9 +109,9 @@ struct lds_frags {
 // activation code is then not compiled into the kernel at all. Measured (profiles/r03_k768_counters.txt): with it
 // present, the plain 8320 x 2304 x 768 product ran 53.7 vs 45.0 us — the same memory instructions, +7 % VALU and
 // +22 % SQ_WAIT_ANY (the larger function scheduled its main loop worse), SQ_WAIT_INST_ANY +1 % (not instruction fetch).
-// ROLES (round 6; variants 26 / 27): the block has twice the waves; waves 0 .. NW-1 read fragments and issue MFMAs
-// only (one per SIMD), waves NW .. 2 NW-1 issue the LDS-DMA of the NST-stage ring and wait for it (one per SIMD), so
-// the DMA's issue cost runs beside the MFMA stream instead of in front of it (the main loop below).
+// ROLES (round 6; variants 26 / 27 / 28): the block has 4 more waves; waves 0 .. NW-1 read fragments and issue MFMAs
+// only (NW = 4: one per SIMD; NW = 8: two per SIMD), waves NW .. NW+3 issue the LDS-DMA of the NST-stage ring and wait
+// for it (one per SIMD), so the DMA's issue cost runs beside the MFMA stream instead of in front of it.
 template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, int ACT = ACT_ANY,
           bool ROLES = false>
 // The body of one tile (gemm_kernel below runs it once per block, or, for ROLES, once per live tile of a grid-stride
@@ -120,8 +120,9 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
                                           float inv_keep, const int bid, const int tiles_m, const int64_t Mv) {
   static_assert(!KOUT || (sizeof(TI) == 2 && 16 * WM * TM == 128 && 16 * WN * TN == 128),
                 "K-outer operands: bf16, 128 x 128 tiles");
-  static_assert(!ROLES || (!KOUT && sizeof(TI) == 2 && WM == 2 && WN == 2 && NST >= 3 && MINB == 1),
-                "roles: bf16 row-major operands, 2 x 2 MFMA waves, a ring of >= 3 stages, one block per CU");
+  static_assert(!ROLES || (!KOUT && sizeof(TI) == 2 && ((WM == 2 && WN == 2 && NST >= 3) || (WM * WN == 8 && NST >= 2))
+                           && MINB == 1),
+                "roles: bf16 row-major operands, 4 MFMA waves on a ring of >= 3 stages or 8 on >= 2, one block per CU");
   // MX block-scaled fp8 (TI = fp8_t): a stage's 128-byte LDS row is one 128-deep K step of
   // v_mfma_scale_f32_16x16x128_f8f6f4 (twice the bf16 flops per staged byte and per fragment byte read); the
   // per-32 E8M0 scales of the wave's 4 fragment rows of A and of B come in one 16-byte load each per stage
@@ -242,7 +243,8 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
   float* lnr = reinterpret_cast<float*>(smem + NST * STB);
   auto ln_prologue = [&]() __attribute__((always_inline)) {
     if constexpr (LNX == 2) {
-      static_assert(NW * 64 == 2 * BM, "two threads per LN table row");
+      static_assert(NW * 64 >= 2 * BM, "two threads per LN table row");
+      if (tid >= 2 * BM) return;  // (8 MFMA waves over 192 rows: the first 384 threads)
       // each thread of the pair holds one half of the row's G pairs: G / 4 16-byte loads issued together (the host
       // guarantees G % 4 == 0 and G <= 4 LNQ), both passes from registers
       constexpr int LNQ = 10;  // 16-byte loads per thread at most: K <= 1280
@@ -382,16 +384,17 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
     // for LDS-DMA it did not issue except through a barrier.
     // Stages past K are issued with out-of-range offsets (nothing is fetched, zeros land in a free slot), so every
     // loop iteration has the same DMA count and the same vmcnt.
-    constexpr int P = (BM + BN) / (8 * NW);  // 1-KiB DMA pieces per loader wave per stage
-    constexpr int PA = BM / (8 * NW);        // of them A rows (pieces i < PA)
-    static_assert((BM + BN) % (8 * NW) == 0 && BM % (8 * NW) == 0 && (NST - 2) * P < 64, "roles: stage split");
+    constexpr int NLW = 4;                    // loader waves
+    constexpr int P = (BM + BN) / (8 * NLW);  // 1-KiB DMA pieces per loader wave per stage
+    constexpr int PA = BM / (8 * NLW);        // of them A rows (pieces i < PA)
+    static_assert((BM + BN) % (8 * NLW) == 0 && BM % (8 * NLW) == 0 && (NST - 2) * P < 64, "roles: stage split");
     const uint32_t sbase = (uint32_t)reinterpret_cast<uintptr_t>(smem);
     if (wave >= NW) {
       const int lw = wave - NW;
       uint32_t voff[P];
 #pragma unroll
       for (int i = 0; i < P; ++i) {
-        const int q = i * NW + lw;  // 8-row piece of the [A tile; B tile] stack
+        const int q = i * NLW + lw;  // 8-row piece of the [A tile; B tile] stack
         const int row = (i < PA ? q : q - BM / 8) * 8 + lrow;
         voff[i] = (uint32_t)((int64_t)row * (i < PA ? p.lda : p.ldb) + lchunk) * ES;
       }
@@ -402,7 +405,7 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
         const bool kin = live && k0 + lchunk < K;
 #pragma unroll
         for (int i = 0; i < P; ++i) {
-          const uint32_t lds = __builtin_amdgcn_readfirstlane(sbase + (uint32_t)(slot * STB + (i * NW + lw) * 1024));
+          const uint32_t lds = __builtin_amdgcn_readfirstlane(sbase + (uint32_t)(slot * STB + (i * NLW + lw) * 1024));
           dma16a(i < PA ? ra_rsrc : rb_rsrc, lds, kin ? voff[i] + kb : OOB);
         }
       };
@@ -450,6 +453,23 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
     ln_prologue();  // (its loads are the MFMA waves' only vector-memory operations)
     __builtin_amdgcn_s_barrier();  // B_0
     __builtin_amdgcn_sched_barrier(0);
+    ICAP_STAMP(2, ICAP_NOW());
+    if constexpr (NW == 8) {
+      // two MFMA waves per SIMD (variant 28, 96 x 64 per wave): one fragment set each (the 168-register budget of
+      // three waves per SIMD), read right before its MFMAs — the partner wave's MFMAs cover the read latency
+      for (int kt = 0; kt < nk; ++kt) {
+        const uint32_t sb = sbase + (uint32_t)((kt % NST) * STB);
+        rd(fa0, fb0, sb + la[0], sb + lb[0]);
+        retire(fa0, fb0);
+        mm(fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        rd(fa0, fb0, sb + la[1], sb + lb[1]);
+        retire(fa0, fb0);
+        mm(fa0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();  // B_{kt+1}: every read of stage kt retired (retire above)
+      }
+    } else {
     rd(fa0, fb0, sbase + la[0], sbase + lb[0]);
     for (int kt = 0; kt < nk; ++kt) {
       const uint32_t sb = sbase + (uint32_t)((kt % NST) * STB);
@@ -465,6 +485,7 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
       }
       mm(fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
+    }
     }
     }
     __syncthreads();  // every MFMA wave is done reading the ring and the loaders' DMA has drained
@@ -709,11 +730,13 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
   // global access of the epilogue is 16 bytes (bf16) — the store tail is issue-bound (cdna_hip_programming.md T21)
   // ROLES: both waves of a SIMD store the tile of its MFMA wave (ew), which stages its accumulators; the rows of
   // even / odd t go to the MFMA / loader wave (half), so the epilogue's VALU and stores run on twice the waves
-  const int ew = ROLES ? (wave & (NW - 1)) : wave;
+  // (8 MFMA waves: each stores its own tile, the loader waves only pass the barriers)
+  constexpr int NHALF = (ROLES && NW == 4) ? 2 : 1;
+  const int ew = NHALF == 2 ? (wave & (NW - 1)) : wave;
   const int ewm = ew / WN, ewn = ew - ewm * WN;
-  const int half = ROLES ? wave / NW : 0;
-  constexpr int NHALF = ROLES ? 2 : 1;
+  const int half = NHALF == 2 ? wave / NW : 0;
   const bool stager = !ROLES || wave < NW;
+  const bool storer = !ROLES || NHALF == 2 || wave < NW;
   float* cs = reinterpret_cast<float*>(smem) + ew * (EPR * ELD);
   constexpr int EW = 8;
   constexpr int LPR = 16 * TN / EW;  // lanes per staged row (EW columns each)
@@ -746,7 +769,7 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
   const int64_t rb = m0 + ewm * 16 * TM + er;  // row of (pass h, row t) = rb + h EPR + t RPI
   auto prefetch = [&](auto gc) __attribute__((always_inline)) {  // rows of passes [g HPG, g HPG + HPG)
     constexpr int g = decltype(gc)::value;
-    if (want_pre && fullw) {
+    if (want_pre && fullw && storer) {
 #pragma unroll
       for (int i = 0; i < NEP; ++i) {
         if (NHALF > 1 && (i % (EPR / RPI)) % NHALF != half) continue;  // (roles: the other wave's rows)
@@ -848,7 +871,7 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
       __syncthreads();
       static_for<0, EPR / RPI>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
-        if (NHALF == 1 || t % NHALF == half)
+        if ((NHALF == 1 || t % NHALF == half) && storer)
           store_row(h, t, (want_pre && fullw) ? &pre[(h % HPG) * (EPR / RPI) + t] : nullptr);
       });
       __syncthreads();
@@ -858,8 +881,10 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
       constexpr int h = decltype(hc)::value;
       if (stager) stage_rows(hc);
       __syncthreads();
+      if (storer) {
 #pragma unroll 2
-      for (int t = half; t < EPR / RPI; t += NHALF) store_row(h, t, nullptr);
+        for (int t = half; t < EPR / RPI; t += NHALF) store_row(h, t, nullptr);
+      }
       __syncthreads();
     });
   }
@@ -868,7 +893,7 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
 
 template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, int ACT = ACT_ANY,
           bool ROLES = false>
-__global__ __launch_bounds__(64 * WM * WN * (ROLES ? 2 : 1), MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
+__global__ __launch_bounds__(64 * (WM * WN + (ROLES ? 4 : 0)), MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
                                                                   int nk_split, uint32_t drop_thresh, float inv_keep) {
   const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < p.M ? (int64_t)*p.m_dev : p.M;  // device row count
   if constexpr (ROLES) {

@@ -117,9 +117,10 @@ typedef struct {
   /*     csrc/gemm8p.hip) — same use; 6 = the 256 x 128 tile kernel on the 3-stage ring (csrc/gemm_tile.h       */
   /*     variant 22) for unsplit bf16 row-major launches, M >= 256 — same use; 7 = 192 x 64 tiles (variant 24:  */
   /*     4 waves stacked in M) for bf16 row-major launches without a LayerNorm fold / consumer, M >= 192,       */
-  /*     unsplit — same use; 8 / 9 = the split-role ring kernel (4 MFMA waves + 4 LDS-DMA waves, one block    */
-  /*     per CU: csrc/gemm_tile.h ROLES) on 128 x 256 (variant 26) / 96 x 128 (variant 27) tiles for unsplit     */
-  /*     bf16 row-major launches without ln_gamma (9: no LayerNorm consumer) — same use.                      */
+  /*     unsplit — same use; 8 / 9 / 10 = the split-role ring kernel (4 or 8 MFMA waves + 4 LDS-DMA waves,    */
+  /*     one block per CU: csrc/gemm_tile.h ROLES) on 128 x 256 (variant 26) / 96 x 128 (variant 27) /          */
+  /*     192 x 256 (variant 28) tiles for unsplit bf16 row-major launches without ln_gamma (9: no LayerNorm     */
+  /*     consumer) — same use.                                                                                 */
   int32_t path;
   /* in_dtype == ICAP_FP8_MX: the E8M0 block scales of A (M rows) and B (N rows), K % 128 == 0, lda / ldb      */
   /* multiples of 16, 16-byte aligned. For a 128-element K stage s and 64-row group g, 256 bytes at offset      */

@@ -20,7 +20,7 @@ from gemm_helpers import _assert_same, _run, rnd
 
 pytestmark = pytest.mark.gpu
 
-R256, R96 = "3, 1, 2, 2, 4, 8", "5, 1, 2, 2, 3, 4"
+R256, R96, R192 = "3, 1, 2, 2, 4, 8", "5, 1, 2, 2, 3, 4", "2, 1, 2, 4, 6, 4"
 
 SHAPES = [  # (M, N, K, roles)
     (3584, 2304, 768, 256),  # GPT-2 c_attn at the packed rows
@@ -33,11 +33,16 @@ SHAPES = [  # (M, N, K, roles)
     (384, 256, 64, 256),     # one k-step (fewer than the ring's stages)
     (200, 130, 128, 96),     # two k-steps, partial tiles
     (6400, 2304, 768, 256),  # CLIP-B/32 qkv
+    (3584, 3072, 768, 192),  # c_fc / mlp c_proj dX on 192 x 256 tiles (8 MFMA waves)
+    (1000, 520, 200, 192),
+    (384, 256, 64, 192),
+    (3200, 3072, 768, 192),  # the mapper's linear1
 ]
 
 
 def _name(tc, act, roles):
-    return f"icap::gemm_kernel<unsigned short, {tc}, {R256 if roles == 256 else R96}, false, {act}, true>"
+    form = {256: R256, 96: R96, 192: R192}[roles]
+    return f"icap::gemm_kernel<unsigned short, {tc}, {form}, false, {act}, true>"
 
 
 @pytest.mark.parametrize("M,N,K,roles", SHAPES)
@@ -74,7 +79,7 @@ def test_roles_repeatable(dev):
 
 
 @pytest.mark.parametrize("M,N,K,roles", [(3584, 2304, 768, 256), (1000, 520, 200, 256), (3584, 768, 768, 96),
-                                         (1000, 520, 200, 96)])
+                                         (1000, 520, 200, 96), (3584, 3072, 768, 192), (1000, 520, 200, 192)])
 def test_roles_epilogues_match_tile(dev, M, N, K, roles):
     A = rnd((M, K), dev, scale=0.1, seed=6)
     B = rnd((N, K), dev, scale=0.1, seed=7)
@@ -99,7 +104,7 @@ def test_roles_epilogues_match_tile(dev, M, N, K, roles):
         _assert_same(name, a, b)
 
 
-@pytest.mark.parametrize("roles,N", [(256, 2304), (96, 768)])
+@pytest.mark.parametrize("roles,N", [(256, 2304), (96, 768), (192, 3072)])
 def test_roles_device_row_count(dev, roles, N):
     """m_dev: rows past the device count are neither computed nor stored; the rest equal the tile path's."""
     M, live, K = 8320, 3584, 768
@@ -116,7 +121,7 @@ def test_roles_device_row_count(dev, roles, N):
     assert bool((C[live:] == 3.0).all())
 
 
-@pytest.mark.parametrize("roles", [256, 96])
+@pytest.mark.parametrize("roles", [256, 96, 192])
 def test_roles_layernorm_stats_producer_matches_tile(dev, roles):
     """C and its (mean, M2) per row and 32-column group equal the tile kernel's (the GPT-2 attn c_proj form: bias +
     residual + dropout + statistics, device row count)."""
@@ -141,8 +146,9 @@ def test_roles_layernorm_stats_producer_matches_tile(dev, roles):
     _assert_same("stats", out[False][1][:live].reshape(live, -1), out[True][1][:live].reshape(live, -1))
 
 
-@pytest.mark.parametrize("N,act", [(2304, L.ACT_NONE), (3072, L.ACT_GELU_NEW)])
-def test_roles_layernorm_consumer_matches_tile(dev, N, act):
+@pytest.mark.parametrize("N,act,roles", [(2304, L.ACT_NONE, 256), (3072, L.ACT_GELU_NEW, 256),
+                                         (3072, L.ACT_GELU_NEW, 192), (3072, L.ACT_QUICK_GELU, 192)])
+def test_roles_layernorm_consumer_matches_tile(dev, N, act, roles):
     """The LayerNorm folded into the consumer's epilogue from handed-over statistics (GPT-2's c_attn / c_fc forward,
     device row count): C and the row mean / rstd outputs equal the tile kernel's."""
     from icap.gpt2 import fold_layernorm
@@ -161,9 +167,9 @@ def test_roles_layernorm_consumer_matches_tile(dev, N, act):
     st = torch.stack((grp.mean(-1), ((grp - grp.mean(-1, keepdim=True)) ** 2).sum(-1)), -1).contiguous()
     out = {}
     for tile in (False, True):
-        kw = dict(tile_only=True) if tile else dict(roles=256)
+        kw = dict(tile_only=True) if tile else dict(roles=roles)
         C = torch.zeros((M, N), device=dev, dtype=torch.bfloat16)
-        aux = torch.zeros_like(C) if act != L.ACT_NONE else None
+        aux = torch.zeros_like(C) if act == L.ACT_GELU_NEW else None
         mo, ro = torch.zeros(M, device=dev), torch.zeros(M, device=dev)
         names = _run(lambda: ops.gemm(x, wf, C, bias=bf, act=act, aux=aux, ln_fold=(wsum, 1e-5), ln_stats_in=st,
                                       ln_rows_out=(mo, ro), m_dev=md, m_hint=live, split_k=1, **kw))
@@ -174,7 +180,7 @@ def test_roles_layernorm_consumer_matches_tile(dev, N, act):
         _assert_same(name, a[:live], b[:live])
 
 
-@pytest.mark.parametrize("roles", [256, 96])
+@pytest.mark.parametrize("roles", [256, 96, 192])
 def test_roles_f32_output_matches_tile(dev, roles):
     M, N, K = 2048, 1024, 320
     A = rnd((M, K), dev, seed=11)
