@@ -85,7 +85,10 @@ class CaptionTrainer:
         B, Lc = batch_size, caption_len
         P = model.total_prefix_length
         self.P = P
-        self.mws = self.mcore.alloc(B, train=True)
+        # (per-layer backward gradient buffers only for the schedules whose weight-gradient products trail the dX
+        # chain on other streams: 433 MB at B = 128 that the default serial schedule does not need)
+        per_layer = dict(per_layer_grads=mapper_dw != "serial") if isinstance(self.mcore, TransformerMapperCore) else {}
+        self.mws = self.mcore.alloc(B, train=True, **per_layer)
         # packed token rows (GPT2Core.alloc_train): the blocks skip each caption's dead tail (positions after its
         # last loss target, which the causal mask keeps out of every loss term)
         self.gws = self.gcore.alloc_train(B, P, Lc, keep_for_dw=self.gpt_trainable, compact_head=compact_head,

@@ -316,7 +316,9 @@ class TransformerMapperCore:
         return g
 
     # -- workspaces ------------------------------------------------------------------------------------------
-    def alloc(self, B: int, train: bool) -> SimpleNamespace:
+    def alloc(self, B: int, train: bool, per_layer_grads: bool = False) -> SimpleNamespace:
+        """per_layer_grads: one set of backward gradient buffers per layer (the side / grouped weight-gradient
+        schedules, whose dW products trail the dX chain); the serial schedule shares two alternating sets."""
         S, D, dt, dev, nl = self.S, self.D, self.dtype, self.dev, self.nl
         M = B * S
         e = lambda *shape, dtype=dt: torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
@@ -337,15 +339,25 @@ class TransformerMapperCore:
         if train:
             ws.dout = torch.zeros((M, D), dtype=dt, device=dev)  # rows t < Hl stay zero
             ws.dres = e(M, D)  # d(mapper input rows): the head step reads it
-            # per-layer gradient buffers of the backward (mapper.backward_steps): every buffer a layer's
-            # weight-gradient products read is written once per step, so those products can trail the dX chain on
-            # a side stream with no write-after-read hazard (8 layers x 11 M x D x 2 B: 433 MB at B = 128)
-            ws.g_r = [e(M, D) for _ in range(nl)]      # residual grad entering layer l (LN#2 output of layer l+1)
-            ws.g_rm = [e(M, D) for _ in range(nl)]     # residual grad after layer l's MLP (its LN#1 output)
-            ws.g_m = [e(M, D) for _ in range(nl)]      # g_r[l] through the layer's output dropout (dy of linear2)
-            ws.g_mm = [e(M, D) for _ in range(nl)]     # g_rm[l] through the attention-output dropout (dy of out_proj)
-            ws.g_dz = [e(M, 4 * D) for _ in range(nl)]    # d(relu pre-activation) (dy of linear1)
-            ws.g_dqkv = [e(M, 3 * D) for _ in range(nl)]  # d(in_proj output) (dy of in_proj)
+            # gradient buffers of the backward (mapper.backward_steps). per_layer_grads: one set per layer — every
+            # buffer a layer's weight-gradient products read is written once per step, so those products can trail
+            # the dX chain on side streams with no write-after-read hazard (8 layers x 11 M x D x 2 B: 433 MB at
+            # B = 128). The serial schedule runs each layer's dW products before the next layer's backward writes
+            # anything, so it shares one set; g_r / g_m alternate by layer parity (layer l reads g_r[l], g_m[l] and
+            # writes g_r[l-1], g_m[l-1]): 2 x 2 + 9 = 13 M x D buffers instead of 88 (round-6 VERDICT item 7)
+            n_set = nl if per_layer_grads else 1
+            n_alt = nl if per_layer_grads else min(2, nl)
+
+            def bufs(n, cols):
+                b = [e(M, cols) for _ in range(n)]
+                return [b[l % n] for l in range(nl)]
+
+            ws.g_r = bufs(n_alt, D)        # residual grad entering layer l (LN#2 output of layer l+1)
+            ws.g_rm = bufs(n_set, D)       # residual grad after layer l's MLP (its LN#1 output)
+            ws.g_m = bufs(n_alt, D)        # g_r[l] through the layer's output dropout (dy of linear2)
+            ws.g_mm = bufs(n_set, D)       # g_rm[l] through the attention-output dropout (dy of out_proj)
+            ws.g_dz = bufs(n_set, 4 * D)   # d(relu pre-activation) (dy of linear1)
+            ws.g_dqkv = bufs(n_set, 3 * D)  # d(in_proj output) (dy of in_proj)
             ws.dz = e(M, 4 * D)
             ws.dqkv = e(M, 3 * D)
             ws.do, ws.da = e(M, D), e(M, D)

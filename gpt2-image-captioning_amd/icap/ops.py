@@ -705,7 +705,9 @@ def patch_embed(pixels: Tensor, w: Tensor, out: Tensor, *, patch: int, prefix: O
         raise L.IcapError("patch_embed: pixels must be contiguous fp32 [B,C,H,H]")
     if w.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
         raise L.IcapError("patch_embed: w and out must be bf16")
-    B, Cc, H, _ = pixels.shape
+    B, Cc, H, W = pixels.shape
+    if H != W:  # the kernel indexes the pixels as H x H
+        raise L.IcapError("patch_embed: pixels must be square [B,C,H,H]")
     NP = 0 if prefix is None else prefix.shape[0]
     N = w.shape[0]
     S = NP + (H // patch) ** 2
@@ -714,8 +716,13 @@ def patch_embed(pixels: Tensor, w: Tensor, out: Tensor, *, patch: int, prefix: O
     for t in (prefix, pos, bias):
         if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
             raise L.IcapError("patch_embed: prefix / pos / bias must be contiguous fp32")
-    if pos is not None and pos.numel() < S * N:
-        raise L.IcapError("patch_embed: pos must hold S x N values")
+    # every per-column operand is indexed with stride N = w.shape[0] (the output columns)
+    if pos is not None and (pos.shape[-1] != N or pos.numel() < S * N):
+        raise L.IcapError("patch_embed: pos must be [S, N] with N = w.shape[0]")
+    if prefix is not None and prefix.shape[-1] != N:
+        raise L.IcapError("patch_embed: prefix must be [NP, N] with N = w.shape[0]")
+    if bias is not None and bias.numel() < N:
+        raise L.IcapError("patch_embed: bias must hold N = w.shape[0] values")
     call("icap_patch_embed", B, Cc, H, patch, NP, N, pixels.data_ptr(), w.data_ptr(), _ld(w), w.shape[1], _p(bias),
          _p(pos), _p(prefix), out.data_ptr(), _ld(out), _stream())
     return out

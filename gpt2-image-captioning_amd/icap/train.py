@@ -80,9 +80,11 @@ def train(train_dataset, model, batch_size: int, num_epochs: int, num_workers: i
             ids, mask, labels = batch["token_ids"], batch["attention_mask"], batch["labels"]
             t = trainer_for(ids.shape[0], ids.shape[1])
             pixels = batch.get("pixel_values") if clip_model is not None else None
-            t.load_batch(ids.to(device, non_blocking=True), mask.to(device, non_blocking=True),
-                         labels.to(device, non_blocking=True), emb=batch["image_embedding"].to(device, non_blocking=True),
-                         pixels=pixels.to(device, non_blocking=True) if pixels is not None else None)
+            # the batch as the loader delivers it (pinned host tensors): load_batch copies it into the trainer's
+            # device buffers asynchronously and reads the packed attention's short-sequence flag from the host
+            # labels on the way (moving the labels to the device first turned that flag off for every batch:
+            # ADVICE r05, engine.load_batch)
+            t.load_batch(ids, mask, labels, emb=batch["image_embedding"], pixels=pixels)
             # train.py:128-159: a cycle starts after each optimizer step; the step is taken every grad_accum_steps
             # batches and at the last batch of the epoch. The cycle's micro-batches accumulate into one shared
             # gradient buffer even when a short last batch runs on another trainer (its own batch shape).

@@ -156,6 +156,60 @@ def test_train_grad_accum_short_last_batch_steps_like_reference(tmp_path):
     assert [f[2] for f in epoch] == [False, False, False, True, False, True]
 
 
+def test_train_takes_short_only_attention_for_short_captions(tmp_path):
+    """train() hands the loader's host batch to the trainer, which reads the packed attention's short-sequence flag
+    from the host labels: with COCO-length captions (every packed sequence <= 32 tokens) every attention launch of
+    the GPT-2 blocks is the short-only form, as in bench.py (the labels were moved to the device first,
+    which kept the flag off for every batch)."""
+    import icap
+    from icap.dataset import SyntheticCaptionDataset
+
+    ds = SyntheticCaptionDataset(6, max_length=12, real=5, vocab_size=512, eos=511, embed_dim=64)
+    seen = []
+    orig = icap.CaptionTrainer.load_batch
+
+    def load_batch(self, ids, mask, labels, emb=None, pixels=None):
+        seen.append(labels.device.type)
+        orig(self, ids, mask, labels, emb=emb, pixels=pixels)
+        seen.append(bool(self.gws.short_only))
+
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model()
+        icap.CaptionTrainer.load_batch = load_batch
+        try:
+            icap.train(ds, model, batch_size=3, num_epochs=1, num_workers=0, device=CPU, outputs_dir=str(tmp_path),
+                       save_every_epoch=10, use_graph=False)
+        finally:
+            icap.CaptionTrainer.load_batch = orig
+        _assert_clean(rec)
+    assert seen == ["cpu", True] * 2, seen
+    attn = [c[1][0]._obj for c in rec.calls if c[0] in ("icap_attention_fwd", "icap_attention_bwd")]
+    gpt = [a for a in attn if a.seq_off]  # the GPT-2 blocks' packed launches (the mapper's are not packed)
+    assert gpt and all(a.short_only == 1 for a in gpt), [a.short_only for a in gpt]
+
+
+def test_serial_mapper_schedule_shares_gradient_buffers():
+    """The default (serial) mapper backward shares one set of gradient buffers across layers (two alternating for
+    the residual stream); the side / grouped schedules keep one per layer."""
+    from icap.mapper import TransformerMapperCore
+
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        model = tiny_model()
+        t = CaptionTrainer(model, 3, 12, num_training_steps=3, dropout=True)
+        assert isinstance(t.mcore, TransformerMapperCore)
+        ws = t.mws
+        nl = len(ws.g_dz)
+        assert len({b.data_ptr() for b in ws.g_dz}) == 1 and len({b.data_ptr() for b in ws.g_dqkv}) == 1
+        assert len({b.data_ptr() for b in ws.g_r}) == min(2, nl) and len({b.data_ptr() for b in ws.g_m}) == min(2, nl)
+        t.load_batch(*batch(3, 12))
+        t.micro_step()
+        _assert_clean(rec)
+        side = CaptionTrainer(model, 3, 12, num_training_steps=3, dropout=True, mapper_dw="side")
+        assert len({b.data_ptr() for b in side.mws.g_dz}) == nl
+
+
 def test_gpt2_small_bench_shape_with_clip_in_bounds():
     """The benchmarked configuration (GPT-2 small + ViT-B/32 + transformer mapper, bf16) at B=8."""
     with dry_run() as rec:

@@ -16,10 +16,10 @@ OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 
 
 def _code_objects(tmp_path):
-    if not os.path.exists(OBJDUMP):
-        pytest.skip("llvm-objdump not available")
     if not os.path.exists(LIB):
         pytest.skip("libicap_hip.so not built")
+    # a built library is always checked: without the disassembler the guard would pass silently
+    assert os.path.exists(OBJDUMP), f"{OBJDUMP} is needed to check the built libicap_hip.so"
     lib = tmp_path / "lib.so"
     shutil.copy(LIB, lib)  # --offloading writes the bundles next to its input
     subprocess.run([OBJDUMP, "--offloading", str(lib)], check=True, capture_output=True, cwd=tmp_path)
@@ -36,3 +36,13 @@ def test_no_packed_fp32(tmp_path):
         if n:
             bad[o.name] = n
     assert not bad, f"packed-FP32 instructions in {bad}"
+
+
+def test_makefile_keeps_vectorizers_off():
+    """The flags that keep packed FP32 out are in CXXFLAGS, and EXTRA cannot switch the vectorizers back on (the
+    Makefile rejects it)."""
+    mk = open(os.path.join(HERE, "..", "gpt2-image-captioning_amd", "csrc", "Makefile")).read()
+    assert "-fno-slp-vectorize -fno-vectorize" in mk
+    r = subprocess.run(["make", "-n", "-C", os.path.join(HERE, "..", "gpt2-image-captioning_amd", "csrc"),
+                        "EXTRA=-fslp-vectorize"], capture_output=True, text=True)
+    assert r.returncode != 0 and "vectoriz" in (r.stdout + r.stderr), (r.returncode, r.stderr[-400:])

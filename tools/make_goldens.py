@@ -9,7 +9,8 @@ outputs. Dropout is disabled (GPT2Config *_pdrop=0 and the mapper's dropout
 modules set to p=0) so outputs are deterministic. Only inputs + outputs are
 written: no reference source travels.
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tools/make_goldens.py [tiny small clip vit clip_l14 dino topp small_train medium ckpt]
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/make_goldens.py [tiny small clip vit clip_l14 dino topp small_train medium ckpt
+                                                            small_bf16w bench128_bf16w]
 """
 
 from __future__ import annotations
@@ -469,6 +470,85 @@ def golden_bench128(workdir):
     print("bench128 loss", out["loss"], "train", losses)
 
 
+def bf16_round_(module):
+    """Every floating parameter of `module` rounded to bf16 in place (kept fp32): the weights the bf16 perf mode
+    computes with (frozen GPT-2 / CLIP weights are stored bf16; the trained mapper's compute copy is its bf16
+    rounding). The reference then computes in fp32 on them: SURVEY.md §8(c) "bf16-rounded-weights" variant."""
+    with torch.no_grad():
+        for prm in module.parameters():
+            if prm.is_floating_point():
+                prm.copy_(prm.to(torch.bfloat16).float())
+
+
+def golden_small_bf16w(workdir):
+    """The 'small' golden (GPT-2 small + transformer mapper, B = 4, L = 50) and the benchmarked greedy shape (128 x 50)
+    with every weight pre-rounded to bf16: the reference's own forward (loss, every position's logsumexp and argmax,
+    selected logit rows) and generate() in fp32 on those weights -> tests/golden/small_bf16w.npz. The bf16 perf mode's
+    remaining difference from it is the rounding of activations, not of weights."""
+    gcfg, mcfg = O.GPT2Cfg(), O.MapperCfg()
+    torch.manual_seed(0)
+    model, _, _ = build_ref(gcfg, mcfg, seed=0)
+    bf16_round_(model)
+    model.eval()
+    ids, mask, labels, emb = O.synthetic_batch(4, 50, 13, gcfg.vocab_size, gcfg.eos, mcfg.embed_dim, seed=1)
+    out = {"ids": ids.numpy(), "mask": mask.numpy(), "labels": labels.numpy(), "emb": emb.numpy()}
+    with torch.no_grad():
+        res = model.forward(caption_token_ids=ids, image_embeddings=emb, attention_mask=mask, labels=labels)
+        out["prefix"] = model.mapping_network(emb).numpy()
+    out["loss"] = np.array([res.loss.item()])
+    lg = res.logits.double()
+    out["lse"] = torch.logsumexp(lg, -1).numpy()
+    out["argmax"] = lg.argmax(-1).numpy()
+    rows = torch.tensor([14, 27, 64])
+    out["logit_rows"] = rows.numpy()
+    out["logits_sel"] = res.logits[:2][:, rows].numpy()
+    g = torch.Generator().manual_seed(5)  # the small_greedy128 embeddings
+    e = torch.randn((128, mcfg.embed_dim), generator=g)
+    e = e / e.norm(dim=-1, keepdim=True)
+    with torch.no_grad():
+        out["greedy128"] = model.generate(e, max_length=50, temperature=0.0).numpy()
+    np.savez_compressed(os.path.join(OUT, "small_bf16w.npz"), **out)
+    print("small_bf16w loss", out["loss"], "greedy128", out["greedy128"].shape)
+
+
+def golden_bench128_bf16w(workdir):
+    """bench128 (the benchmarked B = 128 step) with every weight — CLIP tower, GPT-2, mapper init — pre-rounded to
+    bf16 and the reference computing in fp32: CLIP features, forward loss, 2 train() steps, trained mapper samples
+    -> tests/golden/bench128_bf16w.npz (the bf16 train step's update-direction bounds)."""
+    from transformers import CLIPConfig, CLIPModel
+
+    gcfg, mcfg = O.GPT2Cfg(), O.MapperCfg()
+    hf = CLIPModel(CLIPConfig())
+    missing, unexpected = hf.load_state_dict(O.clip_vision_state_dict(O.ClipCfg(), seed=0), strict=False)
+    assert not unexpected
+    bf16_round_(hf.vision_model)
+    bf16_round_(hf.visual_projection)
+    hf.eval()
+    B = 128
+    px = torch.randn((B, 3, 224, 224), generator=torch.Generator().manual_seed(21))
+    with torch.no_grad():
+        feats = hf.get_image_features(pixel_values=px)
+        feats = getattr(feats, "pooler_output", feats)
+        emb = feats / feats.norm(p=2, dim=-1, keepdim=True)
+    ids, mask, labels, _ = O.synthetic_batch(B, 50, 13, gcfg.vocab_size, gcfg.eos, mcfg.embed_dim, seed=22)
+    torch.manual_seed(0)
+    model, _, _ = build_ref(gcfg, mcfg, seed=0)
+    bf16_round_(model)
+    model.eval()
+    with torch.no_grad():
+        res = model.forward(caption_token_ids=ids, image_embeddings=emb, attention_mask=mask, labels=labels)
+    out = {"pixels_seed": np.array([21]), "batch_seed": np.array([22]), "emb": emb.numpy(),
+           "loss": np.array([res.loss.item()])}
+    init = {k: v.detach().clone() for k, v in model.mapping_network.state_dict().items()}
+    losses = run_ref_train(model, (ids, mask, labels, emb), 2, 1e-4, True, workdir)
+    out["train_losses"] = np.array(losses)
+    for k, v in model.mapping_network.state_dict().items():
+        a = (v.detach() - init[k]).numpy().reshape(-1)  # the update of this (rounded-init) run
+        out["update_sample." + k] = a.copy() if a.size <= 20000 else a[::997].copy()
+    np.savez_compressed(os.path.join(OUT, "bench128_bf16w.npz"), **out)
+    print("bench128_bf16w loss", out["loss"], "train", losses)
+
+
 def golden_ckpt_keys(workdir):
     """Key sets + shapes of the reference's save_parameters() files (src/models.py:489-519) for the transformer
     mapper with GPT-2 frozen / unfrozen and the MLP mapper (GPT-2 small geometry), and of its extraction .pt
@@ -533,6 +613,10 @@ def main():
             golden_bench128(work)
         if not only or "ckpt" in only:
             golden_ckpt_keys(work)
+        if not only or "small_bf16w" in only:
+            golden_small_bf16w(work)
+        if not only or "bench128_bf16w" in only:
+            golden_bench128_bf16w(work)
     finally:
         os.chdir(cwd)
 
