@@ -197,6 +197,11 @@ class ClipCore:
         # [D, C*p*p] (c, ky, kx) order, zero-padded to the 8-multiple row of icap_im2col_patches (p = 14: 592)
         wp = vm.embeddings.patch_embedding.weight.data.reshape(self.D, -1)
         self.Kp = (wp.shape[1] + 7) // 8 * 8
+        # bf16 towers: the fused gather GEMM (icap_patch_embed) where it is the faster form. Measured round 6
+        # (profiles/r06_patch_bench.txt, B = 128): ViT-B/32 fused 101.0 us vs im2col + the split-role GEMM (96 x 128
+        # tiles) + vit_embed 85.8 us — the fused kernel's 6 column tiles each re-gather their rows' fp32 pixels;
+        # ViT-L/14 fused 200.5 vs 221.5 us (K = 588: the GEMM is short, the im2col pass is not)
+        self.fused_patch = self.dtype == torch.bfloat16 and c.patch_size != 32
         if self.Kp != wp.shape[1]:
             wp = torch.nn.functional.pad(wp, (0, self.Kp - wp.shape[1]))
         self.w_patch = self._cvt(wp)
@@ -229,7 +234,7 @@ class ClipCore:
         M = B * self.S
         e = lambda *shape, dtype=dt: torch.empty(shape, dtype=dtype, device=dev)  # noqa: E731
         ws = SimpleNamespace(B=B, M=M)
-        if dt != torch.bfloat16:  # (bf16: icap_patch_embed reads the pixels itself — no patch matrix)
+        if not self.fused_patch:  # (icap_patch_embed reads the pixels itself — no patch matrix)
             ws.patches = e(B * self.G * self.G, self.Kp)
             ws.pe = e(B * self.G * self.G, D)
         ws.x, ws.h1, ws.a, ws.o = e(M, D), e(M, D), e(M, D), e(M, D)
@@ -251,11 +256,11 @@ class ClipCore:
         """Kernel schedule; returns ws.emb (fp32, L2-normalised) — graph-capturable."""
         c, D, B = self.c, self.D, ws.B
         eps = c.layer_norm_eps
-        if self.dtype == torch.bfloat16:
+        if self.fused_patch:
             # Conv2d(stride=patch, bias=False) + [CLS || patches] + positions in one launch that gathers the pixel runs
             # into its LDS stages (round 5: no im2col patch matrix, no separate embedding pass)
             ops.patch_embed(pixels, self.w_patch, ws.h1, patch=c.patch_size, prefix=self.cls.view(1, D), pos=self.pos)
-        else:  # fp32 parity mode: the exact-fp32 tile GEMM over the im2col matrix
+        else:  # the im2col matrix (bf16 / fp32 parity mode) and the GEMM over it
             ops.im2col_patches(pixels, ws.patches, c.patch_size)
             ops.gemm(ws.patches, self.w_patch, ws.pe)  # Conv2d(stride=patch, bias=False) as a GEMM
             ops.vit_embed(ws.pe, self.cls, self.pos, ws.h1, B, self.G * self.G, D)

@@ -54,6 +54,21 @@ class ImageDirectoryDataset(Dataset):
         return list(names), packed, sizes
 
 
+def _worker_context(dev):
+    """The DataLoader workers' start method: never fork them from a process that has initialised HIP. A forked
+    worker shares the parent's pages copy-on-write, HIP runtime threads and locks included, and the parent then DMAs
+    from pageable host memory that the child maps too (round-5 suite hang, DESIGN.md "Extraction loader"); the
+    forkserver starts from a fresh interpreter (no HIP state) and forks the workers from there. Before any GPU call
+    (CPU extraction, tests) plain fork is kept: it is the cheapest start."""
+    if dev is not None and dev.type == "cuda" and torch.cuda.is_initialized():
+        import multiprocessing as mp
+
+        ctx = mp.get_context("forkserver")
+        ctx.set_forkserver_preload(["torch", "PIL.Image", "numpy"])
+        return ctx
+    return None
+
+
 @torch.no_grad()
 def _worker_init(_):
     """DataLoader worker: one intra-op thread (PIL decodes single-threaded; torch's default of one thread per core
@@ -80,7 +95,8 @@ def extract_directory(image_dir: str, output_path: str, embed: Callable, process
     pin = packed and dev is not None and dev.type == "cuda"
     dl = DataLoader(ds, batch_size=batch_size, shuffle=False, num_workers=num_workers, pin_memory=pin,
                     collate_fn=ImageDirectoryDataset.packed_collate if packed else ImageDirectoryDataset.collate_fn,
-                    persistent_workers=False, worker_init_fn=_worker_init if num_workers > 0 else None)
+                    persistent_workers=False, worker_init_fn=_worker_init if num_workers > 0 else None,
+                    multiprocessing_context=_worker_context(dev) if num_workers > 0 else None)
     names: List[str] = []
     embs: List[torch.Tensor] = []
     t_wait = t_issue = 0.0
@@ -104,8 +120,10 @@ def extract_directory(image_dir: str, output_path: str, embed: Callable, process
             batch_names, batch_images = batch
             px = processor(images=batch_images).pixel_values
             if device is not None:
-                # (pageable host memory: a plain copy — non_blocking buys nothing without a pinned source, and one
-                # suite run hung inside such a copy with the loader's workers alive; the packed path pins its buffer)
+                # pageable host memory (the host processor's output): a plain copy. non_blocking from pageable memory
+                # overlaps nothing — the runtime stages it through its own pinned buffer before returning — and it
+                # was one of the two ingredients of the round-5 hang (DESIGN.md "Extraction loader"); the packed
+                # path's buffer is pinned by the loader and copies asynchronously
                 px = px.to(device)
         # the embeddings stay on the device until the end (one copy back, src/embeddings/clip.py:140 copies per
         # batch): no per-batch synchronisation, so the next batch's host work overlaps this batch's kernels

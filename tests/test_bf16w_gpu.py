@@ -12,16 +12,25 @@ import pytest
 import torch
 
 from oracle import icap_oracle as O
-from test_bench_shape_gpu import _run as bench_run
 from test_model_gpu import build, inputs, load, rel
 
 pytestmark = pytest.mark.gpu
 
-# bounds (measured values in the comments; SURVEY.md §7 measured 7.5e-3 max-rel logits and 97.5 % argmax agreement
-# for bf16-input / fp32-accumulate GEMMs against such weights)
-LOSS_D, LOGIT_REL, ARGMAX_MIN, LSE_D = 1e-2, 2.5e-2, 0.95, 2.5e-2
-GREEDY_FIRST, GREEDY_FIVE = 0.95, 0.85
-TRAIN_LOSS_D, COS_ALL, COS_T, REL_T = 1.5e-2, 0.935, 0.89, 0.36
+# bounds, from the values measured on MI355X (r06, profiles/r06_bf16w_tests.txt; SURVEY.md §7 had measured 7.5e-3
+# max-rel logits and 97.5 % argmax agreement for bf16-input / fp32-accumulate GEMMs on such weights):
+#   forward: loss |d| 1.3e-3, selected logits max-rel 1.05e-2, argmax agreement 0.9885, per-position lse 1.8e-4
+#   (against the fp32 golden the bounds are 3e-2 / 5e-2 / 0.90);
+LOSS_D, LOGIT_REL, ARGMAX_MIN, LSE_D = 5e-3, 2e-2, 0.97, 1e-3
+#   greedy 128 x 50: first token 0.953, first five 0.898 — random-init logits have top-1 / top-2 margins down to
+#   ~1e-2, so near-ties decide these, not the weights' rounding (against the fp32 golden: 0.90 / 0.70);
+GREEDY_FIRST, GREEDY_FIVE = 0.93, 0.85
+#   the B = 128 step's first gradient (before clip / AdamW) over the mapper: cosine 0.9808 overall, 0.9724 for the
+#   worst tensor (layers.5.norm2.bias), relative error <= 0.236 — bf16 activations through 12 GPT-2 layers and back;
+#   the losses of 2 steps |d| 1.8e-4 / 4.0e-3 (fp32 golden bound 3e-2)
+GRAD_COS_ALL, GRAD_COS_T, GRAD_REL_T, TRAIN_LOSS_D = 0.97, 0.96, 0.30, 1e-2
+# (the update after AdamW — cosine 0.891 overall, 0.813 for the worst tensor against this golden, the same as against
+# the fp32 one — is bounded by test_bench_shape_gpu.py: AdamW's per-element normalisation turns the bf16 noise of
+# near-zero gradient elements into full-size steps, whatever the weights' rounding)
 
 
 def test_small_forward_bf16_vs_bf16w(dev):
@@ -57,29 +66,47 @@ def test_bf16_greedy128_vs_bf16w(dev):
     assert first >= GREEDY_FIRST and five >= GREEDY_FIVE, (first, five)
 
 
-def test_bench_shape_bf16_vs_bf16w(dev):
-    """The benchmarked B = 128 step (CLIP from pixels, compact LM head, eager then graph replay) against 2 reference
-    train() steps on bf16-rounded weights: losses and the mapper update (param - init, each side from its own init)."""
+def test_bench_shape_bf16_grad_vs_bf16w(dev):
+    """The benchmarked B = 128 step (CLIP from pixels, compact LM head, bf16) against the reference on bf16-rounded
+    weights: the first step's mapper gradient (the flat gradient buffer after one micro-step, before AdamW reads it)
+    per tensor, and the two steps' losses."""
+    from icap import CaptionTrainer
+    from icap.clip import CLIPVisionTower
+
     g = load("bench128_bf16w")
-    _, model, init, losses, emb = bench_run(torch.bfloat16, dev)
-    ce = float(torch.nn.functional.cosine_similarity(emb.double().cpu(), torch.from_numpy(g["emb"]).double(), -1).min())
-    dl = [abs(a - b) for a, b in zip(losses, g["train_losses"])]
-    cos_t, rel_t, ua, ra = {}, {}, [], []
-    for k, v in model.mapping_network.state_dict().items():
-        step = 1 if v.numel() <= 20000 else 997
-        u = (v.detach().double().reshape(-1)[::step] - init[k].double().reshape(-1)[::step]).cpu()
-        r = torch.from_numpy(g["update_sample." + k]).double()
+    B = 128
+    model = build(O.GPT2Cfg(), O.MapperCfg(), torch.bfloat16, dev)
+    tower = CLIPVisionTower.random_init(seed=0).to(dev)
+    ids, mask, labels, _ = O.synthetic_batch(B, 50, 13, seed=int(g["batch_seed"][0]))
+    px = torch.randn((B, 3, 224, 224), generator=torch.Generator().manual_seed(int(g["pixels_seed"][0])))
+    t = CaptionTrainer(model, B, 50, lr=1e-4, num_training_steps=2, dropout=False, clip_model=tower)
+    t.load_batch(ids, mask, labels, pixels=px)
+    t.micro_step(use_graph=False)
+    losses = [t.last_loss.item()]
+    ce = float(torch.nn.functional.cosine_similarity(t.emb_c.float().cpu().double(),
+                                                     torch.from_numpy(g["emb"]).double(), -1).min())
+    cos_t, rel_t, ga, ra = {}, {}, [], []
+    for k, prm in model.mapping_network.named_parameters():
+        if "grad_sample." + k not in g:
+            continue
+        step = 1 if prm.numel() <= 20000 else 997
+        u = t.flat.grad(prm).detach().double().reshape(-1)[::step].cpu()
+        r = torch.from_numpy(g["grad_sample." + k]).double()
         if r.norm() == 0:
             continue
         cos_t[k] = float(torch.nn.functional.cosine_similarity(u, r, dim=0))
         rel_t[k] = float((u - r).norm() / r.norm())
-        ua.append(u)
+        ga.append(u)
         ra.append(r)
-    cos_all = float(torch.nn.functional.cosine_similarity(torch.cat(ua), torch.cat(ra), dim=0))
+    t.micro_step(use_graph=True)
+    losses.append(t.last_loss.item())
+    dl = [abs(a - b) for a, b in zip(losses, g["train_losses"])]
+    cos_all = float(torch.nn.functional.cosine_similarity(torch.cat(ga), torch.cat(ra), dim=0))
     kmin, kmax = min(cos_t, key=cos_t.get), max(rel_t, key=rel_t.get)
-    print(f"bench128 bf16 vs bf16-weight reference: CLIP embedding min cosine {ce:.6f}, loss |d| {dl}, update cosine "
-          f"all {cos_all:.4f}, min {cos_t[kmin]:.4f} ({kmin}), max rel {rel_t[kmax]:.4f} ({kmax})")
-    print("worst cosines:", sorted((round(c, 4), k) for k, c in cos_t.items())[:6])
+    print(f"bench128 bf16 vs bf16-weight reference: CLIP embedding min cosine {ce:.6f}, loss |d| {dl}, first-step "
+          f"gradient cosine all {cos_all:.6f}, min {cos_t[kmin]:.6f} ({kmin}), max rel {rel_t[kmax]:.4f} ({kmax})")
+    print("worst gradient cosines:", sorted((round(c, 6), k) for k, c in cos_t.items())[:6])
+    assert len(cos_t) >= 20
     assert max(dl) < TRAIN_LOSS_D, dl
-    assert cos_all >= COS_ALL and min(cos_t.values()) >= COS_T and max(rel_t.values()) <= REL_T, (
+    assert cos_all >= GRAD_COS_ALL and cos_t[kmin] >= GRAD_COS_T and rel_t[kmax] <= GRAD_REL_T, (
         cos_all, cos_t[kmin], rel_t[kmax])

@@ -539,6 +539,19 @@ def golden_bench128_bf16w(workdir):
         res = model.forward(caption_token_ids=ids, image_embeddings=emb, attention_mask=mask, labels=labels)
     out = {"pixels_seed": np.array([21]), "batch_seed": np.array([22]), "emb": emb.numpy(),
            "loss": np.array([res.loss.item()])}
+    # the first step's gradient of the mean loss w.r.t. every mapper tensor (before clip_grad_norm / AdamW: the
+    # update direction after AdamW's per-element normalisation is dominated by the elements whose gradient is ~0)
+    model.train()
+    for prm in model.gpt.parameters():
+        prm.requires_grad = False
+    model.zero_grad(set_to_none=True)
+    model.forward(caption_token_ids=ids, image_embeddings=emb, attention_mask=mask, labels=labels).loss.backward()
+    for k, prm in model.mapping_network.named_parameters():
+        if prm.grad is None:
+            continue
+        a = prm.grad.detach().numpy().reshape(-1)
+        out["grad_sample." + k] = a.copy() if a.size <= 20000 else a[::997].copy()
+    model.zero_grad(set_to_none=True)
     init = {k: v.detach().clone() for k, v in model.mapping_network.state_dict().items()}
     losses = run_ref_train(model, (ids, mask, labels, emb), 2, 1e-4, True, workdir)
     out["train_losses"] = np.array(losses)
