@@ -201,7 +201,7 @@ class ClipCore:
         # (profiles/r06_patch_bench.txt, B = 128): ViT-B/32 fused 101.0 us vs im2col + the split-role GEMM (96 x 128
         # tiles) + vit_embed 85.8 us — the fused kernel's 6 column tiles each re-gather their rows' fp32 pixels;
         # ViT-L/14 fused 200.5 vs 221.5 us (K = 588: the GEMM is short, the im2col pass is not)
-        self.fused_patch = self.dtype == torch.bfloat16 and c.patch_size != 32
+        self.fused_patch = self.dtype == torch.bfloat16 and self.c.patch_size != 32
         if self.Kp != wp.shape[1]:
             wp = torch.nn.functional.pad(wp, (0, self.Kp - wp.shape[1]))
         self.w_patch = self._cvt(wp)
