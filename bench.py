@@ -176,8 +176,10 @@ def synthetic_batch(B, seed, dev):
     labels = ids.clone()
     labels[mask == 0] = -100
     px = torch.randn((B, 3, 224, 224), generator=g)
-    # ids / mask / labels stay on the host, as a DataLoader delivers them: the trainer reads each batch's packing
-    # flags from host labels (no device sync) and copies them to its device buffers
+    # ids / mask / labels stay on the host, pinned, as icap.train's DataLoader (pin_memory=True) delivers them: the
+    # trainer reads each batch's packing flags from host labels (no device sync) and copies them asynchronously
+    if torch.device(dev).type == "cuda":
+        ids, mask, labels = ids.pin_memory(), mask.pin_memory(), labels.pin_memory()
     return ids, mask, labels, px.to(dev)
 
 

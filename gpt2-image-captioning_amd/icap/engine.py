@@ -31,6 +31,11 @@ GRAD_OVERWRITE = True
 Tensor = torch.Tensor
 
 
+def _async_src(t: Tensor) -> bool:
+    """A host-to-device copy may be queued asynchronously only from pinned memory; device sources always may."""
+    return t.device.type != "cpu" or t.is_pinned()
+
+
 class CaptionTrainer:
     def __init__(self, model, batch_size: int, caption_len: int, *, lr: float = 1e-4, weight_decay: float = 0.01,
                  betas=(0.9, 0.999), eps: float = 1e-8, max_norm: float = 1.0, num_warmup_steps: int = 0,
@@ -192,15 +197,18 @@ class CaptionTrainer:
             # already on the device the flag stays off (both passes launched; same results) rather than forcing a
             # device-to-host sync per batch
             self.gws.short_only = labels.device.type == "cpu" and max_seq_len(labels, self.P) <= 32
-        self.ids.copy_(ids, non_blocking=True)
-        self.mask.copy_(mask, non_blocking=True)
-        self.labels.copy_(labels, non_blocking=True)
+        # asynchronous only from pinned host memory (the loaders' batches) or device memory: a pageable source is
+        # copied synchronously (non_blocking from pageable memory overlaps nothing and was part of the round-5 hang,
+        # DESIGN.md "Extraction loader")
+        self.ids.copy_(ids, non_blocking=_async_src(ids))
+        self.mask.copy_(mask, non_blocking=_async_src(mask))
+        self.labels.copy_(labels, non_blocking=_async_src(labels))
         if pixels is not None:
             if self.pixels is None:
                 raise ValueError("trainer was built without a CLIP tower; pass image embeddings")
-            self.pixels.copy_(pixels, non_blocking=True)
+            self.pixels.copy_(pixels, non_blocking=_async_src(pixels))
         elif emb is not None:
-            self.emb.copy_(emb, non_blocking=True)
+            self.emb.copy_(emb, non_blocking=_async_src(emb))
 
     # -- the step ---------------------------------------------------------------------------------------------
     def _fwd_bwd(self, zero: bool, grad_scale: float) -> None:
