@@ -500,7 +500,7 @@ static int g256_mode() {
 // head 8320 x 50304 x 768: 758 vs 835 us), not on the train step's 2-round K = 768 products (8320 x 3072 x 768:
 // 84 vs 80 us) (profiles/r02_gemm256_bench.txt). path 3 forces it where eligible.
 static bool g256_pick(const icap_gemm_args& p) {
-  if (p.path == 1 || (p.path >= 4 && p.path <= 9)) return false;
+  if (p.path == 1 || (p.path >= 4 && p.path <= 10)) return false;
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.beta != 0.f || p.m_dev || p.split_k > 1) return false;
   if (p.ln_stats_out || p.ln_stats_in) return false;
   if (p.M < 256 || p.N < 256 || p.K < 64) return false;

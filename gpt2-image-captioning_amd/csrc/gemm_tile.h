@@ -893,7 +893,9 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
 
 template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, int ACT = ACT_ANY,
           bool ROLES = false>
-__global__ __launch_bounds__(64 * (WM * WN + (ROLES ? 4 : 0)), MINB) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
+// (hip-clang reads launch_bounds' second argument as waves per SIMD: MINB blocks of NWT waves per CU is MINB NWT / 4
+// rounded up — for the 4-wave blocks the same number)
+__global__ __launch_bounds__(64 * (WM * WN + (ROLES ? 4 : 0)), (MINB * (WM * WN + (ROLES ? 4 : 0)) + 3) / 4) void gemm_kernel(icap_gemm_args p, int tiles_n, int splits,
                                                                   int nk_split, uint32_t drop_thresh, float inv_keep) {
   const int64_t Mv = p.m_dev && (int64_t)*p.m_dev < p.M ? (int64_t)*p.m_dev : p.M;  // device row count
   if constexpr (ROLES) {
