@@ -673,7 +673,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
       const int64_t m_pl = (p.m_dev && p.m_hint > 0 && p.m_hint < p.M) ? p.m_hint : p.M;
       const int64_t t256 = ((m_pl + 255) / 256) * ((p.N + 255) / 256);
       const int64_t cus = device_cus();
-      if (p.K <= 1536 && t256 * 10 >= cus * 8 && t256 <= cus) bn = 256;
+      // and (round 6) many rounds of them: the compact LM head, 1664 live rows x 50304 x 768 = 1379 tiles: 157 vs
+      // 180 us on the 3-block 128 x 128 tiles (hipBLASLt 146; profiles/r06_lmhead_ab.txt)
+      if (p.K <= 1536 && ((t256 * 10 >= cus * 8 && t256 <= cus) || t256 >= 4 * cus)) bn = 256;
     }
     if (bn) {
       pl.g8p = bn;
