@@ -112,6 +112,14 @@ struct lds_frags {
 // ROLES (round 6; variants 26 / 27 / 28): the block has 4 more waves; waves 0 .. NW-1 read fragments and issue MFMAs
 // only (NW = 4: one per SIMD; NW = 8: two per SIMD), waves NW .. NW+3 issue the LDS-DMA of the NST-stage ring and wait
 // for it (one per SIMD), so the DMA's issue cost runs beside the MFMA stream instead of in front of it.
+// epilogue prefetch groups of a ROLES block: the fewest (a divisor of the NH staging passes) that keep a wave's
+// prefetched rows (passes per group x rows per pass / the NHALF waves sharing them) at <= 4 16-byte rows
+constexpr int roles_prefetch_groups(int nh, int rows_per_pass, int nhalf) {
+  for (int g = 1; g < nh; ++g)
+    if (nh % g == 0 && (nh / g) * rows_per_pass / nhalf <= 4) return g;
+  return nh;
+}
+
 template <typename TI, typename TC, int NST, int MINB, int WM, int WN, int TM, int TN, bool KOUT = false, int ACT = ACT_ANY,
           bool ROLES = false>
 // The body of one tile (gemm_kernel below runs it once per block, or, for ROLES, once per live tile of a grid-stride
@@ -758,11 +766,15 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
   // launches a CU holds 1-2 tiles, so nothing else hides it). Out-of-range rows read row Mv-1 (no branch per
   // load: cdna_hip_programming.md §5 trap (c)) and are never stored.
   constexpr int NH = 16 * TM / EPR;              // staging passes
-  constexpr int NPG = MINB >= 4 && NH >= 2 ? 2 : 1;  // prefetch groups: half the rows at a time at 128 VGPRs
+  // prefetch groups: half the rows at a time at 128 VGPRs; ROLES (round 6): at most 4 rows per wave at a time —
+  // the 128 x 256 / 192 x 256 tiles held 8 / 12 and the compiler demoted the array to scratch, each load then waited
+  // for its own round trip before its scratch store (192 x 256 dgelu epilogue: 22.7 us)
+  constexpr int NPG = ROLES ? roles_prefetch_groups(NH, EPR / RPI, NHALF) : (MINB >= 4 && NH >= 2 ? 2 : 1);
   constexpr int HPG = NH / NPG;                  // passes per prefetch group
-  constexpr int NEP = HPG * (EPR / RPI);         // prefetched rows held at once
+  constexpr int NEP = HPG * (EPR / RPI);         // prefetched rows of a group (this wave: NEP / NHALF of them)
   typedef typename rawbf<EW>::T pre_t;
-  pre_t pre[NEP];
+  static_assert(NHALF == 1 || (EPR / RPI) % NHALF == 0, "roles: a wave's prefetched rows alternate");
+  pre_t pre[NEP / NHALF];  // (roles, NHALF = 2: row i of the group is this wave's when i % 2 == half, held at i / 2)
   bool want_pre = false;  // block-uniform: this launch has a bf16 dact_src / resid operand
   const bf16_t* esrc = nullptr;
   int64_t eld = 0;
@@ -775,7 +787,7 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
         if (NHALF > 1 && (i % (EPR / RPI)) % NHALF != half) continue;  // (roles: the other wave's rows)
         const int64_t r0 = rb + (int64_t)(g * NEP + i) * RPI;
         const int64_t row = r0 < Mv ? r0 : Mv - 1;
-        pre[i] = *reinterpret_cast<const pre_t*>(esrc + row * eld + col);
+        pre[i / NHALF] = *reinterpret_cast<const pre_t*>(esrc + row * eld + col);
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the loads here: hipcc would sink each to its use
@@ -872,7 +884,7 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
       static_for<0, EPR / RPI>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
         if ((NHALF == 1 || t % NHALF == half) && storer)
-          store_row(h, t, (want_pre && fullw) ? &pre[(h % HPG) * (EPR / RPI) + t] : nullptr);
+          store_row(h, t, (want_pre && fullw) ? &pre[((h % HPG) * (EPR / RPI) + t) / NHALF] : nullptr);
       });
       __syncthreads();
     });

@@ -25,6 +25,10 @@ CASES = [  # (M, live, N, K, epi, roles, what)
     (8320, 3584, 768, 2304, "plain", 96, "c_attn dX"),
     (8320, 3584, 768, 3072, "resid_drop_lns", 96, "mlp c_proj fwd"),
     (8320, 3584, 768, 3072, "plain", 96, "c_fc dX"),
+    (3584, None, 3072, 768, "plain", 192, "r192 plain 3584x3072"),
+    (8320, 3584, 3072, 768, "lnf_gelu", 192, "r192 c_fc fwd (LN fold, gelu, aux)"),
+    (8320, 3584, 3072, 768, "dgelu", 192, "r192 mlp c_proj dX (dgelu)"),
+    (3584, None, 3072, 3072, "plain", 192, "r192 K 3072"),
 ]
 
 
