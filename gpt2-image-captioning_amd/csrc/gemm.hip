@@ -466,8 +466,8 @@ static int roles_actk(const icap_gemm_args& p, int v) {
   else if (fa == ICAP_ACT_GELU_NEW) a = ACT_FWD + ICAP_ACT_GELU_NEW;
   else if (ba == ICAP_ACT_GELU_NEW) a = ACT_BWD + ICAP_ACT_GELU_NEW;
   else if (fa == ICAP_ACT_QUICK_GELU) a = ACT_FWD + ICAP_ACT_QUICK_GELU;
-  else if ((v == 28 || v == 30) && fa == ICAP_ACT_RELU) a = ACT_FWD + ICAP_ACT_RELU;
-  else if ((v == 28 || v == 30) && ba == ICAP_ACT_RELU) a = ACT_BWD + ICAP_ACT_RELU;
+  else if (v == 28 && fa == ICAP_ACT_RELU) a = ACT_FWD + ICAP_ACT_RELU;
+  else if (v == 28 && ba == ICAP_ACT_RELU) a = ACT_BWD + ICAP_ACT_RELU;
   else a = ACT_ANY;
   if (p.c_dtype != ICAP_BF16) return (p.ln_stats_out || p.ln_stats_in) ? -1 : (a == ACT_OFF ? ACT_OFF : ACT_ANY);
   if (p.ln_stats_out) return a == ACT_OFF ? ACT_LNS : -1;
@@ -500,7 +500,7 @@ static int g256_mode() {
 // head 8320 x 50304 x 768: 758 vs 835 us), not on the train step's 2-round K = 768 products (8320 x 3072 x 768:
 // 84 vs 80 us) (profiles/r02_gemm256_bench.txt). path 3 forces it where eligible.
 static bool g256_pick(const icap_gemm_args& p) {
-  if (p.path == 1 || (p.path >= 4 && p.path <= 12)) return false;
+  if (p.path == 1 || (p.path >= 4 && p.path <= 10)) return false;
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.beta != 0.f || p.m_dev || p.split_k > 1) return false;
   if (p.ln_stats_out || p.ln_stats_in) return false;
   if (p.M < 256 || p.N < 256 || p.K < 64) return false;
@@ -574,8 +574,7 @@ static int roles_pick(const icap_gemm_args& p, int64_t m_plan, int64_t nk, int64
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
-  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 12 && p.path != 11),
-               "icap_gemm: path must be 0, 1, 3 ... 10 or 12");
+  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 10), "icap_gemm: path must be 0, 1 or 3 ... 10");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16 || p.in_dtype == ICAP_FP8_MX,
                "icap_gemm: bad in_dtype");
@@ -818,9 +817,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // variants 26 / 27: the split-role ring (gemm_tile.h ROLES) on 128 x 256 / 96 x 128 tiles, one K range per tile
   // (path 8 / 9 force them where eligible; the automatic rule: roles_pick)
   {
-    const int rv = p.path == 8 ? 26 : p.path == 9 ? 27 : p.path == 10 ? 28 : p.path == 12 ? 30
+    const int rv = p.path == 8 ? 26 : p.path == 9 ? 27 : p.path == 10 ? 28
                    : (p.path == 0 && roles_mode() != 0) ? roles_pick(p, m_plan, nk, cus) : 0;
-    const int bm = rv == 26 ? 128 : (rv == 27 || rv == 30) ? 96 : 192, bn = (rv == 27 || rv == 30) ? 128 : 256;
+    const int bm = rv == 26 ? 128 : rv == 27 ? 96 : 192, bn = rv == 27 ? 128 : 256;
     if (rv && p.M >= bm && p.split_k <= 1) {
       if (const int ar = roles_actk(p, rv); ar >= 0) {
         pl.variant = rv;
@@ -831,7 +830,7 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
         tiles = ((p.M + bm - 1) / bm) * tiles_n;
         pl.tiles_n = (int)tiles_n;
         pl.actk = ar;
-        pl.block = dim3((rv == 28 || rv == 30) ? 3 * GNT : 2 * GNT);  // 12 / 8 waves
+        pl.block = dim3(rv == 28 ? 3 * GNT : 2 * GNT);  // 12 / 8 waves
         pl.grid = dim3((unsigned)(tiles < cus ? tiles : cus));  // the kernel walks the live tiles
         return ICAP_OK;
       }
@@ -941,7 +940,6 @@ static const char* variant_kernel(int v) {
     case 26: return "gemm_kernel<%s, %s, 3, 1, 2, 2, 4, 8, false, %d, true>";
     case 27: return "gemm_kernel<%s, %s, 5, 1, 2, 2, 3, 4, false, %d, true>";
     case 28: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 6, 4, false, %d, true>";
-    case 30: return "gemm_pers_kernel<%s, 3, 3, 4, %d>";
     default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %d>";
   }
 }
@@ -967,8 +965,7 @@ extern "C" const char* icap_gemm_kernel_name(const icap_gemm_args* a) {
     snprintf(fmt, sizeof fmt, "gemm_skinny_kernel<%%s, %%s, %d, 2, %d>", pl.nt, pl.sku);
     snprintf(inner, sizeof inner, fmt, ti, tc);
   } else {
-    if (pl.variant == 30) snprintf(inner, sizeof inner, variant_kernel(pl.variant), tc, pl.actk);  // (no TI)
-    else snprintf(inner, sizeof inner, variant_kernel(pl.variant), ti, tc, pl.actk);
+    snprintf(inner, sizeof inner, variant_kernel(pl.variant), ti, tc, pl.actk);
   }
   snprintf(buf, sizeof buf, "icap::%s", inner);
   return buf;
@@ -1042,8 +1039,7 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const int skew = (pl.variant >= 26 && pl.variant <= 28) ? 0 : kskew_for(p, pl.nk_split);
   const int nks = pl.nk_split | (skew << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
-  if (pl.variant == 30) launch_tile_pers(pl, p, pl.nk_split, s);                      // gemm_tile_pers.hip
-  else if (pl.variant == 26) launch_tile_roles(pl, p, nks, s);                       // gemm_tile_roles.hip
+  if (pl.variant == 26) launch_tile_roles(pl, p, nks, s);                            // gemm_tile_roles.hip
   else if (pl.variant == 27) launch_tile_roles96(pl, p, nks, s);                     // gemm_tile_roles96.hip
   else if (pl.variant == 28) launch_tile_roles192(pl, p, nks, s);                    // gemm_tile_roles192.hip
   else if (pl.variant == 22) launch_tile_r256(pl, p, nks, s);                        // gemm_tile_r256.hip

@@ -32,7 +32,6 @@ void launch_tile_w192(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipS
 void launch_tile_roles(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);    // roles 128 x 256 (26)
 void launch_tile_roles96(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);  // roles 96 x 128 (27)
 void launch_tile_roles192(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s); // roles 192 x 256 (28)
-void launch_tile_pers(const GemmPlan& pl, const icap_gemm_args& p, int nk, hipStream_t s);     // persistent roles (30)
 
 }  // namespace icap
 

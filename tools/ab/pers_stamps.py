@@ -1,6 +1,7 @@
 """Round 6: where the persistent split-role GEMM (variant 30, gemm_pers.h) spends its time — per-block timestamps of the
 diagnostic build (`make -C gpt2-image-captioning_amd/csrc stamps`, ICAP_LIB=.../libicap_hip_stamps.so): start -> the MFMA
-waves past B_0 (first stage landed), then each of the first four tiles' C barrier, and the epilogue waves' end."""
+waves past B_0 (first stage landed), then each of the first four tiles' C barrier, and the epilogue waves' end.
+(Variant 30 was removed from the library after this measurement, profiles/r06_pers_stamps.txt; commit 76ffabb has it.)"""
 import os
 import statistics
 import sys
