@@ -500,7 +500,7 @@ static int g256_mode() {
 // head 8320 x 50304 x 768: 758 vs 835 us), not on the train step's 2-round K = 768 products (8320 x 3072 x 768:
 // 84 vs 80 us) (profiles/r02_gemm256_bench.txt). path 3 forces it where eligible.
 static bool g256_pick(const icap_gemm_args& p) {
-  if (p.path == 1 || (p.path >= 4 && p.path <= 10)) return false;
+  if (p.path == 1 || (p.path >= 4 && p.path <= 11)) return false;
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.beta != 0.f || p.m_dev || p.split_k > 1) return false;
   if (p.ln_stats_out || p.ln_stats_in) return false;
   if (p.M < 256 || p.N < 256 || p.K < 64) return false;
@@ -574,7 +574,7 @@ static int roles_pick(const icap_gemm_args& p, int64_t m_plan, int64_t nk, int64
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
-  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 10), "icap_gemm: path must be 0, 1 or 3 ... 10");
+  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 11), "icap_gemm: path must be 0, 1 or 3 ... 11");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16 || p.in_dtype == ICAP_FP8_MX,
                "icap_gemm: bad in_dtype");
@@ -684,6 +684,34 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
       pl.inv_keep = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
       return ICAP_OK;
     }
+  }
+  // variant 31 (round 6): the K-outer weight-gradient products on the split-role ring (4 MFMA + 4 LDS-DMA waves,
+  // 128 x 128 tiles, 4 stages, one block per CU), K split so tiles x splits fill about one round of CUs, the splits
+  // combined by the slab + reduce pass. path 11 forces it for bf16 K-outer launches.
+  if (p.trans_ab && p.in_dtype == ICAP_BF16 && p.path == 11) {
+    const int64_t nk31 = (p.K + 63) / 64;
+    const int64_t cus = device_cus();
+    int64_t s31 = p.split_k >= 1 ? p.split_k : cus / tiles;
+    if (s31 > 8) s31 = 8;
+    while (s31 > 1 && nk31 / s31 < 4) --s31;
+    if (s31 < 1) s31 = 1;
+    const int64_t nks31 = (nk31 + s31 - 1) / s31;
+    s31 = (nk31 + nks31 - 1) / nks31;  // every split gets >= 1 stage
+    if (s31 > 1) {
+      ICAP_REQUIRE((p.N & 3) == 0, "icap_gemm: split-K requires N % 4 == 0");
+      ICAP_REQUIRE(p.workspace && (reinterpret_cast<uintptr_t>(p.workspace) & 15) == 0 &&
+                       p.workspace_bytes >= s31 * p.M * p.N * (int64_t)sizeof(float),
+                   "icap_gemm: split-K workspace missing, misaligned or too small");
+    }
+    pl.variant = 31;
+    pl.splits = (int)s31;
+    pl.fused = false;
+    pl.nk_split = (int)nks31;
+    pl.tiles_n = (int)tiles_n;
+    pl.actk = (p.act == ICAP_ACT_NONE && p.dact == ICAP_ACT_NONE) ? ACT_OFF : ACT_ANY;
+    pl.block = dim3(2 * GNT);
+    pl.grid = dim3((unsigned)(tiles * s31 < cus ? tiles * s31 : cus));  // the kernel walks tiles x splits
+    return ICAP_OK;
   }
   // split-K over K stages for launches that cannot fill the chip (decode-time M = batch, small projections):
   // fp32 partial slabs in the caller's workspace + one deterministic reduce/epilogue pass — or, with tickets, the
@@ -940,6 +968,7 @@ static const char* variant_kernel(int v) {
     case 26: return "gemm_kernel<%s, %s, 3, 1, 2, 2, 4, 8, false, %d, true>";
     case 27: return "gemm_kernel<%s, %s, 5, 1, 2, 2, 3, 4, false, %d, true>";
     case 28: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 6, 4, false, %d, true>";
+    case 31: return "gemm_kernel<%s, %s, 4, 1, 2, 2, 4, 4, true, %d, true>";
     default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %d>";
   }
 }
@@ -1036,10 +1065,11 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const int sp = pl.splits;
   // (the split-role variants walk K in its natural order: one round of tiles, no lockstep panel misses to stagger,
   // and automatic launches then equal forced ones and the tile path bitwise)
-  const int skew = (pl.variant >= 26 && pl.variant <= 28) ? 0 : kskew_for(p, pl.nk_split);
+  const int skew = (pl.variant >= 26 && pl.variant <= 31) ? 0 : kskew_for(p, pl.nk_split);
   const int nks = pl.nk_split | (skew << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
-  if (pl.variant == 26) launch_tile_roles(pl, p, nks, s);                            // gemm_tile_roles.hip
+  if (pl.variant == 31) launch_tile_roles_kout(pl, p, nks, s);                       // gemm_tile_roles_kout.hip
+  else if (pl.variant == 26) launch_tile_roles(pl, p, nks, s);                       // gemm_tile_roles.hip
   else if (pl.variant == 27) launch_tile_roles96(pl, p, nks, s);                     // gemm_tile_roles96.hip
   else if (pl.variant == 28) launch_tile_roles192(pl, p, nks, s);                    // gemm_tile_roles192.hip
   else if (pl.variant == 22) launch_tile_r256(pl, p, nks, s);                        // gemm_tile_r256.hip

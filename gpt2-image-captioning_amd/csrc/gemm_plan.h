@@ -32,6 +32,7 @@ void launch_tile_w192(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipS
 void launch_tile_roles(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);    // roles 128 x 256 (26)
 void launch_tile_roles96(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);  // roles 96 x 128 (27)
 void launch_tile_roles192(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s); // roles 192 x 256 (28)
+void launch_tile_roles_kout(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s); // roles K-outer (31)
 
 }  // namespace icap
 

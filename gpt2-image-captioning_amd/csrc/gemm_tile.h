@@ -128,9 +128,11 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
                                           float inv_keep, const int bid, const int tiles_m, const int64_t Mv) {
   static_assert(!KOUT || (sizeof(TI) == 2 && 16 * WM * TM == 128 && 16 * WN * TN == 128),
                 "K-outer operands: bf16, 128 x 128 tiles");
-  static_assert(!ROLES || (!KOUT && sizeof(TI) == 2 && ((WM == 2 && WN == 2 && NST >= 3) || (WM * WN == 8 && NST >= 2))
-                           && MINB == 1),
-                "roles: bf16 row-major operands, 4 MFMA waves on a ring of >= 3 stages or 8 on >= 2, one block per CU");
+  static_assert(!ROLES || (sizeof(TI) == 2 && MINB == 1 &&
+                            ((WM == 2 && WN == 2 && NST >= 3 && (!KOUT || (TM == 4 && TN == 4))) ||
+                             (!KOUT && WM * WN == 8 && NST >= 2))),
+                "roles: bf16 operands, 4 MFMA waves on a ring of >= 3 stages (K-outer: 128 x 128 tiles) or 8 on >= 2 "
+                "(row-major), one block per CU");
   // MX block-scaled fp8 (TI = fp8_t): a stage's 128-byte LDS row is one 128-deep K step of
   // v_mfma_scale_f32_16x16x128_f8f6f4 (twice the bf16 flops per staged byte and per fragment byte read); the
   // per-32 E8M0 scales of the wave's 4 fragment rows of A and of B come in one 16-byte load each per stage
@@ -402,13 +404,29 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
       uint32_t voff[P];
 #pragma unroll
       for (int i = 0; i < P; ++i) {
-        const int q = i * NLW + lw;  // 8-row piece of the [A tile; B tile] stack
-        const int row = (i < PA ? q : q - BM / 8) * 8 + lrow;
-        voff[i] = (uint32_t)((int64_t)row * (i < PA ? p.lda : p.ldb) + lchunk) * ES;
+        const int q = i * NLW + lw;  // 1-KiB piece of the [A image; B image] stack
+        if constexpr (KOUT) {
+          // K-outer (round 6): 4 k-rows of 256 B per piece, lane l -> k-row 4 q' + (l >> 4), physical chunk l & 15
+          // holding logical chunk (l & 15) ^ kout_swz(row) (the tile kernel's T10 (b) image)
+          const int krow = (i < PA ? q : q - BM / 8) * 4 + (lane >> 4);
+          voff[i] = (uint32_t)((int64_t)krow * (i < PA ? p.lda : p.ldb) + (((lane & 15) ^ kout_swz(krow)) << 3)) * ES;
+        } else {
+          const int row = (i < PA ? q : q - BM / 8) * 8 + lrow;  // 8-row piece
+          voff[i] = (uint32_t)((int64_t)row * (i < PA ? p.lda : p.ldb) + lchunk) * ES;
+        }
       }
       auto issue = [&](int kt, int slot) __attribute__((always_inline)) {
         const bool live = kt < nk;
         const int64_t k0 = live ? kbase + kstep(kt) : 0;
+        if constexpr (KOUT) {  // k-rows past K lie beyond num_records (zeros)
+          const uint32_t ka = (uint32_t)(k0 * p.lda * ES), kb2 = (uint32_t)(k0 * p.ldb * ES);
+#pragma unroll
+          for (int i = 0; i < P; ++i) {
+            const uint32_t lds = __builtin_amdgcn_readfirstlane(sbase + (uint32_t)(slot * STB + (i * NLW + lw) * 1024));
+            dma16a(i < PA ? ra_rsrc : rb_rsrc, lds, live ? voff[i] + (i < PA ? ka : kb2) : OOB);
+          }
+          return;
+        }
         const uint32_t kb = (uint32_t)(k0 * ES);
         const bool kin = live && k0 + lchunk < K;
 #pragma unroll
@@ -462,7 +480,32 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
     __builtin_amdgcn_s_barrier();  // B_0
     __builtin_amdgcn_sched_barrier(0);
     ICAP_STAMP(2, ICAP_NOW());
-    if constexpr (NW == 8) {
+    if constexpr (KOUT) {
+      // K-outer (round 6, the mapper's weight gradients): fragments by ds_read_b64_tr_b16 pairs from the T10 (b)
+      // images (kout_frag), the same k order on both operands; double-buffered by 32-deep substep like the row-major
+      // loop below, every read of stage kt retired (lgkmcnt(0) + ties) before B_{kt+1}
+      auto rdk = [&](uint32_t sb, int ks, u32x4_t(&fa)[TM], u32x4_t(&fb)[TN]) __attribute__((always_inline)) {
+        const char* As = smem + (sb - sbase);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = __builtin_bit_cast(u32x4_t, kout_frag(As, ks * 32, wm * 16 * TM + i * 16, lane));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = __builtin_bit_cast(u32x4_t, kout_frag(As + BM * GROWB, ks * 32, wn * 16 * TN + j * 16, lane));
+      };
+      rdk(sbase, 0, fa0, fb0);
+      for (int kt = 0; kt < nk; ++kt) {
+        const uint32_t sb = sbase + (uint32_t)((kt % NST) * STB);
+        retire(fa0, fb0);
+        rdk(sb, 1, fa1, fb1);
+        mm(fa0, fb0);
+        retire(fa1, fb1);
+        __builtin_amdgcn_s_barrier();  // B_{kt+1}
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 1 < nk) rdk(sbase + (uint32_t)(((kt + 1) % NST) * STB), 0, fa0, fb0);
+        mm(fa1, fb1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (NW == 8) {
       // two MFMA waves per SIMD (variant 28, 96 x 64 per wave): one fragment set each (the 168-register budget of
       // three waves per SIMD), read right before its MFMAs — the partner wave's MFMAs cover the read latency
       for (int kt = 0; kt < nk; ++kt) {
@@ -727,7 +770,7 @@ __device__ __forceinline__ void gemm_body(icap_gemm_args p, int tiles_n, int spl
   }
   ICAP_STAMP(0, (uint64_t)split | ((uint64_t)(fused ? splits - 1 : 0) << 8) | ((uint64_t)tile << 32));
   ICAP_STAMP(4, ICAP_NOW());
-  const bool whole = ROLES || splits == 1 || fused;  // this block applies the full epilogue
+  const bool whole = splits == 1 || fused;  // this block applies the full epilogue (else: its split's slab)
 
   uint64_t seed = 0;
   if (whole && drop_thresh != 0u) seed = eff_seed(p.seed, p.seed_ptr);
@@ -914,12 +957,13 @@ __global__ __launch_bounds__(64 * (WM * WN + (ROLES ? 4 : 0)), (MINB * (WM * WN 
     // a grid of at most one block per CU walks the live tiles (host: grid = min(tiles, CUs)): with the capacity grid
     // of the packed step (65 row tiles for 28 live ones) the dead blocks — 147 KiB of LDS each, so never co-resident
     // with a live one — were dispatched only as the live ones finished and delayed the launch's end
+    // (K-outer: split-K over slabs, the blocks of every split walked the same way; the reduce pass follows)
     constexpr int BM = 16 * WM * TM;
     const int tiles_m = (int)((p.M + BM - 1) / BM);
-    const int nlive = (int)((Mv + BM - 1) / BM) * tiles_n;
+    const int nlive = (int)((Mv + BM - 1) / BM) * tiles_n * splits;
     for (int b = blockIdx.x; b < nlive; b += gridDim.x)
-      gemm_body<TI, TC, NST, MINB, WM, WN, TM, TN, KOUT, ACT, ROLES>(p, tiles_n, 1, nk_split, drop_thresh, inv_keep, b,
-                                                                       tiles_m, Mv);
+      gemm_body<TI, TC, NST, MINB, WM, WN, TM, TN, KOUT, ACT, ROLES>(p, tiles_n, splits, nk_split, drop_thresh, inv_keep,
+                                                                       b, tiles_m, Mv);
   } else {
     gemm_body<TI, TC, NST, MINB, WM, WN, TM, TN, KOUT, ACT, ROLES>(p, tiles_n, splits, nk_split, drop_thresh, inv_keep,
                                                                      blockIdx.x, (int)(gridDim.x / splits) / tiles_n, Mv);

@@ -1,0 +1,79 @@
+"""The K-outer split-role GEMM (round 6: gemm_kernel<..., KOUT = true, ..., ROLES = true>, variant 31,
+csrc/gemm_tile_roles_kout.hip; ops.gemm(trans_ab=True, roles=1)) — the mapper's weight gradients dW[N, K] += dY[rows, N]^T
+X[rows, K] read in place — against the K-outer tile kernels and fp64.
+
+Four MFMA waves read their fragments with ds_read_b64_tr_b16 from the same T10 (b) images the tile kernel uses (same k
+order on both operands) while four loader waves stream the 4-stage ring, so an unsplit product is bitwise the tile
+kernel's unsplit one, and a product split S ways is bitwise the tile kernel's S-way split (same K ranges, same slab +
+reduce pass). Shapes: the packed step's four products over 3200 token rows, partial tiles and a row count that is no
+multiple of 64; fp32 gradients with beta 0 / 1; the 20-launch repeatability screen of the ring's barrier protocol."""
+
+import pytest
+import torch
+
+from icap import ops
+from gemm_helpers import _assert_same, _run, rnd
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [  # (N, K, rows)
+    (2304, 768, 3200),
+    (768, 768, 3200),
+    (3072, 768, 3200),
+    (768, 3072, 3200),
+    (520, 200, 1000),
+    (256, 136, 72),
+]
+NAME = "icap::gemm_kernel<unsigned short, float, 4, 1, 2, 2, 4, 4, true, 0, true>"
+
+
+def _operands(dev, N, K, rows, seed):
+    dY = rnd((rows, N), dev, scale=0.2, seed=seed)
+    X = rnd((rows, K), dev, seed=seed + 1)
+    G = rnd((N, K), dev, torch.float32, 1.0, seed=seed + 2)
+    return dY, X, G
+
+
+@pytest.mark.parametrize("N,K,rows", SHAPES)
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_roles_kout_unsplit_matches_tile(dev, N, K, rows, beta):
+    dY, X, G = _operands(dev, N, K, rows, 1)
+    C, Ct = G.clone(), G.clone()
+    names = _run(lambda: ops.gemm(dY, X, C, beta=beta, M=N, N=K, K=rows, trans_ab=True, split_k=1, roles=1))
+    assert names == [NAME], names
+    ops.gemm(dY, X, Ct, beta=beta, M=N, N=K, K=rows, trans_ab=True, split_k=1, tile_only=True)
+    torch.cuda.synchronize()
+    _assert_same("dW", C, Ct)
+    ref = dY.double().t() @ X.double() + beta * G.double()
+    err = ((C.double() - ref).abs() / (dY.double().abs().t() @ X.double().abs() + beta * G.double().abs())).max()
+    assert err.item() < 1e-5, err.item()
+
+
+@pytest.mark.parametrize("N,K,rows", SHAPES[:4])
+def test_roles_kout_split_matches_tile_split(dev, N, K, rows):
+    """The automatic split of the roles form equals the tile kernel forced to the same split count, bit for bit."""
+    from test_fused_splitk_gpu import _kernel_names
+
+    dY, X, G = _operands(dev, N, K, rows, 5)
+    C, Ct = G.clone(), G.clone()
+    ws = torch.empty(8 * N * K + 64, device=dev, dtype=torch.float32)
+    recs = _kernel_names(lambda: ops.gemm(dY, X, C, beta=1.0, M=N, N=K, K=rows, trans_ab=True, split_k=0, roles=1,
+                                          workspace=ws))
+    (name, splits, fused), = recs
+    assert name == NAME and not fused, recs  # (3072 x 768: 144 tiles, unsplit)
+    ops.gemm(dY, X, Ct, beta=1.0, M=N, N=K, K=rows, trans_ab=True, split_k=splits, tile_only=True, workspace=ws)
+    torch.cuda.synchronize()
+    _assert_same("dW", C, Ct)
+
+
+def test_roles_kout_repeatable(dev):
+    N, K, rows = 2304, 768, 3200
+    dY, X, G = _operands(dev, N, K, rows, 9)
+    outs = []
+    for _ in range(20):
+        C = G.clone()
+        ops.gemm(dY, X, C, beta=1.0, M=N, N=K, K=rows, trans_ab=True, split_k=0, roles=1)
+        outs.append(C)
+    torch.cuda.synchronize()
+    for i, C in enumerate(outs[1:]):
+        _assert_same(f"launch {i + 1}", C, outs[0])
