@@ -1010,6 +1010,42 @@ extern "C" int icap_gemm_plan_info(const icap_gemm_args* a, int32_t* splits, int
   return ICAP_OK;
 }
 
+extern "C" int icap_gemm_group(const icap_gemm_args* a, int32_t n, void* stream) {
+  ICAP_REQUIRE(a != nullptr && n >= 1 && n <= ICAP_GEMM_GROUP_MAX, "icap_gemm_group: 1 ... 8 products");
+  GemmGroup g;
+  g.n = 0;
+  g.tstart[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    const icap_gemm_args& p = a[i];
+    // (the general argument checks of a single product, then the group's own preconditions)
+    GemmPlan pl;
+    icap_gemm_args q = p;
+    q.split_k = 1;
+    q.path = 0;
+    if (const int rc = gemm_plan(q, pl); rc != ICAP_OK) return rc;
+    ICAP_REQUIRE(p.trans_ab && p.in_dtype == ICAP_BF16 && p.c_dtype == ICAP_F32,
+                 "icap_gemm_group: K-outer (trans_ab) bf16 products with an fp32 C");
+    ICAP_REQUIRE(p.act == ICAP_ACT_NONE && p.dact == ICAP_ACT_NONE && !p.bias && !p.resid && !p.aux && !p.ln_gamma &&
+                     !p.ln_wsum && !p.ln_stats_in && !p.ln_stats_out && p.drop_p == 0.f && !p.m_dev,
+                 "icap_gemm_group: plain products only (alpha, beta; no epilogue operands)");
+    if (p.M == 0 || p.N == 0) continue;
+    ICAP_REQUIRE(p.K > 0, "icap_gemm_group: K must be positive");
+    const int k = g.n;
+    g.a[k] = p;
+    g.a[k].split_k = 1;
+    g.a[k].tickets = nullptr;
+    g.tiles_n[k] = (int)((p.N + GBN - 1) / GBN);
+    g.nk[k] = (int)((p.K + 63) / 64);
+    const int64_t tiles = ((p.M + GBM - 1) / GBM) * (int64_t)g.tiles_n[k];
+    ICAP_REQUIRE(g.tstart[k] + tiles < (1ll << 30), "icap_gemm_group: too many tiles");
+    g.tstart[k + 1] = g.tstart[k] + (int)tiles;
+    ++g.n;
+  }
+  if (g.n == 0) return ICAP_OK;
+  launch_group_kout(g, (int)device_cus(), reinterpret_cast<hipStream_t>(stream));
+  return check_launch("icap_gemm_group");
+}
+
 extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   ICAP_REQUIRE(a != nullptr, "icap_gemm: null args");
   if (a->M == 0 || a->N == 0) return ICAP_OK;

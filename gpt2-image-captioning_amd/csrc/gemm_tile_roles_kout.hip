@@ -21,4 +21,26 @@ void launch_tile_roles_kout(const GemmPlan& pl, const icap_gemm_args& p, int nks
 #undef ICAP_GKK
 }
 
+// A group of K-outer products in ONE launch (icap_gemm_group, round 6): every block walks the concatenated tile list of
+// the group (product i owns tile ids [tstart[i], tstart[i + 1])) with the variant-31 body, unsplit — so a layer's four
+// weight-gradient products fill the chip together (432 tiles at the mapper's shape) without split-K slabs or a reduce
+// pass. Each output tile is the variant-31 (and the K-outer tile kernel's) unsplit MFMA chain: bitwise equal to
+// running the products one by one with split_k = 1.
+__global__ __launch_bounds__(512, 2) void gemm_group_kernel(GemmGroup g) {
+  const int total = g.tstart[g.n];
+  for (int b = blockIdx.x; b < total; b += gridDim.x) {
+    int i = 0;
+    while (i + 1 < g.n && b >= g.tstart[i + 1]) ++i;
+    const icap_gemm_args p = g.a[i];
+    const int tn = g.tiles_n[i];
+    const int tm = (g.tstart[i + 1] - g.tstart[i]) / tn;
+    gemm_body<bf16_t, float, 4, 1, 2, 2, 4, 4, true, ACT_OFF, true>(p, tn, 1, g.nk[i], 0u, 1.f, b - g.tstart[i], tm, p.M);
+  }
+}
+
+void launch_group_kout(const GemmGroup& g, int cus, hipStream_t s) {
+  const int total = g.tstart[g.n];
+  hipLaunchKernelGGL(gemm_group_kernel, dim3((unsigned)(total < cus ? total : cus)), dim3(2 * GNT), 0, s, g);
+}
+
 }  // namespace icap

@@ -114,6 +114,7 @@ SIGNATURES = {
     "icap_version": (C.c_int, []),
     "icap_device_arch_ok": (C.c_int, []),
     "icap_gemm": (C.c_int, [C.POINTER(GemmArgs), vp]),
+    "icap_gemm_group": (C.c_int, [C.POINTER(GemmArgs), C.c_int32, vp]),
     "icap_gemm_kernel_name": (C.c_char_p, [C.POINTER(GemmArgs)]),
     "icap_gemm_plan_info": (C.c_int, [C.POINTER(GemmArgs), vp, vp]),
     "icap_mx_scale_bytes": (sz, [i64, i64]),

@@ -42,15 +42,18 @@ class CaptionTrainer:
                  num_training_steps: int = 1, dropout: bool = True, seed: int = 0, clip_model=None,
                  grad_accum_steps: int = 1, process_group=None, compact_head: bool = True,
                  pack_rows: bool = True, dp_overlap: bool = True, dp_bf16: bool = False, force_overlap: bool = False,
-                 mapper_dw: str = "serial"):
+                 mapper_dw: str = "fused"):
         """pack_rows: packed token rows (GPT2Core.alloc_train); dp_overlap: with N > 1 ranks, all-reduce each backward
         segment's gradient bucket beside the later segments (False: one whole-buffer all-reduce after the backward);
         dp_bf16: exchange the gradients as bf16 (half the bytes; rounds the sum over ranks); force_overlap: take the
         bucketed communication-stream step at world size 1 too (exercises the RCCL calls on one GPU).
         mapper_dw (transformer mapper, GPU): where its weight-gradient products run — "serial" (in the dX chain,
-        split-K), "side" (a second stream beside the dX chain) or "group" (a layer's four products unsplit on four
-        streams at the end of its step). All three give the same gradients; neither alternative measured faster than
-        "serial" (DESIGN.md "Concurrency: the packed-FP32 race"), which stays the default."""
+        split-K), "side" (a second stream beside the dX chain), "group" (a layer's four products unsplit on four
+        streams at the end of its step) or "fused" (a layer's four products in one grouped launch at the end of its
+        step, icap_gemm_group; the default since round 6: 13.99k vs 13.41k images/s for "serial" in one session,
+        profiles/r06_mapper_dw_ab.txt). All give the same gradients up to the summation order of the split ("fused"
+        and "group" bitwise equal); "side" and "group" measured no faster than "serial" (DESIGN.md "Concurrency: the
+        packed-FP32 race")."""
         self.model = model
         self.dtype = model.compute_dtype
         self.B, self.Lc = batch_size, caption_len
@@ -92,7 +95,8 @@ class CaptionTrainer:
         self.P = P
         # (per-layer backward gradient buffers only for the schedules whose weight-gradient products trail the dX
         # chain on other streams: 433 MB at B = 128 that the default serial schedule does not need)
-        per_layer = dict(per_layer_grads=mapper_dw != "serial") if isinstance(self.mcore, TransformerMapperCore) else {}
+        per_layer = (dict(per_layer_grads=mapper_dw in ("side", "group")) if isinstance(self.mcore, TransformerMapperCore)
+                     else {})
         self.mws = self.mcore.alloc(B, train=True, **per_layer)
         # packed token rows (GPT2Core.alloc_train): the blocks skip each caption's dead tail (positions after its
         # last loss target, which the causal mask keeps out of every loss term)
@@ -159,8 +163,8 @@ class CaptionTrainer:
         self.gdr = self.gcore.drops(dropout, seed, self.counter, self.gws.M, B, self.gws.S)
         p_map = 0.1 if isinstance(self.mcore, TransformerMapperCore) else 0.0
         self.mdr = self.mcore.drops(dropout, p_map, seed, self.counter, B)
-        if mapper_dw not in ("serial", "side", "group"):
-            raise ValueError(f"mapper_dw must be 'serial', 'side' or 'group', not {mapper_dw!r}")
+        if mapper_dw not in ("serial", "side", "group", "fused"):
+            raise ValueError(f"mapper_dw must be 'serial', 'side', 'group' or 'fused', not {mapper_dw!r}")
         multi = self.dev.type == "cuda" and isinstance(self.mcore, TransformerMapperCore)
         # the mapper's weight-gradient products on a side stream beside its dX chain (mapper.backward_steps side=)
         self._side = None
@@ -173,6 +177,9 @@ class CaptionTrainer:
             self._group = [torch.cuda.Stream(self.dev) for _ in range(3)]
             for sd in self._group:
                 ops.register_side_stream(sd)
+        # "fused": the four products of a layer in one grouped launch at the end of its step (icap_gemm_group)
+        if mapper_dw == "fused" and isinstance(self.mcore, TransformerMapperCore):
+            self._group = "fused"
 
     def share_state_with(self, other: "CaptionTrainer") -> None:
         """Use `other`'s optimizer step counter and dropout counter (same model, another batch shape)."""

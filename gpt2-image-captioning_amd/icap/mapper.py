@@ -80,6 +80,16 @@ class DWHelper:
         else:              # out[N,K] (nn.Linear grad layout)
             ops.gemm(a, b, out, beta=beta, M=N, N=K, K=Mp, alg_flops=2.0 * M * N * K)
 
+    def dW_group(self, items, M: int, accumulate: bool = True) -> None:
+        """dW += dY^T X for every (dY, X, out) of items in one launch (ops.gemm_group: unsplit K-outer products, no
+        slabs or reduce pass) where every operand allows the in-place K-outer read; otherwise one dW() each."""
+        if self.dtype == torch.bfloat16 and all(_kout_ok(dy) and _kout_ok(x) for dy, x, _ in items):
+            beta = 1.0 if accumulate else 0.0
+            ops.gemm_group([(dy, x, out, dy.shape[1], x.shape[1], M, beta) for dy, x, out in items])
+            return
+        for dy, x, out in items:
+            self.dW(dy, x, out, M=M, accumulate=accumulate)
+
     def db(self, dY: Tensor, out: Tensor, M: int, N: Optional[int] = None, accumulate: bool = True) -> None:
         ops.colsum(dY, out, self.cs_ws, accumulate=accumulate, M=M, N=N)
 
@@ -467,8 +477,13 @@ class TransformerMapperCore:
 
         def flush_dw():
             """The layer's queued dW products, unsplit and side by side (group streams forked from the main stream
-            first, so none of them waits for another), then joined back into the main stream."""
+            first, so none of them waits for another), then joined back into the main stream — or, group = "fused",
+            in one grouped launch on the main stream (icap_gemm_group)."""
             if not st.dw:
+                return
+            if group == "fused":
+                dwh.dW_group(st.dw, M, accumulate=acc)
+                st.dw = []
                 return
             main = torch.cuda.current_stream()
             sides = list(group[: len(st.dw) - 1])

@@ -255,6 +255,32 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     return out
 
 
+def gemm_group(items) -> None:
+    """K-outer weight-gradient products in one launch (include/icap.h icap_gemm_group): items = [(A, B, out, M, N, K,
+    beta), ...] with out[M, N] = A^T B (+ beta out), A [K, M] and B [K, N] bf16 read in place, out fp32; 1 ... 8
+    products, each bitwise what gemm(A, B, out, beta=beta, M=M, N=N, K=K, trans_ab=True, split_k=1, roles=1) gives."""
+    n = len(items)
+    arr = (GemmArgs * n)()
+    for i, (A, B, out, M, N, K, beta) in enumerate(items):
+        a = arr[i]
+        a.trans_ab = 1
+        a.M, a.N, a.K = M, N, K
+        a.in_dtype, a.c_dtype = dtype_code(A.dtype), dtype_code(out.dtype)
+        if B.dtype != A.dtype:
+            raise L.IcapError("gemm_group: A and B must share a dtype")
+        a.A, a.lda = A.data_ptr(), _ld(A)
+        a.B, a.ldb = B.data_ptr(), _ld(B)
+        a.C, a.ldc = out.data_ptr(), _ld(out)
+        a.alpha, a.beta = 1.0, beta
+        a.split_k = 1
+    if GEMM_TIMER is None:
+        call("icap_gemm_group", arr, n, _stream())
+    else:
+        key = ("icap::gemm_group_kernel(icap::GemmGroup)", " + ".join(f"{it[3]}x{it[4]}x{it[5]} kout" for it in items))
+        GEMM_TIMER.launch(key, sum(2.0 * it[3] * it[4] * it[5] for it in items),
+                          lambda: call("icap_gemm_group", arr, n, _stream()))
+
+
 def ln_fold_ok(D: int) -> bool:
     """The LayerNorm-statistics hand-off's shape rule (csrc/gemm.hip gemm_plan): the producer stores (mean, M2) per
     32-column group (N % 32 == 0) and the consumer tile GEMM combines them in its prologue, K % 128 == 0 and

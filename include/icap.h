@@ -178,6 +178,13 @@ const char* icap_gemm_kernel_name(const icap_gemm_args* a);
 /* (tickets) or in a separate reduce pass; ICAP_ERR_ARG on invalid args. Host-only (tests, tools).          */
 int icap_gemm_plan_info(const icap_gemm_args* a, int32_t* splits, int32_t* fused);
 int icap_gemm(const icap_gemm_args* a, void* stream);
+/* Replaces a layer's weight-gradient products of the mapper backward (TORCH/nn/modules/transformer.py:        */
+/* 946-950 linear1 / linear2, TORCH/nn/modules/activation.py in_proj / out_proj via src/train.py:145): a group  */
+/* of n (1 ... 8) K-outer products a[0 .. n-1] (trans_ab, bf16 A / B, fp32 C, alpha / beta, no epilogue        */
+/* operands, no m_dev) in ONE launch, each unsplit on the split-role K-outer kernel (path 11's body): no split-K */
+/* slabs, no reduce pass, the group's tiles filling the chip together. Bitwise what icap_gemm gives each with   */
+/* split_k = 1 and path 11; products with M or N = 0 are skipped.                                              */
+int icap_gemm_group(const icap_gemm_args* a, int32_t n, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* LayerNorm over the last dim D (eps given; GPT-2 ln_1/ln_2/ln_f             */

@@ -48,6 +48,13 @@ def accesses(name, args):
                 ("ln_mean_out", g.ln_mean_out, g.M * 4), ("ln_rstd_out", g.ln_rstd_out, g.M * 4)]
         if g.in_dtype == 2:  # MX block scales (include/icap.h a_scale / b_scale layout)
             out += [("a_scale", g.a_scale, ops.mx_scale_bytes(g.M, g.K)), ("b_scale", g.b_scale, ops.mx_scale_bytes(g.N, g.K))]
+    elif name == "icap_gemm_group":  # n K-outer products (icap_gemm_group): A [K][lda], B [K][ldb], C [M][ldc] fp32
+        arr, n = a[0], a[1]
+        for i in range(n):
+            g = arr[i]
+            ei, ec = ES[g.in_dtype], ES[g.c_dtype]
+            out += [(f"A{i}", g.A, _rows(g.K, g.lda, g.M, ei)), (f"B{i}", g.B, _rows(g.K, g.ldb, g.N, ei)),
+                    (f"C{i}", g.C, _rows(g.M, g.ldc, g.N, ec))]
     elif name in ("icap_attention_fwd", "icap_attention_bwd"):
         t = a[0]._obj
         es = ES[t.dtype]

@@ -197,7 +197,7 @@ def test_serial_mapper_schedule_shares_gradient_buffers():
     with dry_run() as rec:
         icap.weights.ops.call = rec
         model = tiny_model()
-        t = CaptionTrainer(model, 3, 12, num_training_steps=3, dropout=True)
+        t = CaptionTrainer(model, 3, 12, num_training_steps=3, dropout=True, mapper_dw="serial")
         assert isinstance(t.mcore, TransformerMapperCore)
         ws = t.mws
         nl = len(ws.g_dz)
@@ -208,6 +208,25 @@ def test_serial_mapper_schedule_shares_gradient_buffers():
         _assert_clean(rec)
         side = CaptionTrainer(model, 3, 12, num_training_steps=3, dropout=True, mapper_dw="side")
         assert len({b.data_ptr() for b in side.mws.g_dz}) == nl
+
+
+def test_fused_mapper_dw_schedule_in_bounds():
+    """mapper_dw="fused" (round 6): each mapper layer's four weight-gradient products as one icap_gemm_group call at
+    the end of the layer's step, on the shared gradient buffers of the serial schedule (nothing the group reads is
+    rewritten before the layer ends): every product's operands and fp32 output in bounds, one group call per layer."""
+    with dry_run() as rec:
+        icap.weights.ops.call = rec
+        gpt = GPT2LMHeadModel(GPT2Config(n_layer=2))
+        model = ImageCaptioningModel(TransformerMappingNetwork(512, 768, 15, 10, num_layers=2), tokenizer=SimpleNamespace(
+            eos_token_id=50256), gpt=gpt, compute_dtype=torch.bfloat16)
+        t = CaptionTrainer(model, 4, 20, num_training_steps=3, mapper_dw="fused")
+        assert t._group == "fused" and len({b.data_ptr() for b in t.mws.g_dz}) == 1
+        ids, mask, labels, emb = batch(4, 20, vocab=50257, E=512)
+        t.load_batch(ids, mask, labels, emb=emb)
+        t.micro_step()
+        _assert_clean(rec)
+        groups = [c for c in rec.calls if c[0] == "icap_gemm_group"]
+        assert len(groups) == 2 and all(c[1][1] == 4 for c in groups), [c[1][1] for c in groups]
 
 
 def test_gpt2_small_bench_shape_with_clip_in_bounds():

@@ -77,3 +77,35 @@ def test_roles_kout_repeatable(dev):
     torch.cuda.synchronize()
     for i, C in enumerate(outs[1:]):
         _assert_same(f"launch {i + 1}", C, outs[0])
+
+
+def test_gemm_group_matches_single_products(dev):
+    """icap_gemm_group: the mapper layer's four products (and a partial-tile one) in one launch, beta 1 and 0 mixed,
+    bitwise what each gives alone on the unsplit K-outer split-role kernel."""
+    items, refs = [], []
+    for i, (N, K, rows) in enumerate(SHAPES[:5]):
+        dY, X, G = _operands(dev, N, K, 3200 if i < 4 else rows, 20 + i)
+        beta = 0.0 if i == 1 else 1.0
+        C, Cr = G.clone(), G.clone()
+        ops.gemm(dY, X, Cr, beta=beta, M=N, N=K, K=dY.shape[0], trans_ab=True, split_k=1, roles=1)
+        items.append((dY, X, C, N, K, dY.shape[0], beta))
+        refs.append(Cr)
+    ops.gemm_group(items)
+    torch.cuda.synchronize()
+    for i, (it, Cr) in enumerate(zip(items, refs)):
+        _assert_same(f"product {i}", it[2], Cr)
+
+
+def test_gemm_group_rejects_epilogue_operands(dev):
+    from icap import _lib as L
+
+    dY, X, G = _operands(dev, 256, 128, 64, 40)
+    arr = (L.GemmArgs * 1)()
+    a = arr[0]
+    a.trans_ab, a.M, a.N, a.K = 1, 256, 128, 64
+    a.in_dtype, a.c_dtype = L.BF16, L.F32
+    a.A, a.lda, a.B, a.ldb, a.C, a.ldc = dY.data_ptr(), 256, X.data_ptr(), 128, G.data_ptr(), 128
+    a.alpha, a.beta, a.split_k = 1.0, 1.0, 1
+    a.bias = G.data_ptr()
+    with pytest.raises(L.IcapError):
+        ops.call("icap_gemm_group", arr, 1, ops._stream())

@@ -21,10 +21,11 @@ def _batch(seed, dev, B=6, L=14):
 
 
 def _trainer(dev, monkeypatch, group):
+    """group: True / "group" (four streams), "fused" (one grouped launch), False (serial)."""
+    mode = "group" if group is True else group if group else "serial"
     model = build(TINY_G, TINY_M, torch.bfloat16, dev)
-    t = CaptionTrainer(model, 6, 14, lr=1e-3, num_training_steps=8, dropout=True, seed=3,
-                       mapper_dw="group" if group else "serial")
-    assert (t._group is not None) == group
+    t = CaptionTrainer(model, 6, 14, lr=1e-3, num_training_steps=8, dropout=True, seed=3, mapper_dw=mode)
+    assert (t._group is not None) == bool(group)
     return t
 
 
@@ -36,24 +37,33 @@ def _grads(dev, monkeypatch, group):
     return t.flat.flat_grad.clone()
 
 
-def test_grouped_dw_matches_serial(dev, monkeypatch):
-    g1 = _grads(dev, monkeypatch, True)
+@pytest.mark.parametrize("group", [True, "fused"])
+def test_grouped_dw_matches_serial(dev, monkeypatch, group):
+    g1 = _grads(dev, monkeypatch, group)
     g0 = _grads(dev, monkeypatch, False)
     assert torch.isfinite(g1).all()
     err = float((g1.double() - g0.double()).abs().max()) / float(g0.abs().max())
     assert err < 1e-5, err
 
 
-def test_grouped_dw_reproducible(dev, monkeypatch):
-    a = _grads(dev, monkeypatch, True)
-    b = _grads(dev, monkeypatch, True)
+@pytest.mark.parametrize("group", [True, "fused"])
+def test_grouped_dw_reproducible(dev, monkeypatch, group):
+    a = _grads(dev, monkeypatch, group)
+    b = _grads(dev, monkeypatch, group)
     assert torch.equal(a, b)
 
 
-def test_grouped_dw_graph_equals_eager(dev, monkeypatch):
+def test_fused_dw_bitwise_group(dev, monkeypatch):
+    """mapper_dw="fused" (one grouped launch on the K-outer split-role body) and "group" (the K-outer tile kernel on
+    four streams) both run each product unsplit in natural K order: bitwise the same gradients."""
+    assert torch.equal(_grads(dev, monkeypatch, "fused"), _grads(dev, monkeypatch, True))
+
+
+@pytest.mark.parametrize("group", [True, "fused"])
+def test_grouped_dw_graph_equals_eager(dev, monkeypatch, group):
     out = []
     for use_graph in (True, False):
-        t = _trainer(dev, monkeypatch, True)
+        t = _trainer(dev, monkeypatch, group)
         for s in range(3):
             t.load_batch(*_batch(10 + s, dev))
             t.micro_step(use_graph=use_graph)
