@@ -177,8 +177,9 @@ class CaptionTrainer:
             self._group = [torch.cuda.Stream(self.dev) for _ in range(3)]
             for sd in self._group:
                 ops.register_side_stream(sd)
-        # "fused": the four products of a layer in one grouped launch at the end of its step (icap_gemm_group)
-        if mapper_dw == "fused" and isinstance(self.mcore, TransformerMapperCore):
+        # "fused": the four products of a layer in one grouped launch at the end of its step (icap_gemm_group; bf16 —
+        # the fp32 parity mode keeps the serial schedule, whose per-product transposes the group has no form for)
+        if mapper_dw == "fused" and isinstance(self.mcore, TransformerMapperCore) and self.dtype == torch.bfloat16:
             self._group = "fused"
 
     def share_state_with(self, other: "CaptionTrainer") -> None:
