@@ -49,6 +49,8 @@ class DWHelper:
         self.tB = torch.zeros(max_cols * self.Mp_max, dtype=dtype, device=device)
         self.cs_cols = max(max_cols, colsum_cols)
         self.cs_ws = torch.empty(ops.colsum_workspace(max_rows, self.cs_cols), dtype=torch.uint8, device=device)
+        # bf16 ones [rows][8]: the B operand of the bias gradients inside a grouped launch (db = dY^T . 1, dW_group)
+        self.ones = torch.ones((max(max_rows, 1), 8), dtype=dtype, device=device) if dtype == torch.bfloat16 else None
         self.ln_ws = torch.empty(max(ops.layernorm_bwd_workspace(ln_rows, ln_D), 16), dtype=torch.uint8,
                                  device=device)
 
@@ -80,15 +82,24 @@ class DWHelper:
         else:              # out[N,K] (nn.Linear grad layout)
             ops.gemm(a, b, out, beta=beta, M=N, N=K, K=Mp, alg_flops=2.0 * M * N * K)
 
-    def dW_group(self, items, M: int, accumulate: bool = True) -> None:
+    def dW_group(self, items, M: int, accumulate: bool = True, db_items=()) -> bool:
         """dW += dY^T X for every (dY, X, out) of items in one launch (ops.gemm_group: unsplit K-outer products, no
-        slabs or reduce pass) where every operand allows the in-place K-outer read; otherwise one dW() each."""
+        slabs or reduce pass) where every operand allows the in-place K-outer read; otherwise one dW() each.
+        db_items: (dY, db) bias gradients db += dY^T . 1 taken into the same launch as K-outer products against a
+        ones column (fp32 MFMA sums over the rows instead of icap_colsum_batch: no launches of their own, and their
+        tiles fill the CUs the dW tiles leave idle in the launch's last round). Returns whether db_items were done."""
+        beta = 1.0 if accumulate else 0.0
         if self.dtype == torch.bfloat16 and all(_kout_ok(dy) and _kout_ok(x) for dy, x, _ in items):
-            beta = 1.0 if accumulate else 0.0
-            ops.gemm_group([(dy, x, out, dy.shape[1], x.shape[1], M, beta) for dy, x, out in items])
-            return
+            group = [(dy, x, out, dy.shape[1], x.shape[1], M, beta) for dy, x, out in items]
+            took_db = (self.ones is not None and M <= self.ones.shape[0] and len(group) + len(db_items) <= 8
+                       and all(_kout_ok(dy) and out.is_contiguous() for dy, out in db_items))
+            if took_db:
+                group += [(dy, self.ones, out.view(-1, 1), dy.shape[1], 1, M, beta) for dy, out in db_items]
+            ops.gemm_group(group)
+            return took_db
         for dy, x, out in items:
             self.dW(dy, x, out, M=M, accumulate=accumulate)
+        return False
 
     def db(self, dY: Tensor, out: Tensor, M: int, N: Optional[int] = None, accumulate: bool = True) -> None:
         ops.colsum(dY, out, self.cs_ws, accumulate=accumulate, M=M, N=N)
@@ -482,7 +493,8 @@ class TransformerMapperCore:
             if not st.dw:
                 return
             if group == "fused":
-                dwh.dW_group(st.dw, M, accumulate=acc)
+                if dwh.dW_group(st.dw, M, accumulate=acc, db_items=st.db):
+                    st.db = []  # (the bias gradients went into the same launch)
                 st.dw = []
                 return
             main = torch.cuda.current_stream()

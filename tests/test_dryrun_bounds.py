@@ -211,8 +211,8 @@ def test_serial_mapper_schedule_shares_gradient_buffers():
 
 
 def test_fused_mapper_dw_schedule_in_bounds():
-    """mapper_dw="fused" (round 6): each mapper layer's four weight-gradient products as one icap_gemm_group call at
-    the end of the layer's step, on the shared gradient buffers of the serial schedule (nothing the group reads is
+    """mapper_dw="fused" (round 6): each mapper layer's four weight-gradient products and four bias gradients as one
+    icap_gemm_group call at the end of the layer's step, on the shared gradient buffers of the serial schedule (nothing the group reads is
     rewritten before the layer ends): every product's operands and fp32 output in bounds, one group call per layer."""
     with dry_run() as rec:
         icap.weights.ops.call = rec
@@ -226,7 +226,9 @@ def test_fused_mapper_dw_schedule_in_bounds():
         t.micro_step()
         _assert_clean(rec)
         groups = [c for c in rec.calls if c[0] == "icap_gemm_group"]
-        assert len(groups) == 2 and all(c[1][1] == 4 for c in groups), [c[1][1] for c in groups]
+        # four weight products + the four bias gradients (ones-column products) per layer
+        assert len(groups) == 2 and all(c[1][1] == 8 for c in groups), [c[1][1] for c in groups]
+        assert not [c for c in rec.calls if c[0] == "icap_colsum_batch"], "bias gradients outside the group"
 
 
 def test_gpt2_small_bench_shape_with_clip_in_bounds():

@@ -109,3 +109,23 @@ def test_gemm_group_rejects_epilogue_operands(dev):
     a.bias = G.data_ptr()
     with pytest.raises(L.IcapError):
         ops.call("icap_gemm_group", arr, 1, ops._stream())
+
+
+def test_gemm_group_bias_gradient_ones_column(dev):
+    """The bias gradients of the fused mapper schedule: db[N] (+)= dY[rows, N]^T . ones[rows] as K-outer products
+    against a ones column (N = 1, ldb = 8, C viewed [N, 1]) in the same launch as a weight product; equal to the fp64
+    column sums to fp32 accumulation order (rel 1e-5 of sum |dY|)."""
+    rows = 3200
+    ones = torch.ones((rows, 8), device=dev, dtype=torch.bfloat16)
+    dY, X, G = _operands(dev, 2304, 768, rows, 50)
+    dY2 = rnd((rows, 768), dev, scale=0.3, seed=55)
+    db1 = rnd((2304,), dev, torch.float32, 1.0, seed=56)
+    db2 = torch.zeros(768, device=dev)
+    r1 = db1.double() + dY.double().sum(0)
+    r2 = dY2.double().sum(0)
+    ops.gemm_group([(dY, X, G, 2304, 768, rows, 1.0), (dY, ones, db1.view(-1, 1), 2304, 1, rows, 1.0),
+                    (dY2, ones, db2.view(-1, 1), 768, 1, rows, 0.0)])
+    torch.cuda.synchronize()
+    for got, ref, src in ((db1, r1, dY), (db2, r2, dY2)):
+        err = ((got.double() - ref).abs() / (src.double().abs().sum(0) + 1e-30)).max().item()
+        assert err < 1e-5, err

@@ -53,10 +53,15 @@ def test_grouped_dw_reproducible(dev, monkeypatch, group):
     assert torch.equal(a, b)
 
 
-def test_fused_dw_bitwise_group(dev, monkeypatch):
-    """mapper_dw="fused" (one grouped launch on the K-outer split-role body) and "group" (the K-outer tile kernel on
-    four streams) both run each product unsplit in natural K order: bitwise the same gradients."""
-    assert torch.equal(_grads(dev, monkeypatch, "fused"), _grads(dev, monkeypatch, True))
+def test_fused_dw_matches_group(dev, monkeypatch):
+    """mapper_dw="fused" (one grouped launch on the K-outer split-role body, the bias gradients as products against a
+    ones column in the same launch) and "group" (the K-outer tile kernel on four streams + column sums) run each
+    weight product unsplit in natural K order — bitwise the same weight gradients — and sum the bias gradients in
+    different orders (fp32): equal to rel 1e-6 of the largest entry."""
+    a, b = _grads(dev, monkeypatch, "fused"), _grads(dev, monkeypatch, True)
+    err = float((a.double() - b.double()).abs().max()) / float(b.abs().max())
+    assert err < 1e-6, err
+    assert float((a == b).float().mean()) > 0.9  # the weight gradients (most of the buffer) bitwise
 
 
 @pytest.mark.parametrize("group", [True, "fused"])
