@@ -462,7 +462,7 @@ static int roles_actk(const icap_gemm_args& p, int v) {
   const int fa = p.dact == ICAP_ACT_NONE ? p.act : -1, ba = p.act == ICAP_ACT_NONE ? p.dact : -1;
   int a;
   if (p.act == ICAP_ACT_NONE && p.dact == ICAP_ACT_NONE) a = ACT_OFF;
-  else if (v == 27) a = ACT_ANY;
+  else if (v == 27 || v == 32) a = ACT_ANY;
   else if (fa == ICAP_ACT_GELU_NEW) a = ACT_FWD + ICAP_ACT_GELU_NEW;
   else if (ba == ICAP_ACT_GELU_NEW) a = ACT_BWD + ICAP_ACT_GELU_NEW;
   else if (fa == ICAP_ACT_QUICK_GELU) a = ACT_FWD + ICAP_ACT_QUICK_GELU;
@@ -472,7 +472,7 @@ static int roles_actk(const icap_gemm_args& p, int v) {
   if (p.c_dtype != ICAP_BF16) return (p.ln_stats_out || p.ln_stats_in) ? -1 : (a == ACT_OFF ? ACT_OFF : ACT_ANY);
   if (p.ln_stats_out) return a == ACT_OFF ? ACT_LNS : -1;
   if (p.ln_stats_in) {
-    if (v == 27) return -1;
+    if (v == 27 || v == 32) return -1;
     return (a == ACT_OFF || a == ACT_FWD + ICAP_ACT_GELU_NEW || a == ACT_FWD + ICAP_ACT_QUICK_GELU) ? ACT_LNF + a : -1;
   }
   return a;
@@ -500,7 +500,7 @@ static int g256_mode() {
 // head 8320 x 50304 x 768: 758 vs 835 us), not on the train step's 2-round K = 768 products (8320 x 3072 x 768:
 // 84 vs 80 us) (profiles/r02_gemm256_bench.txt). path 3 forces it where eligible.
 static bool g256_pick(const icap_gemm_args& p) {
-  if (p.path == 1 || (p.path >= 4 && p.path <= 11)) return false;
+  if (p.path == 1 || (p.path >= 4 && p.path <= 12)) return false;
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.ln_gamma || p.beta != 0.f || p.m_dev || p.split_k > 1) return false;
   if (p.ln_stats_out || p.ln_stats_in) return false;
   if (p.M < 256 || p.N < 256 || p.K < 64) return false;
@@ -565,6 +565,10 @@ static int roles_pick(const icap_gemm_args& p, int64_t m_plan, int64_t nk, int64
   if (p.in_dtype != ICAP_BF16 || p.trans_ab || p.split_k > 1) return 0;
   if (p.N <= 1024) {
     const int64_t t = ((m_plan + 95) / 96) * ((p.N + 127) / 128);
+    // more than one round of 96 x 128 tiles, one of 160 x 128 at least 80 % full: 160 x 128 (CLIP-B/32's 6400 x 768
+    // out_proj / fc2 with the LayerNorm statistics: 240 tiles against 402, profiles/r06_roles160_ab.txt)
+    const int64_t t160 = ((m_plan + 159) / 160) * ((p.N + 127) / 128);
+    if (nk <= 96 && t > cus && t160 <= cus && t160 * 10 >= cus * 8) return 32;
     if (nk > 96 || t * 5 < cus * 3) return 0;
     return (t <= cus || (nk >= 32 && 2 * t >= 3 * cus && t <= 2 * cus)) ? 27 : 0;
   }
@@ -574,7 +578,7 @@ static int roles_pick(const icap_gemm_args& p, int64_t m_plan, int64_t nk, int64
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   ICAP_REQUIRE(p.M >= 0 && p.N >= 0 && p.K >= 0, "icap_gemm: negative size");
-  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 11), "icap_gemm: path must be 0, 1 or 3 ... 11");
+  ICAP_REQUIRE(p.path == 0 || p.path == 1 || (p.path >= 3 && p.path <= 12), "icap_gemm: path must be 0, 1 or 3 ... 12");
   ICAP_REQUIRE(p.A && p.B && p.C, "icap_gemm: null operand");
   ICAP_REQUIRE(p.in_dtype == ICAP_F32 || p.in_dtype == ICAP_BF16 || p.in_dtype == ICAP_FP8_MX,
                "icap_gemm: bad in_dtype");
@@ -845,9 +849,9 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
   // variants 26 / 27: the split-role ring (gemm_tile.h ROLES) on 128 x 256 / 96 x 128 tiles, one K range per tile
   // (path 8 / 9 force them where eligible; the automatic rule: roles_pick)
   {
-    const int rv = p.path == 8 ? 26 : p.path == 9 ? 27 : p.path == 10 ? 28
+    const int rv = p.path == 8 ? 26 : p.path == 9 ? 27 : p.path == 10 ? 28 : p.path == 12 ? 32
                    : (p.path == 0 && roles_mode() != 0) ? roles_pick(p, m_plan, nk, cus) : 0;
-    const int bm = rv == 26 ? 128 : rv == 27 ? 96 : 192, bn = rv == 27 ? 128 : 256;
+    const int bm = rv == 26 ? 128 : rv == 27 ? 96 : rv == 32 ? 160 : 192, bn = (rv == 27 || rv == 32) ? 128 : 256;
     if (rv && p.M >= bm && p.split_k <= 1) {
       if (const int ar = roles_actk(p, rv); ar >= 0) {
         pl.variant = rv;
@@ -969,6 +973,7 @@ static const char* variant_kernel(int v) {
     case 27: return "gemm_kernel<%s, %s, 5, 1, 2, 2, 3, 4, false, %d, true>";
     case 28: return "gemm_kernel<%s, %s, 2, 1, 2, 4, 6, 4, false, %d, true>";
     case 31: return "gemm_kernel<%s, %s, 4, 1, 2, 2, 4, 4, true, %d, true>";
+    case 32: return "gemm_kernel<%s, %s, 4, 1, 2, 2, 5, 4, false, %d, true>";
     default: return "gemm_kernel<%s, %s, 1, 3, 2, 2, 4, 4, true, %d>";
   }
 }
@@ -1101,11 +1106,12 @@ extern "C" int icap_gemm(const icap_gemm_args* a, void* stream) {
   const int sp = pl.splits;
   // (the split-role variants walk K in its natural order: one round of tiles, no lockstep panel misses to stagger,
   // and automatic launches then equal forced ones and the tile path bitwise)
-  const int skew = (pl.variant >= 26 && pl.variant <= 31) ? 0 : kskew_for(p, pl.nk_split);
+  const int skew = (pl.variant >= 26 && pl.variant <= 32) ? 0 : kskew_for(p, pl.nk_split);
   const int nks = pl.nk_split | (skew << 20) | (gemm_diag() << 28) | (gemm_acquire() << 30);
   const dim3 rgrid((unsigned)((p.M * (p.N / 4) + 255) / 256));
   if (pl.variant == 31) launch_tile_roles_kout(pl, p, nks, s);                       // gemm_tile_roles_kout.hip
   else if (pl.variant == 26) launch_tile_roles(pl, p, nks, s);                       // gemm_tile_roles.hip
+  else if (pl.variant == 32) launch_tile_roles160(pl, p, nks, s);                    // gemm_tile_roles160.hip
   else if (pl.variant == 27) launch_tile_roles96(pl, p, nks, s);                     // gemm_tile_roles96.hip
   else if (pl.variant == 28) launch_tile_roles192(pl, p, nks, s);                    // gemm_tile_roles192.hip
   else if (pl.variant == 22) launch_tile_r256(pl, p, nks, s);                        // gemm_tile_r256.hip

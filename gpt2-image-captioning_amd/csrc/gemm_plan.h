@@ -33,6 +33,7 @@ void launch_tile_roles(const GemmPlan& pl, const icap_gemm_args& p, int nks, hip
 void launch_tile_roles96(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);  // roles 96 x 128 (27)
 void launch_tile_roles192(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s); // roles 192 x 256 (28)
 void launch_tile_roles_kout(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s); // roles K-outer (31)
+void launch_tile_roles160(const GemmPlan& pl, const icap_gemm_args& p, int nks, hipStream_t s);  // roles 160 x 128 (32)
 // a group of K-outer weight-gradient products run in one launch (icap_gemm_group)
 constexpr int ICAP_GEMM_GROUP_MAX = 8;
 struct GemmGroup {

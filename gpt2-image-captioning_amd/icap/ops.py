@@ -173,7 +173,8 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     22) wherever eligible, unsplit (A/B measurements, path-equality tests); w192: 192 x 64 tiles (variant 24)
     wherever eligible, unsplit (same use); roles = 256 / 96 / 192: the split-role ring kernel on 128 x 256 (variant
     26) / 96 x 128 (variant 27) / 192 x 256 (variant 28) tiles wherever eligible, unsplit (same use); roles = 1 with
-    trans_ab: the K-outer split-role kernel (variant 31, 128 x 128 tiles; split_k 0 = its own split rule).
+    trans_ab: the K-outer split-role kernel (variant 31, 128 x 128 tiles; split_k 0 = its own split rule); roles = 160:
+    160 x 128 tiles (variant 32).
     ln_stats_out: fp32 [M, N/32, 2] — this (producer) launch also writes (mean, M2) of each row's 32-column groups of
     the stored C; ln_stats_in (with ln_fold = (wsum, eps)): the LayerNorm of A folded into the epilogue from the
     producer's statistics (tile kernels, any M); ln_rows_out: (mean, rstd) fp32 [M] of that LayerNorm (for its
@@ -228,7 +229,7 @@ def gemm(A: Tensor, B: Tensor, out: Tensor, *, bias: Optional[Tensor] = None, ac
     a.m_hint = int(m_hint) if (m_hint is not None and m_dev is not None) else 0
     a.path = (1 if tile_only else 3 if g256 else 4 if g8p == 128 else 5 if g8p == 256 else 6 if r256 else
               7 if w192 else 8 if roles == 256 else 9 if roles == 96 else 10 if roles == 192 else
-              11 if roles == 1 else 0)
+              11 if roles == 1 else 12 if roles == 160 else 0)
     if ln is not None:
         a.ln_gamma, a.ln_beta, a.ln_eps = ln[0].data_ptr(), ln[1].data_ptr(), float(ln[2])
     if ln_fold is not None:

@@ -121,7 +121,8 @@ typedef struct {
   /*     one block per CU: csrc/gemm_tile.h ROLES) on 128 x 256 (variant 26) / 96 x 128 (variant 27) /          */
   /*     192 x 256 (variant 28) tiles for unsplit bf16 row-major launches without ln_gamma (9: no LayerNorm     */
   /*     consumer) — same use; 11 = the K-outer split-role kernel (variant 31, 128 x 128 tiles) for bf16        */
-  /*     trans_ab launches, K split over slabs by its own rule unless split_k is given — same use.              */
+  /*     trans_ab launches, K split over slabs by its own rule unless split_k is given — same use; 12 = the     */
+  /*     split-role ring on 160 x 128 tiles (variant 32, no LayerNorm consumer) — same use.                     */
   int32_t path;
   /* in_dtype == ICAP_FP8_MX: the E8M0 block scales of A (M rows) and B (N rows), K % 128 == 0, lda / ldb      */
   /* multiples of 16, 16-byte aligned. For a 128-element K stage s and 64-row group g, 256 bytes at offset      */

@@ -1,5 +1,6 @@
 """The split-role ring kernels (round 6: gemm_kernel<..., ROLES = true>, csrc/gemm_tile.h; variant 26 = 128 x 256 tiles,
-csrc/gemm_tile_roles.hip; variant 27 = 96 x 128 tiles, csrc/gemm_tile_roles96.hip) against the 128-row tile kernels
+csrc/gemm_tile_roles.hip; variant 27 = 96 x 128 tiles, csrc/gemm_tile_roles96.hip; variant 32 = 160 x 128 tiles,
+csrc/gemm_tile_roles160.hip) against the 128-row tile kernels
 and fp64.
 
 Four MFMA waves read fragments and issue the MFMAs, four loader waves issue the LDS-DMA of the ring; the MFMA chain per
@@ -20,7 +21,7 @@ from gemm_helpers import _assert_same, _run, rnd
 
 pytestmark = pytest.mark.gpu
 
-R256, R96, R192 = "3, 1, 2, 2, 4, 8", "5, 1, 2, 2, 3, 4", "2, 1, 2, 4, 6, 4"
+R256, R96, R192, R160 = "3, 1, 2, 2, 4, 8", "5, 1, 2, 2, 3, 4", "2, 1, 2, 4, 6, 4", "4, 1, 2, 2, 5, 4"
 
 SHAPES = [  # (M, N, K, roles)
     (3584, 2304, 768, 256),  # GPT-2 c_attn at the packed rows
@@ -37,11 +38,15 @@ SHAPES = [  # (M, N, K, roles)
     (1000, 520, 200, 192),
     (384, 256, 64, 192),
     (3200, 3072, 768, 192),  # the mapper's linear1
+    (6400, 768, 768, 160),   # CLIP-B/32 out_proj on 160 x 128 tiles (variant 32)
+    (6400, 768, 3072, 160),  # CLIP-B/32 fc2
+    (1000, 520, 200, 160),
+    (200, 130, 128, 160),
 ]
 
 
 def _name(tc, act, roles):
-    form = {256: R256, 96: R96, 192: R192}[roles]
+    form = {256: R256, 96: R96, 192: R192, 160: R160}[roles]
     return f"icap::gemm_kernel<unsigned short, {tc}, {form}, false, {act}, true>"
 
 
@@ -79,7 +84,8 @@ def test_roles_repeatable(dev):
 
 
 @pytest.mark.parametrize("M,N,K,roles", [(3584, 2304, 768, 256), (1000, 520, 200, 256), (3584, 768, 768, 96),
-                                         (1000, 520, 200, 96), (3584, 3072, 768, 192), (1000, 520, 200, 192)])
+                                         (1000, 520, 200, 96), (3584, 3072, 768, 192), (1000, 520, 200, 192),
+                                         (6400, 768, 768, 160), (1000, 520, 200, 160)])
 def test_roles_epilogues_match_tile(dev, M, N, K, roles):
     A = rnd((M, K), dev, scale=0.1, seed=6)
     B = rnd((N, K), dev, scale=0.1, seed=7)
@@ -104,7 +110,7 @@ def test_roles_epilogues_match_tile(dev, M, N, K, roles):
         _assert_same(name, a, b)
 
 
-@pytest.mark.parametrize("roles,N", [(256, 2304), (96, 768), (192, 3072)])
+@pytest.mark.parametrize("roles,N", [(256, 2304), (96, 768), (192, 3072), (160, 768)])
 def test_roles_device_row_count(dev, roles, N):
     """m_dev: rows past the device count are neither computed nor stored; the rest equal the tile path's."""
     M, live, K = 8320, 3584, 768
@@ -121,7 +127,7 @@ def test_roles_device_row_count(dev, roles, N):
     assert bool((C[live:] == 3.0).all())
 
 
-@pytest.mark.parametrize("roles", [256, 96, 192])
+@pytest.mark.parametrize("roles", [256, 96, 192, 160])
 def test_roles_layernorm_stats_producer_matches_tile(dev, roles):
     """C and its (mean, M2) per row and 32-column group equal the tile kernel's (the GPT-2 attn c_proj form: bias +
     residual + dropout + statistics, device row count)."""
@@ -180,7 +186,7 @@ def test_roles_layernorm_consumer_matches_tile(dev, N, act, roles):
         _assert_same(name, a[:live], b[:live])
 
 
-@pytest.mark.parametrize("roles", [256, 96, 192])
+@pytest.mark.parametrize("roles", [256, 96, 192, 160])
 def test_roles_f32_output_matches_tile(dev, roles):
     M, N, K = 2048, 1024, 320
     A = rnd((M, K), dev, seed=11)

@@ -1,5 +1,5 @@
 """Round 6: the split-role ring kernels (variant 26 = 128 x 256 tiles, ops.gemm(roles=256); variant 27 = 96 x 128,
-roles=96; variant 28 = 192 x 256 with 8 MFMA waves, roles=192) against the automatic plan and hipBLASLt (torch.mm, plain products only) on the train step's products,
+roles=96; variant 28 = 192 x 256 with 8 MFMA waves, roles=192; variant 32 = 160 x 128, roles=160) against the automatic plan and hipBLASLt (torch.mm, plain products only) on the train step's products,
 with the epilogue each one has in the step. Each form is captured as 20 back-to-back launches in a HIP graph and
 replayed 7 times (best per-launch us). '!' = not allclose to auto. Usage: python tools/ab/roles_ab.py [skew]
 (skew: also the roles forms with K-skew 1, ICAP_ROLES_SKEW, read only by the diagnostic build)."""
@@ -89,7 +89,7 @@ def main():
     skew = len(sys.argv) > 1 and sys.argv[1] == "skew"
     g = torch.Generator(device="cpu").manual_seed(0)
     forms = [("auto", {}, {}), ("r256", {}, dict(roles=256)), ("r96", {}, dict(roles=96)),
-             ("r192", {}, dict(roles=192))]
+             ("r192", {}, dict(roles=192)), ("r160", {}, dict(roles=160))]
     if skew:
         forms += [("r256s", {"ICAP_ROLES_SKEW": "1"}, dict(roles=256)), ("r96s", {"ICAP_ROLES_SKEW": "1"},
                                                                          dict(roles=96))]
