@@ -852,18 +852,32 @@ static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {
     const int rv = p.path == 8 ? 26 : p.path == 9 ? 27 : p.path == 10 ? 28 : p.path == 12 ? 32
                    : (p.path == 0 && roles_mode() != 0) ? roles_pick(p, m_plan, nk, cus) : 0;
     const int bm = rv == 26 ? 128 : rv == 27 ? 96 : rv == 32 ? 160 : 192, bn = (rv == 27 || rv == 32) ? 128 : 256;
-    if (rv && p.M >= bm && p.split_k <= 1) {
+    // a caller's split_k > 1 (the long-K LM head dX): K ranges over fp32 slabs + the reduce pass, as the tile path
+    // (no LayerNorm hand-off: it needs the whole epilogue in the kernel)
+    const bool rsplit = p.split_k > 1 && !lnx && rv != 28;
+    if (rv && p.M >= bm && (p.split_k <= 1 || rsplit)) {
       if (const int ar = roles_actk(p, rv); ar >= 0) {
+        int64_t rs = 1;
+        if (rsplit) {
+          rs = p.split_k < nk ? p.split_k : nk;
+          rs = (nk + (nk + rs - 1) / rs - 1) / ((nk + rs - 1) / rs);  // every split gets >= 1 stage
+        }
+        if (rs > 1) {
+          ICAP_REQUIRE((p.N & 3) == 0, "icap_gemm: split-K requires N % 4 == 0");
+          ICAP_REQUIRE(p.workspace && (reinterpret_cast<uintptr_t>(p.workspace) & 15) == 0 &&
+                           p.workspace_bytes >= rs * p.M * p.N * (int64_t)sizeof(float),
+                       "icap_gemm: split-K workspace missing, misaligned or too small");
+        }
         pl.variant = rv;
-        pl.splits = 1;
+        pl.splits = (int)rs;
         pl.fused = false;
-        pl.nk_split = (int)nk;
+        pl.nk_split = (int)((nk + rs - 1) / rs);
         tiles_n = (p.N + bn - 1) / bn;
         tiles = ((p.M + bm - 1) / bm) * tiles_n;
         pl.tiles_n = (int)tiles_n;
         pl.actk = ar;
         pl.block = dim3(rv == 28 ? 3 * GNT : 2 * GNT);  // 12 / 8 waves
-        pl.grid = dim3((unsigned)(tiles < cus ? tiles : cus));  // the kernel walks the live tiles
+        pl.grid = dim3((unsigned)(tiles * rs < cus ? tiles * rs : cus));  // the kernel walks the live tiles
         return ICAP_OK;
       }
     }

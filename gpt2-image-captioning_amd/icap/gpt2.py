@@ -36,6 +36,19 @@ TRAIN_LN_FOLD = True
 Tensor = torch.Tensor
 
 
+_CUS = {}
+
+
+def _device_cus(dev) -> int:
+    """Compute units of the device (the split rule of the LM head dX)."""
+    if dev.type != "cuda" or not torch.cuda.is_available():
+        return 256  # (the CPU dry run of the schedules: MI355X's count)
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _CUS:
+        _CUS[i] = int(torch.cuda.get_device_properties(i).multi_processor_count)
+    return _CUS[i]
+
+
 @dataclass
 class GPT2Config:  # HF/models/gpt2/configuration_gpt2.py:84-103
     vocab_size: int = 50257
@@ -579,12 +592,18 @@ class GPT2Core:
             raise L.IcapError("compact LM head: the tied wte gradient needs every row (alloc_train(keep_for_dw))")
         rows = ws.head_rows_hint if (cp and ws.head_rows_hint is not None) else ws.Mh
         # dh_f = dlogits . wte (K padded); compact: target rows only, scattered back by the ln_f backward
-        split = 0
+        split, rkw = 0, {}
         if cp and rows > 128:  # long K (50304), few output tiles: split K so ~2 blocks/CU work on the live rows
             tiles = -(-rows // 128) * -(-D // 128)
             split = max(1, min(16, round(512 / max(tiles, 1))))
+            if dlogits.dtype == torch.bfloat16 and ws.qdl is None:
+                # bf16: the 128 x 256 split-role ring, tiles x splits in one round of the CUs (1664 rows: 39 tiles x
+                # 6 splits; 127 vs 147 us for the tile kernel at its split, profiles/r06_lmhead_dx_ab.txt)
+                t256 = -(-rows // 128) * -(-D // 256)
+                split = max(1, min(16, _device_cus(dlogits.device) // max(t256, 1)))
+                rkw = dict(roles=256)
         self._mm(dlogits, ws.qdl, self.wte_t, getattr(self, "qwte_t", None), ws.dhf, rows_dev=ws.n_valid if cp else None,
-                 M=ws.Mh, m_dev=ws.n_valid if cp else None, alg_flops=2.0 * rows * D * self.V, split_k=split)
+                 M=ws.Mh, m_dev=ws.n_valid if cp else None, alg_flops=2.0 * rows * D * self.V, split_k=split, **rkw)
         if grads is not None:  # d(wte) from the tied LM head: dW[V,D] += dlogits^T . hf
             dw.dW(dlogits, ws.hf, grads.wte, M=M, N=self.V)
         rd, seqs = ws.m_live, ws.seqs  # packed rows (None: every row)

@@ -198,3 +198,24 @@ def test_roles_f32_output_matches_tile(dev, roles):
     ops.gemm(A, B, Ct, split_k=1, tile_only=True)
     torch.cuda.synchronize()
     _assert_same("C", C, Ct)
+
+
+@pytest.mark.parametrize("roles,split", [(96, 3), (256, 4), (160, 2)])
+def test_roles_split_k_matches_tile(dev, roles, split):
+    """A caller's split_k > 1 on the split-role rings (the long-K LM head dX): each split's K range on the ring, fp32
+    slabs, the same reduce pass — bitwise the tile kernel at the same split (device row count, K tail, partial tiles)."""
+    M, N, K, live = 1000, 776, 8192 + 40, 931
+    A = rnd((M, K), dev, scale=0.1, seed=21)
+    B = rnd((N, K), dev, scale=0.1, seed=22)
+    md = torch.tensor([live], dtype=torch.int32, device=dev)
+    ws = torch.empty(split * M * N, device=dev, dtype=torch.float32)
+    C = torch.full((M, N), 3.0, device=dev, dtype=torch.bfloat16)
+    Ct = C.clone()
+    names = _run(lambda: ops.gemm(A, B, C, m_dev=md, m_hint=live, split_k=split, roles=roles, workspace=ws))
+    assert names == [_name("unsigned short", 0, roles)], names
+    ops.gemm(A, B, Ct, m_dev=md, m_hint=live, split_k=split, tile_only=True, workspace=ws)
+    torch.cuda.synchronize()
+    _assert_same("C", C[:live], Ct[:live])
+    ref = A[:live].double() @ B.double().t()
+    err = ((C[:live].double() - ref).abs() / (A[:live].double().abs() @ B.double().abs().t())).max().item()
+    assert err < 1e-2, err
