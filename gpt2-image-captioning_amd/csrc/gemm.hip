@@ -33,6 +33,19 @@ __device__ __forceinline__ uint4 ln_chunk<float>(const uint4 a, float mean, floa
                     __float_as_uint((__uint_as_float(a.w) - mean) * rs * g[3] + bt[3]));
 }
 
+// v + the same register of lane ^ 16 / lane ^ 32 on the VALU's cross-lane paths (v_permlane16_swap /
+// v_permlane32_swap; the bits equal v + __shfl_xor(v, 16 / 32), whose ds_bpermute is an LDS round trip each)
+__device__ __forceinline__ float xor16_sum(float v) {
+  const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                   false, false);
+  return __builtin_bit_cast(float, (unsigned)sw[0]) + __builtin_bit_cast(float, (unsigned)sw[1]);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v),
+                                                   false, false);
+  return __builtin_bit_cast(float, (unsigned)sw[0]) + __builtin_bit_cast(float, (unsigned)sw[1]);
+}
+
 constexpr int SK_WAVES = 8;
 constexpr int SK_LNK = 1280;  // LN-fused launches up to this K stage gamma / beta in LDS
 // NT: 16-column slabs per block (the host picks the fewest that fit the grid in one pass over the CUs);
@@ -108,6 +121,16 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   __builtin_amdgcn_sched_barrier(0);
   // every wave runs at least one (possibly all-zero) pass, so the LN-stats barrier below is block-uniform
   load_steps(wave);
+  // LayerNorm statistics from the fragments (below): each row's first element, issued with the fragment loads
+  // (instantiations with few fragment registers only: the others would spill; LN-fused launches have K = D)
+  constexpr bool LN_FRAG = ES == 2 && SKU * (MT + NT) <= 24;
+  const bool fold = p.ln_wsum != nullptr;
+  const bool ln_frag = LN_FRAG && (fuse_ln || fold) && nks <= (int64_t)SK_WAVES * SKU;
+  uint4 x0raw[MT];
+  if (LN_FRAG && ln_frag) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) x0raw[i] = bload(ra, (uint32_t)((i * 16 + fr) * p.lda * ES));  // rows past M: zero
+  }
   __builtin_amdgcn_sched_barrier(0);
   if (ln_lds) {
 #pragma unroll
@@ -126,13 +149,22 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   const int64_t erow = m0 + er, ecol = n0 + ec;
   const bool eact = threadIdx.x < BM * QPR && erow < M && ecol < N;
   float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  float wsum4[4] = {0.f, 0.f, 0.f, 0.f};  // (folded LayerNorm: W row sums, fetched here, not after the reduction)
   uint2 pre = make_uint2(0u, 0u);
   bool use_pre = false;
   if (eact) {
-    if (p.bias && p.dact == ICAP_ACT_NONE) {
+    // one 16-byte load per operand for a full, aligned quad (the bias / wsum vectors of the decode launches)
+    auto quad = [&](const float* v, float* dst) {
+      if (ecol + 4 <= N && (reinterpret_cast<uintptr_t>(v + ecol) & 15) == 0) {
+        const float4 q = *reinterpret_cast<const float4*>(v + ecol);
+        dst[0] = q.x; dst[1] = q.y; dst[2] = q.z; dst[3] = q.w;
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bias4[e] = (ecol + e < N) ? p.bias[ecol + e] : 0.f;
-    }
+        for (int e = 0; e < 4; ++e) dst[e] = (ecol + e < N) ? v[ecol + e] : 0.f;
+      }
+    };
+    if (p.bias && p.dact == ICAP_ACT_NONE) quad(p.bias, bias4);
+    if (p.ln_wsum) quad(p.ln_wsum, wsum4);
     if constexpr (sizeof(TC) == 2) {
       const bf16_t* src = reinterpret_cast<const bf16_t*>(p.dact != ICAP_ACT_NONE ? p.dact_src : p.resid);
       const int64_t lds_ = p.dact != ICAP_ACT_NONE ? p.ld_dact : p.ldr;
@@ -152,24 +184,21 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
   __shared__ float ln_mr[BM][2];
   __shared__ float lnp[SK_WAVES][BM];
   __shared__ float lnp2[SK_WAVES][BM];
-  // (instantiations with few fragment registers only: the others would spill; LN-fused launches have K = D)
-  constexpr bool LN_FRAG = ES == 2 && SKU * (MT + NT) <= 24;
   // folded LayerNorm (icap_gemm_args.ln_wsum): the same row statistics, but only the epilogue needs them
   // (C = rstd (A.B^T - mean wsum) + bias), so the MFMAs run on the raw fragments without waiting for them: the
-  // wave partials go to LDS here and are summed by the epilogue threads after the partial-tile reduction barrier
-  const bool fold = p.ln_wsum != nullptr;
-  const bool ln_frag = LN_FRAG && (fuse_ln || fold) && nks <= (int64_t)SK_WAVES * SKU;
+  // wave partials are computed after the MFMAs are issued (the VALU pass overlaps the matrix cores), go to LDS and
+  // are summed by the epilogue threads after the partial-tile reduction barrier
   float ln_mean[MT], ln_rs[MT];
-  if (LN_FRAG && ln_frag) {
-    // one pass over the fragments: per-row sums of (x - x0) and (x - x0)^2 with x0 the row's first element (the
-    // shifted-data form: no cancellation between E[x^2] and mean^2 when |mean| >> std), reduced together (lane
-    // groups by shuffles, the 8 waves through LDS in a fixed order); mean = x0 + E[d], var = E[d^2] - E[d]^2
+  // one pass over the fragments: per-row sums of (x - x0) and (x - x0)^2 with x0 the row's first element (the
+  // shifted-data form: no cancellation between E[x^2] and mean^2 when |mean| >> std), reduced together (lane
+  // groups by shuffles, the 8 waves through LDS in a fixed order); mean = x0 + E[d], var = E[d^2] - E[d]^2
+  auto frag_stats = [&]() {
     auto chunk_in = [&](int u) { return (int64_t)(wave + u * SK_WAVES) * KSTEP + fg * EPC < K; };
     float part[MT], part2[MT], x0[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       float v0[8];
-      unpack_bf16(bload(ra, (uint32_t)((i * 16 + fr) * p.lda * ES)), v0);  // rows past M: zero
+      unpack_bf16(x0raw[i], v0);
       x0[i] = v0[0];
       part[i] = 0.f;
       part2[i] = 0.f;
@@ -187,17 +216,18 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
           }
         }
       }
-      part[i] += __shfl_xor(part[i], 16, 64);
-      part[i] += __shfl_xor(part[i], 32, 64);
-      part2[i] += __shfl_xor(part2[i], 16, 64);
-      part2[i] += __shfl_xor(part2[i], 32, 64);
+      part[i] = xor32_sum(xor16_sum(part[i]));
+      part2[i] = xor32_sum(xor16_sum(part2[i]));
       if (fg == 0) {
         lnp[wave][i * 16 + fr] = part[i];
         lnp2[wave][i * 16 + fr] = part2[i];
         if (fold && wave == 0) ln_mr[i * 16 + fr][0] = x0[i];
       }
     }
-    if (fuse_ln) {  // (fold: the partials are published by the reduction barrier below)
+  };
+  if (LN_FRAG && ln_frag && fuse_ln) {
+    frag_stats();
+    {
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
@@ -208,12 +238,14 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
           t2 += lnp2[w][i * 16 + fr];
         }
         const float dm = t / (float)K;
-        ln_mean[i] = x0[i] + dm;
+        float v0[8];
+        unpack_bf16(x0raw[i], v0);
+        ln_mean[i] = v0[0] + dm;
         const float var = t2 / (float)K - dm * dm;
         ln_rs[i] = 1.f / sqrtf((var > 0.f ? var : 0.f) + p.ln_eps);
       }
     }
-  } else if (fuse_ln || fold) {
+  } else if ((fuse_ln || fold) && !(LN_FRAG && ln_frag)) {
     const int t = threadIdx.x & 15;
     for (int rr = threadIdx.x >> 4; rr < BM; rr += 64 * SK_WAVES / 16) {
       const int64_t row = m0 + rr < M ? m0 + rr : M - 1;
@@ -287,6 +319,11 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
     if (base >= nks) break;
     load_steps(base);
   }
+#if defined(ICAP_SKABL) && ICAP_SKABL == 1
+  // (ablation build only: no statistics pass; the outputs are wrong)
+#else
+  if (LN_FRAG && ln_frag && !fuse_ln) frag_stats();  // folded: one pass, after the MFMAs are issued
+#endif
   // round 1: waves [HALF, 2 HALF) park their partials, waves [0, HALF) add them; round 2: the HALF sums -> LDS
   auto park = [&](float* dst) {
 #pragma unroll
@@ -318,7 +355,11 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
     const float4 v = *reinterpret_cast<const float4*>(&red[w][er * RLD + ec]);
     x[0] += v.x; x[1] += v.y; x[2] += v.z; x[3] += v.w;
   }
+#if defined(ICAP_SKABL) && ICAP_SKABL == 2
+  if (false) {  // (ablation build only: no folded epilogue; the outputs are wrong)
+#else
   if (fold) {  // rstd (acc - mean wsum); the host passed bias = b + W . beta
+#endif
     float mean, rs;
     if (ln_frag) {  // the wave partials in wave order (the order of the LN-fused form above)
       float t = 0.f, t2 = 0.f;
@@ -336,7 +377,7 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
       rs = ln_mr[er][1];
     }
 #pragma unroll
-    for (int e = 0; e < 4; ++e) x[e] = ecol + e < N ? rs * (x[e] - mean * p.ln_wsum[ecol + e]) : x[e];
+    for (int e = 0; e < 4; ++e) x[e] = ecol + e < N ? rs * (x[e] - mean * wsum4[e]) : x[e];
   }
   // two call sites rather than a selected pointer (a pointer select on a local puts it in scratch)
   if (use_pre) epiw<TC, 4>(p, erow, ecol, x, bias4, ecol + 4 <= N, seed, drop_thresh, inv_keep, &pre);

@@ -61,12 +61,18 @@ def main():
 
     wb = lambda w: w.numel() * 2  # noqa: E731
     case("qkv   128x2304x768  ln+bias", lambda: ops.gemm(x, w_attn, qkv, bias=b3, M=B, ln=ln), wb(w_attn))
+    wsa = w_attn.float().sum(1)
+    case("qkv   128x2304x768  fold+bias", lambda: ops.gemm(x, w_attn, qkv, bias=b3, M=B, ln_fold=(wsa, 1e-5)),
+         wb(w_attn))
     case("qkv   128x2304x768  bias", lambda: ops.gemm(x, w_attn, qkv, bias=b3, M=B), wb(w_attn))
     case("qkv   128x2304x768  plain", lambda: ops.gemm(x, w_attn, qkv, M=B), wb(w_attn))
     case("proj  128x768x768   bias+resid", lambda: ops.gemm(o, w_proj, out1, bias=b1, resid=x, M=B), wb(w_proj))
     case("proj  128x768x768   plain", lambda: ops.gemm(o, w_proj, out1, M=B), wb(w_proj))
     case("fc    128x3072x768  ln+bias+gelu",
          lambda: ops.gemm(h1, w_fc, out4, bias=b4, act=L.ACT_GELU_NEW, M=B, ln=ln), wb(w_fc))
+    wsf = w_fc.float().sum(1)
+    case("fc    128x3072x768  fold+bias+gelu",
+         lambda: ops.gemm(h1, w_fc, out4, bias=b4, act=L.ACT_GELU_NEW, M=B, ln_fold=(wsf, 1e-5)), wb(w_fc))
     case("fc    128x3072x768  plain", lambda: ops.gemm(h1, w_fc, out4, M=B), wb(w_fc))
     case("mp    128x768x3072  bias+resid", lambda: ops.gemm(f, w_mp, out1, bias=b1, resid=h1, M=B), wb(w_mp))
     case("mp    128x768x3072  plain", lambda: ops.gemm(f, w_mp, out1, M=B), wb(w_mp))
@@ -81,8 +87,8 @@ def main():
     wpe = r(1024, D)
     case("greedy_next 128x50257", lambda: ops.greedy_next(logits, V, 50256, fin, toks, 3, wte, wpe, 70, D, x),
          B * Vp * 2)
-    per_token = sum(us for n, us, _ in rows if n.startswith(("qkv   128x2304x768  ln", "proj  128x768x768   bias",
-                                                               "fc    128x3072x768  ln", "mp    128x768x3072  bias",
+    per_token = sum(us for n, us, _ in rows if n.startswith(("qkv   128x2304x768  fold", "proj  128x768x768   bias",
+                                                               "fc    128x3072x768  fold", "mp    128x768x3072  bias",
                                                                "attn_decode pos=40")))
     head = sum(us for n, us, _ in rows if n.startswith(("ln_f", "lm_head", "greedy_next")))
     print(f"estimated token: 12 x {per_token:.1f} + head {head:.1f} = {12 * per_token + head:.1f} us")
