@@ -613,8 +613,10 @@ static int roles_pick(const icap_gemm_args& p, int64_t m_plan, int64_t nk, int64
     if (nk > 96 || t * 5 < cus * 3) return 0;
     return (t <= cus || (nk >= 32 && 2 * t >= 3 * cus && t <= 2 * cus)) ? 27 : 0;
   }
+  // (one row tile — the greedy decode's LM head, 128 x 50304 — stays on the double-buffered tile loop below: 20.4
+  // vs 21.9 us, profiles/r06_lmhead_dx_ab.txt)
   const int64_t t = ((m_plan + 127) / 128) * ((p.N + 255) / 256);
-  return (t <= cus && t * 5 >= cus * 3) ? 26 : 0;
+  return (m_plan > 128 && t <= cus && t * 5 >= cus * 3) ? 26 : 0;
 }
 
 static int gemm_plan(const icap_gemm_args& p, GemmPlan& pl) {

@@ -187,7 +187,8 @@ __global__ __launch_bounds__(1024) void ln_param_reduce(int nblk, int D, const f
   const int which = blockIdx.y;
   float a = 0.f;
   if (c < D) {
-#pragma unroll 4
+    // the 16 row loads of a thread (nblk <= 256: LN_BWD_BLOCKS) issued together, then added in row order
+#pragma unroll 16
     for (int i = ty; i < nblk; i += 16) a += partial[(int64_t)i * 2 * D + which * D + c];
   }
   red[ty][tx] = a;
