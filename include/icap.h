@@ -120,7 +120,7 @@ typedef struct {
   /*     unsplit — same use; 8 / 9 / 10 = the split-role ring kernel (4 or 8 MFMA waves + 4 LDS-DMA waves,    */
   /*     one block per CU: csrc/gemm_tile.h ROLES) on 128 x 256 (variant 26) / 96 x 128 (variant 27) /          */
   /*     192 x 256 (variant 28) tiles for bf16 row-major launches without ln_gamma (9: no LayerNorm consumer),  */
-  /*     unsplit unless split_k > 1 is given (26 / 27: fp32 slabs + the reduce pass, as the tile kernels, no    */
+  /*     unsplit unless split_k > 1 is given (not 28: fp32 slabs + the reduce pass, as the tile kernels, no     */
   /*     LayerNorm hand-off) — same use; 11 = the K-outer split-role kernel (variant 31, 128 x 128 tiles) for bf16 */
   /*     trans_ab launches, K split over slabs by its own rule unless split_k is given — same use; 12 = the     */
   /*     split-role ring on 160 x 128 tiles (variant 32, no LayerNorm consumer) — same use.                     */
