@@ -319,11 +319,7 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
     if (base >= nks) break;
     load_steps(base);
   }
-#if defined(ICAP_SKABL) && ICAP_SKABL == 1
-  // (ablation build only: no statistics pass; the outputs are wrong)
-#else
   if (LN_FRAG && ln_frag && !fuse_ln) frag_stats();  // folded: one pass, after the MFMAs are issued
-#endif
   // round 1: waves [HALF, 2 HALF) park their partials, waves [0, HALF) add them; round 2: the HALF sums -> LDS
   auto park = [&](float* dst) {
 #pragma unroll
@@ -355,11 +351,7 @@ __global__ __launch_bounds__(64 * SK_WAVES) void gemm_skinny_kernel(icap_gemm_ar
     const float4 v = *reinterpret_cast<const float4*>(&red[w][er * RLD + ec]);
     x[0] += v.x; x[1] += v.y; x[2] += v.z; x[3] += v.w;
   }
-#if defined(ICAP_SKABL) && ICAP_SKABL == 2
-  if (false) {  // (ablation build only: no folded epilogue; the outputs are wrong)
-#else
   if (fold) {  // rstd (acc - mean wsum); the host passed bias = b + W . beta
-#endif
     float mean, rs;
     if (ln_frag) {  // the wave partials in wave order (the order of the LN-fused form above)
       float t = 0.f, t2 = 0.f;
