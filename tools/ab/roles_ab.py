@@ -89,7 +89,7 @@ def main():
     skew = len(sys.argv) > 1 and sys.argv[1] == "skew"
     g = torch.Generator(device="cpu").manual_seed(0)
     forms = [("auto", {}, {}), ("r256", {}, dict(roles=256)), ("r96", {}, dict(roles=96)),
-             ("r192", {}, dict(roles=192)), ("r160", {}, dict(roles=160))]
+             ("r192", {}, dict(roles=192)), ("r160", {}, dict(roles=160)), ("g8p256", {}, dict(g8p=256))]
     if skew:
         forms += [("r256s", {"ICAP_ROLES_SKEW": "1"}, dict(roles=256)), ("r96s", {"ICAP_ROLES_SKEW": "1"},
                                                                          dict(roles=96))]
