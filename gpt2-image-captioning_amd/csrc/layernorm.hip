@@ -535,8 +535,58 @@ extern "C" int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const 
                        gamma, mean, rstd, (const float*)dy, lddy, (const float*)dres, lddres, (float*)dx,
                        lddx, (float*)dx_drop, thr, inv_keep, seed, seed_ptr, offset, partial, dy_rowmap, rows_dev);
   int rc = check_launch("icap_layernorm_bwd");
-  if (rc != ICAP_OK || !want_params) return rc;
+  if (rc != ICAP_OK || !want_params || (param_overwrite & 2)) return rc;  // (bit 1: the caller batches the reduce)
   hipLaunchKernelGGL(ln_param_reduce, dim3((unsigned)((D + 63) / 64), 2), dim3(1024), 0, s, nb, (int)D, partial,
-                     dgamma, dbeta, param_overwrite ? 0 : 1);
+                     dgamma, dbeta, (param_overwrite & 1) ? 0 : 1);
   return check_launch("icap_layernorm_bwd(reduce)");
+}
+
+// The deferred parameter reduces of several LayerNorm backwards in one launch: blockIdx.z = item, the same
+// per-block sums as ln_param_reduce (so the stored dgamma / dbeta are bitwise the unbatched ones).
+struct LnParamBatch {
+  icap_ln_param_item it[ICAP_LN_PARAM_BATCH_MAX];
+  int nblk[ICAP_LN_PARAM_BATCH_MAX];
+};
+__global__ __launch_bounds__(1024) void ln_param_reduce_batch(LnParamBatch b) {
+  const icap_ln_param_item& it = b.it[blockIdx.z];
+  const int D = (int)it.D;
+  if ((int)blockIdx.x * 64 >= D) return;  // (items narrower than the widest)
+  __shared__ float red[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int which = blockIdx.y;
+  const float* partial = reinterpret_cast<const float*>(it.workspace);
+  float a = 0.f;
+  if (c < D) {
+#pragma unroll 16
+    for (int i = ty; i < b.nblk[blockIdx.z]; i += 16) a += partial[(int64_t)i * 2 * D + which * D + c];
+  }
+  red[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && c < D) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][tx];
+    float* dst = which ? it.dbeta : it.dgamma;
+    if (dst) dst[c] = it.overwrite ? s : dst[c] + s;
+  }
+}
+
+extern "C" int icap_ln_param_reduce_batch(int32_t n, const icap_ln_param_item* items, void* stream) {
+  ICAP_REQUIRE(n >= 0 && n <= ICAP_LN_PARAM_BATCH_MAX && (n == 0 || items),
+               "icap_ln_param_reduce_batch: 0 ... ICAP_LN_PARAM_BATCH_MAX items");
+  if (n == 0) return ICAP_OK;
+  LnParamBatch b{};
+  int64_t dmax = 0;
+  for (int i = 0; i < n; ++i) {
+    const icap_ln_param_item& it = items[i];
+    ICAP_REQUIRE(it.workspace && it.rows > 0 && it.D > 0 && it.D % 4 == 0 && it.D <= LN8_DMAX,
+                 "icap_ln_param_reduce_batch: workspace, rows > 0 and D (a multiple of 4, <= 1536) per item");
+    b.it[i] = it;
+    b.nblk[i] = ln_blocks(it.rows, LN_BWD_BLOCKS);
+    if (it.D > dmax) dmax = it.D;
+  }
+  hipLaunchKernelGGL(ln_param_reduce_batch, dim3((unsigned)((dmax + 63) / 64), 2, (unsigned)n), dim3(1024), 0,
+                     reinterpret_cast<hipStream_t>(stream), b);
+  return check_launch("icap_ln_param_reduce_batch");
 }

@@ -55,6 +55,10 @@ class GemmArgs(C.Structure):
     ]
 
 
+class LnParamItem(C.Structure):
+    _fields_ = [("workspace", vp), ("rows", i64), ("D", i64), ("dgamma", vp), ("dbeta", vp), ("overwrite", i32)]
+
+
 class TransposeItem(C.Structure):
     _fields_ = [("src", vp), ("lds", i64), ("dst", vp), ("ldd", i64), ("rows", i64), ("cols", i64)]
 
@@ -123,6 +127,7 @@ SIGNATURES = {
     "icap_layernorm_bwd_workspace_bytes": (sz, [i64, i64]),
     "icap_layernorm_bwd": (C.c_int, [i32, i64, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, vp,
                                      f32, u64, u64, vp, vp, vp, vp, vp, vp, i32, vp]),
+    "icap_ln_param_reduce_batch": (C.c_int, [i32, C.POINTER(LnParamItem), vp]),
     "icap_attention_fwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_bwd": (C.c_int, [C.POINTER(AttnArgs), vp]),
     "icap_attention_decode": (C.c_int, [i32, i32, i32, i32, i32, vp, i64, vp, i64, f32, vp]),

@@ -35,6 +35,10 @@ def _kout_ok(t: Tensor) -> bool:
     return t.data_ptr() % 16 == 0 and t.stride(0) % 8 == 0 and t.stride(-1) == 1
 
 
+# a mapper layer's two LayerNorm parameter reduces in one launch at the layer's end (ops.ln_param_reduce_batch;
+# bitwise the per-call reduces). Read when the backward is built, so a captured graph keeps the setting.
+LN_PARAM_BATCH = True
+
 class DWHelper:
     """dW[N,K] += dY[M,N]^T . X[M,K] on the MFMA GEMM. bf16: one K-outer product (trans_ab) straight from dY
     and X; fp32 (parity mode): both operands are transposed into K(=M)-contiguous scratch (M padded to 64 with
@@ -53,6 +57,10 @@ class DWHelper:
         self.ones = torch.ones((max(max_rows, 1), 8), dtype=dtype, device=device) if dtype == torch.bfloat16 else None
         self.ln_ws = torch.empty(max(ops.layernorm_bwd_workspace(ln_rows, ln_D), 16), dtype=torch.uint8,
                                  device=device)
+        # a second one: a mapper layer's two LayerNorm backwards leave their dgamma / dbeta partials side by side and
+        # reduce them in one launch at the layer's end (ops.ln_param_reduce_batch)
+        self.ln_ws2 = torch.empty_like(self.ln_ws)
+        self.ln_rows, self.ln_D = ln_rows, ln_D
 
     def _t(self, buf: Tensor, src: Tensor, M: int, N: int, Mp: int) -> Tensor:
         dst = buf[: N * Mp].view(N, Mp)
@@ -538,7 +546,7 @@ class TransformerMapperCore:
             d1 = dr.d1(l)
             ops.layernorm_bwd(ws.h1[l], w.n2_g, ws.mean2[l], ws.rstd2[l], ws.da, ws.g_rm[l], dres=r,
                               dx_drop=ws.g_mm[l] if d1.p > 0 else None, drop=d1, dgamma=gl.n2_g, dbeta=gl.n2_b,
-                              workspace=dwh.ln_ws, param_accumulate=acc)
+                              workspace=dwh.ln_ws2, param_accumulate=acc, defer_params=LN_PARAM_BATCH)
             dy2 = ws.g_mm[l] if d1.p > 0 else ws.g_rm[l]
             wgrad(dy2, ws.o[l], gl.out_w, gl.out_b)
             ops.gemm(dy2, w.out_wt, ws.do)
@@ -550,7 +558,10 @@ class TransformerMapperCore:
             out = ws.g_r[l - 1] if l > 0 else ws.dres  # d(layer input): the next layer's residual grad / the head's
             ops.layernorm_bwd(ws.x[l], w.n1_g, ws.mean1[l], ws.rstd1[l], ws.da, out, dres=ws.g_rm[l],
                               dx_drop=ws.g_m[l - 1] if (l > 0 and nxt.p > 0) else None, drop=nxt, dgamma=gl.n1_g,
-                              dbeta=gl.n1_b, workspace=dwh.ln_ws, param_accumulate=acc)
+                              dbeta=gl.n1_b, workspace=dwh.ln_ws, param_accumulate=acc, defer_params=LN_PARAM_BATCH)
+            if LN_PARAM_BATCH:
+                ops.ln_param_reduce_batch([(dwh.ln_ws2, M, D, gl.n2_g, gl.n2_b, acc),
+                                           (dwh.ln_ws, M, D, gl.n1_g, gl.n1_b, acc)])
             st.r = out
             flush_dw()
             flush_db()

@@ -406,16 +406,32 @@ def layernorm_bwd(x: Tensor, gamma: Tensor, mean: Tensor, rstd: Tensor, dy: Tens
                   dgamma: Optional[Tensor] = None, dbeta: Optional[Tensor] = None,
                   workspace: Optional[Tensor] = None, rows: Optional[int] = None,
                   dy_rowmap: Optional[Tensor] = None, rows_dev: Optional[Tensor] = None,
-                  param_accumulate: bool = True) -> Tensor:
+                  param_accumulate: bool = True, defer_params: bool = False) -> Tensor:
     """dy_rowmap: int32 [rows]; dy of row r is dy row dy_rowmap[r] (zero when < 0). rows_dev: as layernorm_fwd.
-    param_accumulate: dgamma / dbeta += (True) or = (False: the first micro-batch of a cycle)."""
+    param_accumulate: dgamma / dbeta += (True) or = (False: the first micro-batch of a cycle).
+    defer_params: leave the dgamma / dbeta partials in `workspace` for ln_param_reduce_batch (no reduce launch)."""
     rows = _rows(x) if rows is None else rows
     D = gamma.shape[0]
     call("icap_layernorm_bwd", dtype_code(x.dtype), rows, D, x.data_ptr(), _ld(x), gamma.data_ptr(),
          mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), _ld(dy), _p(dres), _ld(dres) if dres is not None else 0,
          dx.data_ptr(), _ld(dx), _p(dx_drop), drop.p, drop.seed, drop.offset, drop.ptr, _p(dgamma), _p(dbeta),
-         _p(workspace), _p(dy_rowmap), _p(rows_dev), 0 if param_accumulate else 1, _stream())
+         _p(workspace), _p(dy_rowmap), _p(rows_dev), (0 if param_accumulate else 1) | (2 if defer_params else 0),
+         _stream())
     return dx
+
+
+def ln_param_reduce_batch(items) -> None:
+    """The deferred dgamma / dbeta reduces of several layernorm_bwd(..., defer_params=True) calls in one launch
+    (include/icap.h icap_ln_param_reduce_batch): items = [(workspace, rows, D, dgamma, dbeta, accumulate), ...];
+    bitwise the per-call reduce."""
+    n = len(items)
+    if n == 0:
+        return
+    arr = (L.LnParamItem * n)()
+    for i, (ws, rows, D, dg, db, acc) in enumerate(items):
+        arr[i].workspace, arr[i].rows, arr[i].D = ws.data_ptr(), rows, D
+        arr[i].dgamma, arr[i].dbeta, arr[i].overwrite = _p(dg), _p(db), 0 if acc else 1
+    call("icap_ln_param_reduce_batch", n, arr, _stream())
 
 
 def _attn_args(qkv: Tensor, B: int, S: int, H: int, hd: int, rsb: int, rss: int, scale: float, causal: bool,

@@ -205,9 +205,12 @@ int icap_layernorm_fwd(int32_t dtype, int64_t rows, int64_t D, const void* x, in
                        void* stream);
 /* dx = LN'(x)^T dy [+ dres];  optional dx_drop = dx * dropmask(p,seed,offset)  */
 /* (the residual-dropout backward of the producing layer, fused);             */
-/* optional dgamma/dbeta (fp32 [D]: += by default, = when param_overwrite != 0 */
-/* — the first micro-batch of a cycle overwrites instead of zeroing first) via a */
-/* caller workspace of icap_layernorm_bwd_workspace_bytes(rows, D) bytes.      */
+/* optional dgamma/dbeta (fp32 [D]: += by default, = when param_overwrite bit 0 */
+/* is set — the first micro-batch of a cycle overwrites instead of zeroing     */
+/* first) via a caller workspace of icap_layernorm_bwd_workspace_bytes(rows, D) */
+/* bytes. param_overwrite bit 1: leave the per-block partials in the workspace */
+/* and skip their reduce — the caller reduces them with                        */
+/* icap_ln_param_reduce_batch (several LayerNorms in one launch).              */
 /* dy_rowmap (optional int32 [rows]): dy of row r is dy row dy_rowmap[r], or 0 */
 /* when it is < 0 (scatters the LM-head target-row gradient back).             */
 /* rows_dev: as in icap_layernorm_fwd.                                         */
@@ -219,6 +222,14 @@ int icap_layernorm_bwd(int32_t dtype, int64_t rows, int64_t D, const void* x, in
                        uint64_t offset, const uint64_t* seed_ptr, float* dgamma, float* dbeta,
                        void* workspace, const int32_t* dy_rowmap, const int32_t* rows_dev,
                        int32_t param_overwrite, void* stream);
+/* The deferred dgamma / dbeta reduces (param_overwrite bit 1 above) of n <= ICAP_LN_PARAM_BATCH_MAX LayerNorm    */
+/* backwards in one launch; item: that call's workspace, rows, D, dgamma, dbeta and overwrite (bit 0). Bitwise   */
+/* the per-call reduce.                                                                                         */
+#define ICAP_LN_PARAM_BATCH_MAX 16
+typedef struct icap_ln_param_item {
+  const void* workspace; int64_t rows; int64_t D; float* dgamma; float* dbeta; int32_t overwrite;
+} icap_ln_param_item;
+int icap_ln_param_reduce_batch(int32_t n, const icap_ln_param_item* items, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Multi-head softmax attention over a fused QKV activation.                  */

@@ -97,6 +97,12 @@ def accesses(name, args):
                 ("dbeta", db, D * 4), ("dy_rowmap", dymap, rows * 4), ("rows_dev", rdev, 4)]
         if dg or db:
             out.append(("ws", ws, ops.layernorm_bwd_workspace(rows, D)))
+    elif name == "icap_ln_param_reduce_batch":
+        n, arr = a[0], a[1]
+        for i in range(n):
+            it = arr[i]
+            out += [(f"ws{i}", it.workspace, ops.layernorm_bwd_workspace(it.rows, it.D)),
+                    (f"dgamma{i}", it.dgamma, it.D * 4), (f"dbeta{i}", it.dbeta, it.D * 4)]
     elif name == "icap_gpt2_embed":
         dt, B, P, L, D, pre, pbs, wte, wpe, ids, x, _p, _sd, _o, sp, so, sl, _s = a
         es = ES[dt]

@@ -37,7 +37,7 @@ _SCALARS = {"int": C.c_int, "int32_t": C.c_int32, "int64_t": C.c_int64, "uint64_
             "float": C.c_float}
 _STRUCTS = {"icap_gemm_args": _lib.GemmArgs, "icap_attn_args": _lib.AttnArgs, "icap_adamw_args": _lib.AdamWArgs,
             "icap_beam_args": _lib.BeamArgs, "icap_transpose_item": _lib.TransposeItem,
-            "icap_colsum_item": _lib.ColsumItem}
+            "icap_colsum_item": _lib.ColsumItem, "icap_ln_param_item": _lib.LnParamItem}
 
 
 def header_prototypes():
@@ -126,7 +126,7 @@ def test_version_and_workspace_queries():
 
 
 @pytest.mark.parametrize("struct,cname", [(_lib.GemmArgs, "icap_gemm_args"), (_lib.AttnArgs, "icap_attn_args"),
-                                          (_lib.AdamWArgs, "icap_adamw_args")])
+                                          (_lib.AdamWArgs, "icap_adamw_args"), (_lib.LnParamItem, "icap_ln_param_item")])
 def test_struct_layout_matches_header(struct, cname):
     fields = [f for f, _ in struct._fields_]
     prog = ["#include <stdio.h>", "#include <stddef.h>", '#include "icap.h"', "int main(void){",

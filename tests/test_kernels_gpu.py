@@ -647,3 +647,37 @@ def test_transpose_batch_equals_single(dev):
     torch.cuda.synchronize()
     for s_, o in zip(srcs, outs):
         assert torch.equal(o, s_.t())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_param_reduce_batch_bitwise(dev, dtype):
+    """The mapper's deferred dgamma / dbeta reduces (layernorm_bwd(defer_params=True) + one ln_param_reduce_batch per
+    layer, include/icap.h icap_ln_param_reduce_batch) store bitwise what the per-call reduce stores, in both the
+    accumulate and the overwrite form; the dx outputs are untouched by the deferral."""
+    rows, D = 3200, 768
+    xs = [rnd((rows, D), dev, dtype, seed=60 + i) for i in range(2)]
+    dys = [rnd((rows, D), dev, dtype, seed=70 + i) for i in range(2)]
+    gms = [rnd((D,), dev, scale=0.5, seed=80 + i) + 1 for i in range(2)]
+    stats = []
+    for x, g in zip(xs, gms):
+        mean, rstd = torch.empty(rows, device=dev), torch.empty(rows, device=dev)
+        ops.layernorm_fwd(x, g, torch.zeros(D, device=dev), 1e-5, torch.empty_like(x), mean, rstd)
+        stats.append((mean, rstd))
+    wsz = ops.layernorm_bwd_workspace(rows, D)
+    for acc in (True, False):
+        res = {}
+        for mode in ("call", "batch"):
+            wss = [torch.empty(wsz, dtype=torch.uint8, device=dev) for _ in range(2)]
+            dg = [rnd((D,), dev, seed=90 + i) for i in range(2)]
+            db = [rnd((D,), dev, seed=95 + i) for i in range(2)]
+            dxs = [torch.empty_like(xs[0]) for _ in range(2)]
+            for i in range(2):
+                ops.layernorm_bwd(xs[i], gms[i], stats[i][0], stats[i][1], dys[i], dxs[i], dgamma=dg[i], dbeta=db[i],
+                                  workspace=wss[i], param_accumulate=acc, defer_params=(mode == "batch"))
+            if mode == "batch":
+                ops.ln_param_reduce_batch([(wss[i], rows, D, dg[i], db[i], acc) for i in range(2)])
+            res[mode] = (dg, db, dxs)
+        torch.cuda.synchronize()
+        for a, b in zip(res["call"], res["batch"]):
+            for u, v in zip(a, b):
+                assert torch.equal(u, v)
